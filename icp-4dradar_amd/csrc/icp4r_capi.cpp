@@ -1,0 +1,570 @@
+// icp4r_capi.cpp — the C ABI (include/icp4r/icp4r.h) over the HIP kernels.
+//
+// Host-side mirror of the PCL boundary the reference calls (src/iterative_closest_point.cpp:510-521):
+// a context owns one device's stream and grow-only device buffers; every entry validates its
+// arguments, launches, and reports a status plus a thread-local message (icp4r_last_error).  There
+// is no CPU fallback: if the device path cannot run, the call fails with ICP4R_E_HIP.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "icp4r/icp4r.h"
+#include "icp4r_internal.hpp"
+
+using namespace icp4r;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                 \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess) return fail(ICP4R_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                          __FILE__, __LINE__);                                        \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct EventPair {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
+struct icp4r_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // staging for the host-buffer entry points
+    DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, idx, d2, T;
+    // batch workspace
+    DevBuf X, nn_d2, nn_idx, state;
+    std::vector<EventPair> nn_events, batch_events;
+    size_t nn_used = 0, batch_used = 0;
+};
+
+namespace {
+
+struct Plan {
+    int q;
+    bool packed;  // v_pk_* FP32 sweep (two queries per register pair)
+    int splits;
+    int64_t blocks;
+};
+
+// Geometry of the NN sweep: Q queries per lane (fewer when pairs are few, so the grid still fills
+// 256 CUs), then split the target range until there are >= 2048 workgroups (8 per CU) while each
+// split keeps >= 256 targets.  Batches of 8k-point pairs end up at Q = 16, one split.
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
+    const int64_t want = 2048;
+    Plan pl;
+    pl.q = kMaxQ;
+    // tuning override (tools/tune_sweep.py): ICP4R_NN_Q=1|2|4|8|16 caps the queries per lane
+    if (const char* e = getenv("ICP4R_NN_Q")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) pl.q = v;
+    }
+    auto qblocks = [&](int q) { return (int64_t)((max_n + kNNWG * q - 1) / (kNNWG * q)); };
+    while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) < want) pl.q /= 2;
+    pl.splits = 1;
+    while ((int64_t)npairs * qblocks(pl.q) * pl.splits < want && max_m / (pl.splits * 2) >= 256 && pl.splits < 64)
+        pl.splits *= 2;
+    pl.blocks = (int64_t)npairs * qblocks(pl.q) * pl.splits;
+    pl.packed = nn_mode != ICP4R_NN_BRUTE && pl.q >= 2;
+    return pl;
+}
+
+float max_d2_threshold(double max_dist) {
+    const double md2 = max_dist * max_dist;
+    if (!(md2 < (double)FLT_MAX)) return FLT_MAX;  // also +inf / NaN: keep every finite d2
+    float f = (float)md2;
+    if ((double)f > md2) f = nextafterf(f, 0.0f);
+    return f;
+}
+
+int make_kparams(const icp4r_params* p, KParams* kp) {
+    icp4r_params d;
+    if (!p) {
+        icp4r_params_default(&d);
+        p = &d;
+    }
+    if (p->max_iterations < 0) return fail(ICP4R_E_INVALID, "max_iterations must be >= 0");
+    if (p->numerics != ICP4R_NUMERICS_PCL && p->numerics != ICP4R_NUMERICS_F64)
+        return fail(ICP4R_E_INVALID, "unknown numerics mode %d", p->numerics);
+    if (p->nn_mode != ICP4R_NN_AUTO && p->nn_mode != ICP4R_NN_BRUTE && p->nn_mode != ICP4R_NN_BRUTE_PACKED)
+        return fail(ICP4R_E_INVALID, "unknown nn_mode %d", p->nn_mode);
+    if (!(p->huber_delta > 0)) return fail(ICP4R_E_INVALID, "huber_delta must be > 0 (+inf disables)");
+    memset(kp, 0, sizeof(*kp));
+    kp->conv.max_iterations = p->max_iterations;
+    kp->conv.max_similar = p->max_iterations_similar_transforms;
+    kp->conv.rot_thr = p->transformation_rotation_epsilon > 0 ? p->transformation_rotation_epsilon
+                                                              : 1.0 - p->transformation_epsilon;
+    kp->conv.trans_thr = p->transformation_epsilon;
+    kp->conv.abs_mse = p->mse_threshold_absolute;
+    kp->conv.rel_mse = p->euclidean_fitness_epsilon;
+    kp->min_corr = p->min_correspondences;
+    kp->numerics = p->numerics;
+    kp->compute_fitness = p->compute_fitness;
+    kp->max_d2 = max_d2_threshold(p->max_correspondence_distance);
+    kp->huber_delta = p->huber_delta;
+    kp->fit_max_range = p->fitness_max_range;
+    return ICP4R_OK;
+}
+
+int check_cloud(const float* c, int32_t n, int32_t stride, const char* what) {
+    if (n < 0) return fail(ICP4R_E_INVALID, "%s: negative point count", what);
+    if (n > 0 && !c) return fail(ICP4R_E_INVALID, "%s: NULL cloud with %d points", what, n);
+    if (stride < 12 || stride % 4) return fail(ICP4R_E_INVALID, "%s: stride %d bytes (need >= 12, multiple of 4)", what, stride);
+    return ICP4R_OK;
+}
+
+void pack_host(const float* c, int32_t n, int32_t stride_bytes, std::vector<float>& out) {
+    out.resize((size_t)(n > 0 ? n : 1) * 4);
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c);
+    for (int32_t i = 0; i < n; ++i) {
+        const float* p = reinterpret_cast<const float*>(b + (size_t)i * stride_bytes);
+        out[4 * (size_t)i + 0] = p[0];
+        out[4 * (size_t)i + 1] = p[1];
+        out[4 * (size_t)i + 2] = p[2];
+        out[4 * (size_t)i + 3] = stride_bytes >= 16 ? p[3] : 0.0f;
+    }
+}
+
+int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
+    if (used == v.size()) {
+        EventPair e;
+        HIP_TRY(hipEventCreate(&e.start));
+        HIP_TRY(hipEventCreate(&e.stop));
+        v.push_back(e);
+    }
+    *out = &v[used++];
+    return ICP4R_OK;
+}
+
+// The whole registration of a device-resident batch as one stream-ordered launch sequence.
+int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m, int max_iterations,
+              int nn_mode, hipStream_t st) {
+    if (npairs <= 0) return ICP4R_OK;
+    const Plan pl = make_plan(npairs, max_n > 0 ? max_n : 1, max_m, nn_mode);
+    const int64_t x_stride = ((max_n > 0 ? max_n : 1) + 3) & ~3;
+    const int64_t slots = (int64_t)npairs * x_stride;
+    HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
+    HIP_TRY(ctx->nn_d2.ensure((size_t)slots * pl.splits * sizeof(float)));
+    HIP_TRY(ctx->nn_idx.ensure((size_t)slots * pl.splits * sizeof(int32_t)));
+    HIP_TRY(ctx->state.ensure((size_t)npairs * sizeof(PairState)));
+    WorkArgs w;
+    w.X = static_cast<float4*>(ctx->X.p);
+    w.nn_d2 = static_cast<float*>(ctx->nn_d2.p);
+    w.nn_idx = static_cast<int32_t*>(ctx->nn_idx.p);
+    w.state = static_cast<PairState*>(ctx->state.p);
+    w.x_stride = x_stride;
+    w.slot_stride = slots;
+    w.splits = pl.splits;
+    EventPair* be;
+    int rc;
+    if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
+    HIP_TRY(hipEventRecord(be->start, st));
+    HIP_TRY(launch_init(a, w, npairs, st));
+    // PCL's do { ... } while (!converged): at least one iteration even for max_iterations == 0.
+    const int iters = max_iterations > 0 ? max_iterations : 1;
+    for (int it = 0; it < iters; ++it) {
+        EventPair* ne;
+        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
+        HIP_TRY(hipEventRecord(ne->start, st));
+        HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n > 0 ? max_n : 1, 0, st));
+        HIP_TRY(hipEventRecord(ne->stop, st));
+        HIP_TRY(launch_update(a, w, npairs, st));
+    }
+    if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
+    if (a.kp.compute_fitness) {
+        EventPair* ne;
+        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
+        HIP_TRY(hipEventRecord(ne->start, st));
+        HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n > 0 ? max_n : 1, 1, st));
+        HIP_TRY(hipEventRecord(ne->stop, st));
+    }
+    HIP_TRY(launch_finish(a, w, npairs, st));
+    HIP_TRY(hipEventRecord(be->stop, st));
+    return ICP4R_OK;
+}
+
+int events_avg(std::vector<EventPair>& v, size_t used, double* avg_ms) {
+    double tot = 0.0;
+    for (size_t i = 0; i < used; ++i) {
+        HIP_TRY(hipEventSynchronize(v[i].stop));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, v[i].start, v[i].stop));
+        tot += ms;
+    }
+    *avg_ms = used ? tot / (double)used : 0.0;
+    return ICP4R_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* icp4r_version(void) { return "icp4r 0.1.0 (gfx950, HIP)"; }
+int icp4r_abi_version(void) { return ICP4R_ABI_VERSION; }
+const char* icp4r_last_error(void) { return g_last_error.c_str(); }
+
+void icp4r_params_default(icp4r_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->max_iterations = 10;                       // Registration::max_iterations_
+    p->min_correspondences = 3;                   // Registration::min_number_correspondences_
+    p->max_correspondence_distance = sqrt(DBL_MAX);  // Registration::corr_dist_threshold_
+    p->transformation_epsilon = 0.0;
+    p->transformation_rotation_epsilon = 0.0;
+    p->euclidean_fitness_epsilon = -DBL_MAX;
+    p->mse_threshold_absolute = 1e-12;            // DefaultConvergenceCriteria
+    p->max_iterations_similar_transforms = 0;
+    p->numerics = ICP4R_NUMERICS_PCL;
+    p->nn_mode = ICP4R_NN_AUTO;
+    p->compute_fitness = 1;
+    p->huber_delta = INFINITY;
+    p->fitness_max_range = DBL_MAX;
+}
+
+int icp4r_device_count(int* count) {
+    if (!count) return fail(ICP4R_E_INVALID, "count is NULL");
+    HIP_TRY(hipGetDeviceCount(count));
+    return ICP4R_OK;
+}
+
+int icp4r_create(icp4r_ctx** out, int device) {
+    if (!out) return fail(ICP4R_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(ICP4R_E_INVALID, "device %d out of range (%d devices)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    icp4r_ctx* c = new icp4r_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(ICP4R_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return ICP4R_OK;
+}
+
+int icp4r_destroy(icp4r_ctx* ctx) {
+    if (!ctx) return ICP4R_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
+                      &ctx->aligned, &ctx->results, &ctx->idx, &ctx->d2, &ctx->T, &ctx->X, &ctx->nn_d2,
+                      &ctx->nn_idx, &ctx->state})
+        b->release();
+    for (auto* v : {&ctx->nn_events, &ctx->batch_events})
+        for (auto& ev : *v) {
+            (void)hipEventDestroy(ev.start);
+            (void)hipEventDestroy(ev.stop);
+        }
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return ICP4R_OK;
+}
+
+int icp4r_align(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_bytes, const float* tgt, int32_t m,
+                int32_t tgt_stride_bytes, const float* guess, const icp4r_params* params, icp4r_result* out,
+                float* aligned_out, int32_t out_stride_bytes) {
+    if (!ctx || !out) return fail(ICP4R_E_INVALID, "ctx/out is NULL");
+    int rc;
+    if ((rc = check_cloud(src, n, src_stride_bytes, "source"))) return rc;
+    if ((rc = check_cloud(tgt, m, tgt_stride_bytes, "target"))) return rc;
+    if (aligned_out && (out_stride_bytes < 12 || out_stride_bytes % 4))
+        return fail(ICP4R_E_INVALID, "aligned_out stride %d bytes", out_stride_bytes);
+    KParams kp;
+    if ((rc = make_kparams(params, &kp))) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> hs, ht;
+    pack_host(src, n, src_stride_bytes, hs);
+    pack_host(tgt, m, tgt_stride_bytes, ht);
+    const int64_t zero64 = 0;
+    HIP_TRY(ctx->src.ensure(hs.size() * sizeof(float)));
+    HIP_TRY(ctx->tgt.ensure(ht.size() * sizeof(float)));
+    HIP_TRY(ctx->src_off.ensure(16));
+    HIP_TRY(ctx->tgt_off.ensure(16));
+    HIP_TRY(ctx->src_n.ensure(16));
+    HIP_TRY(ctx->tgt_n.ensure(16));
+    HIP_TRY(ctx->guess.ensure(16 * sizeof(float)));
+    HIP_TRY(ctx->results.ensure(sizeof(icp4r_result)));
+    HIP_TRY(ctx->aligned.ensure(hs.size() * sizeof(float)));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->src.p, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_n.p, &n, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_n.p, &m, 4, hipMemcpyHostToDevice, st));
+    if (guess) HIP_TRY(hipMemcpyAsync(ctx->guess.p, guess, 16 * sizeof(float), hipMemcpyHostToDevice, st));
+    PairArgs a;
+    a.src = static_cast<const float4*>(ctx->src.p);
+    a.tgt = static_cast<const float4*>(ctx->tgt.p);
+    a.src_off = static_cast<const int64_t*>(ctx->src_off.p);
+    a.tgt_off = static_cast<const int64_t*>(ctx->tgt_off.p);
+    a.src_n = static_cast<const int32_t*>(ctx->src_n.p);
+    a.tgt_n = static_cast<const int32_t*>(ctx->tgt_n.p);
+    a.guess = guess ? static_cast<const float*>(ctx->guess.p) : nullptr;
+    a.aligned = aligned_out ? static_cast<float4*>(ctx->aligned.p) : nullptr;
+    a.results = static_cast<Result*>(ctx->results.p);
+    a.kp = kp;
+    const int iters = params ? params->max_iterations : 10;
+    if ((rc = run_pairs(ctx, a, 1, n, m, iters, params ? params->nn_mode : ICP4R_NN_AUTO, st))) return rc;
+    HIP_TRY(hipMemcpyAsync(out, ctx->results.p, sizeof(icp4r_result), hipMemcpyDeviceToHost, st));
+    std::vector<float> ha;
+    if (aligned_out && n > 0) {
+        ha.resize((size_t)n * 4);
+        HIP_TRY(hipMemcpyAsync(ha.data(), ctx->aligned.p, ha.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (aligned_out && n > 0) {
+        unsigned char* o = reinterpret_cast<unsigned char*>(aligned_out);
+        for (int32_t i = 0; i < n; ++i) {
+            float* q = reinterpret_cast<float*>(o + (size_t)i * out_stride_bytes);
+            q[0] = ha[4 * (size_t)i];
+            q[1] = ha[4 * (size_t)i + 1];
+            q[2] = ha[4 * (size_t)i + 2];
+            if (out_stride_bytes >= 16) q[3] = ha[4 * (size_t)i + 3];
+        }
+    }
+    if (out->status != ICP4R_OK) {
+        const char* what = out->status == ICP4R_E_TOO_FEW_CORR ? "Not enough correspondences found. Relax your threshold parameters."
+                           : out->status == ICP4R_E_EMPTY      ? "No input target dataset was given!"
+                           : out->status == ICP4R_E_NONFINITE  ? "non-finite coordinate in an input cloud"
+                                                               : "registration failed";
+        return fail(out->status, "[icp4r::IterativeClosestPoint::computeTransformation] %s", what);
+    }
+    return ICP4R_OK;
+}
+
+int icp4r_align_batch_device(icp4r_ctx* ctx, const icp4r_batch* b, const icp4r_params* params, icp4r_result* results,
+                             void* hip_stream) {
+    if (!ctx || !b || !results) return fail(ICP4R_E_INVALID, "ctx/batch/results is NULL");
+    if (b->npairs < 0) return fail(ICP4R_E_INVALID, "npairs < 0");
+    if (b->npairs == 0) return ICP4R_OK;
+    if (!b->src || !b->tgt || !b->src_off || !b->src_n || !b->tgt_off || !b->tgt_n)
+        return fail(ICP4R_E_INVALID, "batch has a NULL device array");
+    if (b->max_src_n < 0 || b->max_tgt_n < 0) return fail(ICP4R_E_INVALID, "negative max sizes");
+    KParams kp;
+    int rc;
+    if ((rc = make_kparams(params, &kp))) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    PairArgs a;
+    a.src = reinterpret_cast<const float4*>(b->src);
+    a.tgt = reinterpret_cast<const float4*>(b->tgt);
+    a.src_off = b->src_off;
+    a.src_n = b->src_n;
+    a.tgt_off = b->tgt_off;
+    a.tgt_n = b->tgt_n;
+    a.guess = b->guess;
+    a.aligned = reinterpret_cast<float4*>(b->aligned);
+    a.results = reinterpret_cast<Result*>(results);
+    a.kp = kp;
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    return run_pairs(ctx, a, b->npairs, b->max_src_n, b->max_tgt_n, params ? params->max_iterations : 10,
+                     params ? params->nn_mode : ICP4R_NN_AUTO, st);
+}
+
+int icp4r_align_batch_host(icp4r_ctx* ctx, const float* src, const int64_t* src_off, const int32_t* src_n,
+                           const float* tgt, const int64_t* tgt_off, const int32_t* tgt_n, int32_t npairs,
+                           const float* guess, const icp4r_params* params, icp4r_result* results) {
+    if (!ctx || !results || npairs < 0) return fail(ICP4R_E_INVALID, "bad arguments");
+    if (npairs == 0) return ICP4R_OK;
+    if (!src_off || !src_n || !tgt_off || !tgt_n) return fail(ICP4R_E_INVALID, "NULL offset/count array");
+    int64_t ns = 0, nt = 0;
+    int32_t max_n = 0, max_m = 0;
+    for (int32_t p = 0; p < npairs; ++p) {
+        if (src_n[p] < 0 || tgt_n[p] < 0 || src_off[p] < 0 || tgt_off[p] < 0)
+            return fail(ICP4R_E_INVALID, "pair %d: negative offset/count", p);
+        if (src_off[p] + src_n[p] > ns) ns = src_off[p] + src_n[p];
+        if (tgt_off[p] + tgt_n[p] > nt) nt = tgt_off[p] + tgt_n[p];
+        if (src_n[p] > max_n) max_n = src_n[p];
+        if (tgt_n[p] > max_m) max_m = tgt_n[p];
+    }
+    if ((ns > 0 && !src) || (nt > 0 && !tgt)) return fail(ICP4R_E_INVALID, "NULL cloud data");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(ctx->src.ensure((size_t)(ns > 0 ? ns : 1) * 16));
+    HIP_TRY(ctx->tgt.ensure((size_t)(nt > 0 ? nt : 1) * 16));
+    HIP_TRY(ctx->src_off.ensure((size_t)npairs * 8));
+    HIP_TRY(ctx->tgt_off.ensure((size_t)npairs * 8));
+    HIP_TRY(ctx->src_n.ensure((size_t)npairs * 4));
+    HIP_TRY(ctx->tgt_n.ensure((size_t)npairs * 4));
+    HIP_TRY(ctx->results.ensure((size_t)npairs * sizeof(icp4r_result)));
+    if (guess) HIP_TRY(ctx->guess.ensure((size_t)npairs * 64));
+    if (ns > 0) HIP_TRY(hipMemcpyAsync(ctx->src.p, src, (size_t)ns * 16, hipMemcpyHostToDevice, st));
+    if (nt > 0) HIP_TRY(hipMemcpyAsync(ctx->tgt.p, tgt, (size_t)nt * 16, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, src_off, (size_t)npairs * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, tgt_off, (size_t)npairs * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_n.p, src_n, (size_t)npairs * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_n.p, tgt_n, (size_t)npairs * 4, hipMemcpyHostToDevice, st));
+    if (guess) HIP_TRY(hipMemcpyAsync(ctx->guess.p, guess, (size_t)npairs * 64, hipMemcpyHostToDevice, st));
+    icp4r_batch b;
+    memset(&b, 0, sizeof(b));
+    b.src = static_cast<const float*>(ctx->src.p);
+    b.tgt = static_cast<const float*>(ctx->tgt.p);
+    b.src_off = static_cast<const int64_t*>(ctx->src_off.p);
+    b.tgt_off = static_cast<const int64_t*>(ctx->tgt_off.p);
+    b.src_n = static_cast<const int32_t*>(ctx->src_n.p);
+    b.tgt_n = static_cast<const int32_t*>(ctx->tgt_n.p);
+    b.guess = guess ? static_cast<const float*>(ctx->guess.p) : nullptr;
+    b.npairs = npairs;
+    b.max_src_n = max_n;
+    b.max_tgt_n = max_m;
+    int rc = icp4r_align_batch_device(ctx, &b, params, static_cast<icp4r_result*>(ctx->results.p), st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(results, ctx->results.p, (size_t)npairs * sizeof(icp4r_result), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return ICP4R_OK;
+}
+
+int icp4r_nearest(icp4r_ctx* ctx, const float* query, int32_t n, int32_t query_stride_bytes, const float* tgt,
+                  int32_t m, int32_t tgt_stride_bytes, int32_t* idx_out, float* d2_out) {
+    if (!ctx || (n > 0 && (!idx_out || !d2_out))) return fail(ICP4R_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = check_cloud(query, n, query_stride_bytes, "query"))) return rc;
+    if ((rc = check_cloud(tgt, m, tgt_stride_bytes, "target"))) return rc;
+    if (m == 0) return fail(ICP4R_E_EMPTY, "empty target");
+    if (n == 0) return ICP4R_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> hq, ht;
+    pack_host(query, n, query_stride_bytes, hq);
+    pack_host(tgt, m, tgt_stride_bytes, ht);
+    hipStream_t st = ctx->stream;
+    HIP_TRY(ctx->src.ensure(hq.size() * 4));
+    HIP_TRY(ctx->tgt.ensure(ht.size() * 4));
+    HIP_TRY(ctx->idx.ensure((size_t)n * 4));
+    HIP_TRY(ctx->d2.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(ctx->src.p, hq.data(), hq.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_nn_query(static_cast<const float4*>(ctx->src.p), n, static_cast<const float4*>(ctx->tgt.p), m,
+                             nullptr, static_cast<int32_t*>(ctx->idx.p), static_cast<float*>(ctx->d2.p), st));
+    HIP_TRY(hipMemcpyAsync(idx_out, ctx->idx.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(d2_out, ctx->d2.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return ICP4R_OK;
+}
+
+int icp4r_fitness(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_bytes, const float* tgt, int32_t m,
+                  int32_t tgt_stride_bytes, const float* T, double max_range, double* fitness) {
+    if (!ctx || !T || !fitness) return fail(ICP4R_E_INVALID, "NULL argument");
+    int rc;
+    if ((rc = check_cloud(src, n, src_stride_bytes, "source"))) return rc;
+    if ((rc = check_cloud(tgt, m, tgt_stride_bytes, "target"))) return rc;
+    *fitness = DBL_MAX;
+    if (m == 0) return fail(ICP4R_E_EMPTY, "empty target");
+    if (n == 0) return ICP4R_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> hs, ht, d2((size_t)n);
+    pack_host(src, n, src_stride_bytes, hs);
+    pack_host(tgt, m, tgt_stride_bytes, ht);
+    hipStream_t st = ctx->stream;
+    HIP_TRY(ctx->src.ensure(hs.size() * 4));
+    HIP_TRY(ctx->tgt.ensure(ht.size() * 4));
+    HIP_TRY(ctx->idx.ensure((size_t)n * 4));
+    HIP_TRY(ctx->d2.ensure((size_t)n * 4));
+    HIP_TRY(ctx->T.ensure(64));
+    HIP_TRY(hipMemcpyAsync(ctx->src.p, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->T.p, T, 64, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_nn_query(static_cast<const float4*>(ctx->src.p), n, static_cast<const float4*>(ctx->tgt.p), m,
+                             static_cast<const float*>(ctx->T.p), static_cast<int32_t*>(ctx->idx.p),
+                             static_cast<float*>(ctx->d2.p), st));
+    HIP_TRY(hipMemcpyAsync(d2.data(), ctx->d2.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // Registration::getFitnessScore: sequential double sum over points with d2 <= max_range
+    double sum = 0.0;
+    int nr = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (d2[i] <= max_range) {
+            sum += d2[i];
+            ++nr;
+        }
+    *fitness = nr > 0 ? sum / nr : DBL_MAX;
+    return ICP4R_OK;
+}
+
+int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream) {
+    if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream));
+    return ICP4R_OK;
+}
+
+int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches) {
+    if (!ctx || !avg_ms) return fail(ICP4R_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = events_avg(ctx->nn_events, ctx->nn_used, avg_ms);
+    if (launches) *launches = (int32_t)ctx->nn_used;
+    return rc;
+}
+
+int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls) {
+    if (!ctx || !avg_ms) return fail(ICP4R_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = events_avg(ctx->batch_events, ctx->batch_used, avg_ms);
+    if (calls) *calls = (int32_t)ctx->batch_used;
+    return rc;
+}
+
+int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
+    if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
+    ctx->nn_used = 0;
+    ctx->batch_used = 0;
+    return ICP4R_OK;
+}
+
+int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t* q, int32_t* splits, int64_t* nn_blocks) {
+    if (npairs <= 0 || max_src_n < 0 || max_tgt_n < 0) return fail(ICP4R_E_INVALID, "bad shape");
+    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n);
+    if (q) *q = pl.q;
+    if (splits) *splits = pl.splits;
+    if (nn_blocks) *nn_blocks = pl.blocks;
+    return ICP4R_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,376 @@
+"""icp4r — MI355X-native drop-in for the ICP registration the reference node runs.
+
+Host-side mirror of the PCL surface used at ``/root/reference/src/iterative_closest_point.cpp:510-521``
+(``pcl::IterativeClosestPoint<PointXYZI, PointXYZI>``) over the C ABI in ``include/icp4r/icp4r.h``:
+
+    icp = IterativeClosestPoint()
+    icp.setInputSource(cloud_src_in)        # (N, >=3) float32: x, y, z[, intensity, ...]
+    icp.setInputTarget(cloud_tar_in)
+    Final = icp.align()                     # align(output) -> transformed source
+    icp.hasConverged(), icp.getFitnessScore()
+    T = icp.getFinalTransformation()        # 4x4 float32 (Eigen::Matrix4f values)
+
+The product path is the HIP library ``icp4r/_lib/libicp4r.so`` (gfx950).  There is no CPU fallback:
+if the library or a GPU is missing, calls raise :class:`ICP4RError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+__all__ = [
+    "ICP4RError", "Params", "Result", "Batch", "Context", "IterativeClosestPoint", "library_path", "load",
+    "default_params", "NUMERICS_PCL", "NUMERICS_F64", "status_name", "EXPORTED_SYMBOLS",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(HERE, "_lib", "libicp4r.so")
+
+OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
+NUMERICS_PCL, NUMERICS_F64 = 0, 1
+NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED = 0, 1, 2
+DBL_MAX = sys.float_info.max
+
+_STATUS = {OK: "ICP4R_OK", E_INVALID: "ICP4R_E_INVALID", E_EMPTY: "ICP4R_E_EMPTY",
+           E_TOO_FEW_CORR: "ICP4R_E_TOO_FEW_CORR", E_NONFINITE: "ICP4R_E_NONFINITE", E_HIP: "ICP4R_E_HIP",
+           E_RCCL: "ICP4R_E_RCCL", E_NOMEM: "ICP4R_E_NOMEM", E_TOO_LARGE: "ICP4R_E_TOO_LARGE"}
+
+# every function declared in include/icp4r/icp4r.h (tests check the library exports all of them)
+EXPORTED_SYMBOLS = [
+    "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
+    "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
+    "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
+    "icp4r_kernel_time_reset", "icp4r_plan",
+]
+
+
+def status_name(code: int) -> str:
+    return _STATUS.get(code, f"status {code}")
+
+
+class ICP4RError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{status_name(code)}: {msg}")
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("max_iterations", C.c_int32),
+        ("min_correspondences", C.c_int32),
+        ("max_correspondence_distance", C.c_double),
+        ("transformation_epsilon", C.c_double),
+        ("transformation_rotation_epsilon", C.c_double),
+        ("euclidean_fitness_epsilon", C.c_double),
+        ("mse_threshold_absolute", C.c_double),
+        ("max_iterations_similar_transforms", C.c_int32),
+        ("numerics", C.c_int32),
+        ("nn_mode", C.c_int32),
+        ("compute_fitness", C.c_int32),
+        ("huber_delta", C.c_double),
+        ("fitness_max_range", C.c_double),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("T", C.c_float * 16),
+        ("fitness", C.c_double),
+        ("iterations", C.c_int32),
+        ("converged", C.c_int32),
+        ("status", C.c_int32),
+        ("convergence_state", C.c_int32),
+        ("n_correspondences", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+    def matrix(self) -> np.ndarray:
+        """getFinalTransformation(): 4x4 float32 (stored column-major like Eigen)."""
+        return np.array(self.T, np.float32).reshape(4, 4).T.copy()
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("src", C.c_void_p), ("tgt", C.c_void_p),
+        ("src_off", C.c_void_p), ("src_n", C.c_void_p),
+        ("tgt_off", C.c_void_p), ("tgt_n", C.c_void_p),
+        ("guess", C.c_void_p), ("aligned", C.c_void_p),
+        ("npairs", C.c_int32), ("max_src_n", C.c_int32), ("max_tgt_n", C.c_int32), ("reserved", C.c_int32),
+    ]
+
+
+assert C.sizeof(Result) == 96
+RESULT_DTYPE = np.dtype([("T", np.float32, 16), ("fitness", np.float64), ("iterations", np.int32),
+                         ("converged", np.int32), ("status", np.int32), ("convergence_state", np.int32),
+                         ("n_correspondences", np.int32), ("reserved", np.int32)])
+assert RESULT_DTYPE.itemsize == 96
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(library_path):
+        raise ICP4RError(E_HIP, f"{library_path} not built (run __graft_entry__.build() or make -C icp-4dradar_amd)")
+    L = C.CDLL(library_path)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "icp4r_version": (C.c_char_p, []),
+        "icp4r_abi_version": (C.c_int, []),
+        "icp4r_last_error": (C.c_char_p, []),
+        "icp4r_params_default": (None, [C.POINTER(Params)]),
+        "icp4r_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "icp4r_create": (C.c_int, [C.POINTER(vp), C.c_int]),
+        "icp4r_destroy": (C.c_int, [vp]),
+        "icp4r_align": (C.c_int, [vp, vp, i32, i32, vp, i32, i32, vp, C.POINTER(Params), C.POINTER(Result), vp, i32]),
+        "icp4r_align_batch_device": (C.c_int, [vp, C.POINTER(Batch), C.POINTER(Params), vp, vp]),
+        "icp4r_align_batch_host": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i32, vp, C.POINTER(Params), vp]),
+        "icp4r_fitness": (C.c_int, [vp, vp, i32, i32, vp, i32, i32, vp, C.c_double, C.POINTER(C.c_double)]),
+        "icp4r_nearest": (C.c_int, [vp, vp, i32, i32, vp, i32, i32, vp, vp]),
+        "icp4r_synchronize": (C.c_int, [vp, vp]),
+        "icp4r_kernel_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
+        "icp4r_batch_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
+        "icp4r_kernel_time_reset": (C.c_int, [vp]),
+        "icp4r_plan": (C.c_int, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != OK:
+        raise ICP4RError(rc, f"{what}: {load().icp4r_last_error().decode()}")
+
+
+def default_params(**kw) -> Params:
+    p = Params()
+    load().icp4r_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _cloud(a) -> tuple[np.ndarray, int, int]:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] < 3:
+        raise ICP4RError(E_INVALID, f"cloud must be (N, >=3) float32, got {a.shape}")
+    return a, a.shape[0], a.shape[1] * 4
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+class Context:
+    """One HIP device's stream and buffers (icp4r_create / icp4r_destroy)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load()
+        self._h = C.c_void_p()
+        _check(self._lib.icp4r_create(C.byref(self._h), device), "icp4r_create")
+        self.device = device
+
+    def close(self):
+        if self._h:
+            self._lib.icp4r_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- single pair, host buffers ------------------------------------------------------------
+    def align(self, src, tgt, params: Params | None = None, guess=None, want_aligned: bool = False):
+        s, n, ss = _cloud(src)
+        t, m, ts = _cloud(tgt)
+        p = params if params is not None else default_params()
+        r = Result()
+        g = None
+        if guess is not None:
+            g = np.ascontiguousarray(np.asarray(guess, np.float32).T.reshape(16))
+        out = np.zeros((n, 4), np.float32) if want_aligned else None
+        rc = self._lib.icp4r_align(self._h, _ptr(s), n, ss, _ptr(t), m, ts, _ptr(g) if g is not None else None,
+                                   C.byref(p), C.byref(r), _ptr(out) if out is not None else None, 16)
+        if rc not in (OK, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE):
+            _check(rc, "icp4r_align")
+        return r, out
+
+    def align_batch_host(self, src: np.ndarray, src_off, src_n, tgt: np.ndarray, tgt_off, tgt_n,
+                         params: Params | None = None, guess=None) -> np.ndarray:
+        """Batch from host float4 arrays; returns a structured array of results (RESULT_DTYPE)."""
+        src = np.ascontiguousarray(src, np.float32).reshape(-1, 4)
+        tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 4)
+        so = np.ascontiguousarray(src_off, np.int64)
+        sn = np.ascontiguousarray(src_n, np.int32)
+        to = np.ascontiguousarray(tgt_off, np.int64)
+        tn = np.ascontiguousarray(tgt_n, np.int32)
+        npairs = len(sn)
+        res = np.zeros(npairs, RESULT_DTYPE)
+        g = None
+        if guess is not None:
+            g = np.ascontiguousarray(np.asarray(guess, np.float32).transpose(0, 2, 1).reshape(npairs, 16))
+        p = params if params is not None else default_params()
+        _check(self._lib.icp4r_align_batch_host(self._h, _ptr(src), _ptr(so), _ptr(sn), _ptr(tgt), _ptr(to), _ptr(tn),
+                                                npairs, _ptr(g) if g is not None else None, C.byref(p),
+                                                res.ctypes.data), "icp4r_align_batch_host")
+        return res
+
+    def align_batch_device(self, batch: Batch, params: Params, results_ptr: int, stream: int | None = None):
+        """Device-resident batch (pointers from torch.cuda tensors or hipMalloc); asynchronous."""
+        _check(self._lib.icp4r_align_batch_device(self._h, C.byref(batch), C.byref(params), C.c_void_p(results_ptr),
+                                                  C.c_void_p(stream) if stream else None), "icp4r_align_batch_device")
+
+    def nearest(self, query, tgt):
+        q, n, qs = _cloud(query)
+        t, m, ts = _cloud(tgt)
+        idx = np.empty(n, np.int32)
+        d2 = np.empty(n, np.float32)
+        _check(self._lib.icp4r_nearest(self._h, _ptr(q), n, qs, _ptr(t), m, ts, _ptr(idx), _ptr(d2)), "icp4r_nearest")
+        return idx, d2
+
+    def fitness(self, src, tgt, T, max_range: float = DBL_MAX) -> float:
+        s, n, ss = _cloud(src)
+        t, m, ts = _cloud(tgt)
+        Tc = np.ascontiguousarray(np.asarray(T, np.float32).T.reshape(16))
+        out = C.c_double()
+        _check(self._lib.icp4r_fitness(self._h, _ptr(s), n, ss, _ptr(t), m, ts, _ptr(Tc), max_range, C.byref(out)),
+               "icp4r_fitness")
+        return out.value
+
+    def synchronize(self, stream: int | None = None):
+        _check(self._lib.icp4r_synchronize(self._h, C.c_void_p(stream) if stream else None), "icp4r_synchronize")
+
+    def kernel_time_ms(self) -> tuple[float, int]:
+        ms, k = C.c_double(), C.c_int32()
+        _check(self._lib.icp4r_kernel_time_ms(self._h, C.byref(ms), C.byref(k)), "icp4r_kernel_time_ms")
+        return ms.value, k.value
+
+    def batch_time_ms(self) -> tuple[float, int]:
+        ms, k = C.c_double(), C.c_int32()
+        _check(self._lib.icp4r_batch_time_ms(self._h, C.byref(ms), C.byref(k)), "icp4r_batch_time_ms")
+        return ms.value, k.value
+
+    def reset_timers(self):
+        _check(self._lib.icp4r_kernel_time_reset(self._h), "icp4r_kernel_time_reset")
+
+
+def plan(npairs: int, max_src_n: int, max_tgt_n: int) -> dict:
+    q, s, b = C.c_int32(), C.c_int32(), C.c_int64()
+    _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, C.byref(q), C.byref(s), C.byref(b)), "icp4r_plan")
+    return {"q": q.value, "splits": s.value, "nn_blocks": b.value}
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("ICP4R_DEVICE", "0")))
+    return _default_ctx
+
+
+class IterativeClosestPoint:
+    """pcl::IterativeClosestPoint<PointXYZI, PointXYZI> surface (PCL 1.8.1 defaults)."""
+
+    def __init__(self, context: Context | None = None):
+        self._ctx = context
+        self._p = default_params()
+        self._src = None
+        self._tgt = None
+        self._result: Result | None = None
+
+    # --- Registration setters ---
+    def setInputSource(self, cloud):
+        self._src = np.ascontiguousarray(cloud, np.float32)
+        self._result = None
+
+    def setInputTarget(self, cloud):
+        self._tgt = np.ascontiguousarray(cloud, np.float32)
+        self._result = None
+
+    def setMaximumIterations(self, nr_iterations: int):
+        self._p.max_iterations = int(nr_iterations)
+
+    def getMaximumIterations(self) -> int:
+        return self._p.max_iterations
+
+    def setMaxCorrespondenceDistance(self, distance_threshold: float):
+        self._p.max_correspondence_distance = float(distance_threshold)
+
+    def getMaxCorrespondenceDistance(self) -> float:
+        return self._p.max_correspondence_distance
+
+    def setTransformationEpsilon(self, epsilon: float):
+        self._p.transformation_epsilon = float(epsilon)
+
+    def setTransformationRotationEpsilon(self, epsilon: float):
+        self._p.transformation_rotation_epsilon = float(epsilon)
+
+    def setEuclideanFitnessEpsilon(self, epsilon: float):
+        self._p.euclidean_fitness_epsilon = float(epsilon)
+
+    # build extensions (no PCL counterpart)
+    def setHuberDelta(self, delta: float):
+        self._p.huber_delta = float(delta)
+
+    def setNumerics(self, numerics: int):
+        self._p.numerics = int(numerics)
+
+    def params(self) -> Params:
+        return self._p
+
+    # --- Registration::align ---
+    def align(self, output=None, guess=None) -> np.ndarray:
+        if self._tgt is None:
+            raise ICP4RError(E_EMPTY, "No input target dataset was given!")
+        if self._src is None:
+            raise ICP4RError(E_INVALID, "No input source dataset was given!")
+        ctx = self._ctx or default_context()
+        r, aligned = ctx.align(self._src, self._tgt, self._p, guess=guess, want_aligned=True)
+        self._result = r
+        out = self._src.copy()
+        out[:, :3] = aligned[:, :3]
+        if output is not None:
+            output[...] = out
+            return output
+        return out
+
+    def hasConverged(self) -> bool:
+        return bool(self._result is not None and self._result.converged)
+
+    def getFinalTransformation(self) -> np.ndarray:
+        if self._result is None:
+            return np.eye(4, dtype=np.float32)
+        return self._result.matrix()
+
+    def getFitnessScore(self, max_range: float = DBL_MAX) -> float:
+        if self._result is None:
+            return DBL_MAX
+        if max_range == self._p.fitness_max_range:
+            return self._result.fitness  # computed once inside align
+        return (self._ctx or default_context()).fitness(self._src, self._tgt, self.getFinalTransformation(), max_range)
+
+    # introspection beyond PCL's getters (same information PCL keeps privately)
+    def result(self) -> Result | None:
+        return self._result
+
+    def nr_iterations(self) -> int:
+        return 0 if self._result is None else self._result.iterations

@@ -1,0 +1,176 @@
+/*
+ * icp4r.h — C ABI of the MI355X-native ICP registration core (drop-in boundary).
+ *
+ * Replaces the PCL 1.8.1 default rigid ICP the reference node instantiates at
+ * /root/reference/src/iterative_closest_point.cpp:510-521:
+ *
+ *     pcl::IterativeClosestPoint<pcl::PointXYZI, pcl::PointXYZI> icp;     // :510
+ *     icp.setInputSource(cloud_src_in);                                  // :511
+ *     icp.setInputTarget(cloud_tar_in);                                  // :512
+ *     icp.align(*Final);                                                 // :514
+ *     icp.hasConverged(); icp.getFitnessScore();                         // :516, :520
+ *     icp.getFinalTransformation().cast<double>();                       // :521
+ *
+ * and the same getter surface consumed at /root/reference/src/radar_odometry.cpp:399-412.
+ * The C++ facade include/icp4r/pcl_compat.hpp maps those method names onto these entry points;
+ * INTEGRATION.md shows the binding a maintainer adds.
+ *
+ * Conventions: plain pointers and sizes only; every entry returns int status (0 = OK, < 0 = error,
+ * see icp4r_status) and records a message retrievable with icp4r_last_error() (thread-local).
+ * Matrices are 4x4 float COLUMN-MAJOR (= Eigen::Matrix4f storage; Eigen::Map<Matrix4f>(T) works).
+ * A context owns one HIP device's buffers and stream; calls on one context are serialized.
+ */
+#ifndef ICP4R_H
+#define ICP4R_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICP4R_ABI_VERSION 1
+
+typedef enum icp4r_status {
+    ICP4R_OK = 0,
+    ICP4R_E_INVALID = -1,      /* bad argument / stride / size                                  */
+    ICP4R_E_EMPTY = -2,        /* empty target: Registration::initCompute fails, align returns  */
+    ICP4R_E_TOO_FEW_CORR = -3, /* |C| < min_correspondences: PCL_ERROR, converged = false       */
+    ICP4R_E_NONFINITE = -4,    /* NaN/Inf coordinate in an input cloud (rejected up front)      */
+    ICP4R_E_HIP = -5,          /* HIP runtime failure (message has the HIP error string)        */
+    ICP4R_E_RCCL = -6,         /* reserved for the multi-GPU driver                              */
+    ICP4R_E_NOMEM = -7,        /* device or host allocation failed                               */
+    ICP4R_E_TOO_LARGE = -8     /* a size exceeds what the selected kernel supports               */
+} icp4r_status;
+
+/* pcl::registration::DefaultConvergenceCriteria<float>::ConvergenceState, same order. */
+typedef enum icp4r_convergence_state {
+    ICP4R_CONV_NOT_CONVERGED = 0,
+    ICP4R_CONV_ITERATIONS = 1,
+    ICP4R_CONV_TRANSFORM = 2,
+    ICP4R_CONV_ABS_MSE = 3,
+    ICP4R_CONV_REL_MSE = 4,
+    ICP4R_CONV_NO_CORRESPONDENCES = 5
+} icp4r_convergence_state;
+
+/* Umeyama arithmetic.
+ * PCL: centroids by the sequential float fold Eigen 3.3 performs (bit-identical to PCL when
+ *      the correspondences are), cross-covariance of the float-demeaned points summed in double,
+ *      3x3 SVD in double, R and t rounded to float as Matrix4f.  Matches PCL's float ICP to
+ *      ~1e-6 m: the default, and what the ≤1e-4 parity bar is stated against.
+ * F64: every moment summed in double (more accurate than PCL; differs from it by PCL's own
+ *      float-centroid noise, up to ~2e-4 m on 8k-point clouds). */
+typedef enum icp4r_numerics { ICP4R_NUMERICS_PCL = 0, ICP4R_NUMERICS_F64 = 1 } icp4r_numerics;
+
+/* Correspondence search.  All modes return the exact nearest neighbour under FLANN's
+ * L2_Simple<float> distance ((dx*dx + dy*dy) + dz*dz, float, unfused); ties -> lowest index. */
+typedef enum icp4r_nn_mode {
+    ICP4R_NN_AUTO = 0,         /* pick per shape (currently ICP4R_NN_BRUTE_PACKED)                   */
+    ICP4R_NN_BRUTE = 1,        /* exhaustive scan, target streamed through the scalar cache, FP32    */
+    ICP4R_NN_BRUTE_PACKED = 2  /* same scan, two queries per v_pk_{add,mul}_f32 (identical results) */
+} icp4r_nn_mode;
+
+typedef struct icp4r_params {
+    int32_t max_iterations;                    /* setMaximumIterations;           PCL default 10        */
+    int32_t min_correspondences;               /* min_number_correspondences_;    3                     */
+    double max_correspondence_distance;        /* setMaxCorrespondenceDistance;   sqrt(DBL_MAX)         */
+    double transformation_epsilon;             /* setTransformationEpsilon;       0                     */
+    double transformation_rotation_epsilon;    /* setTransformationRotationEpsilon; 0 (-> 1 - eps)      */
+    double euclidean_fitness_epsilon;          /* setEuclideanFitnessEpsilon;     -DBL_MAX              */
+    double mse_threshold_absolute;             /* DefaultConvergenceCriteria;     1e-12 (< 0: disabled) */
+    int32_t max_iterations_similar_transforms; /* DefaultConvergenceCriteria;     0                     */
+    int32_t numerics;                          /* icp4r_numerics;                 ICP4R_NUMERICS_PCL    */
+    int32_t nn_mode;                           /* icp4r_nn_mode;                  ICP4R_NN_AUTO         */
+    int32_t compute_fitness;                   /* 1: getFitnessScore(fitness_max_range) computed once   */
+    double huber_delta;                        /* build extension (no PCL counterpart); +inf == PCL     */
+    double fitness_max_range;                  /* getFitnessScore(max_range);     DBL_MAX               */
+    int32_t reserved[8];
+} icp4r_params;
+
+typedef struct icp4r_result {
+    float T[16];               /* getFinalTransformation(), column-major                     */
+    double fitness;            /* getFitnessScore(fitness_max_range); DBL_MAX if no point    */
+    int32_t iterations;        /* nr_iterations_                                              */
+    int32_t converged;         /* hasConverged()                                              */
+    int32_t status;            /* icp4r_status of this pair                                   */
+    int32_t convergence_state; /* icp4r_convergence_state                                     */
+    int32_t n_correspondences; /* |C| of the last iteration                                   */
+    int32_t reserved;
+} icp4r_result; /* 96 bytes */
+
+/* Device-resident batch: every cloud is float4 (x, y, z, intensity) = 16 B/point in HBM. */
+typedef struct icp4r_batch {
+    const float* src;        /* device: concatenated source clouds, float4 per point          */
+    const float* tgt;        /* device: concatenated target clouds, float4 per point          */
+    const int64_t* src_off;  /* device[npairs]: first point of pair p's source                */
+    const int32_t* src_n;    /* device[npairs]                                                */
+    const int64_t* tgt_off;  /* device[npairs]                                                */
+    const int32_t* tgt_n;    /* device[npairs]                                                */
+    const float* guess;      /* device[npairs*16] column-major, or NULL (identity)            */
+    float* aligned;          /* device: optional output clouds, same layout as src, or NULL   */
+    int32_t npairs;
+    int32_t max_src_n;       /* host-known upper bound of src_n[] (selects the kernel)        */
+    int32_t max_tgt_n;       /* host-known upper bound of tgt_n[]                             */
+    int32_t reserved;
+} icp4r_batch;
+
+typedef struct icp4r_ctx icp4r_ctx;
+
+const char* icp4r_version(void);
+int icp4r_abi_version(void);
+const char* icp4r_last_error(void);
+void icp4r_params_default(icp4r_params* p);
+int icp4r_device_count(int* count);
+
+int icp4r_create(icp4r_ctx** out, int device);
+int icp4r_destroy(icp4r_ctx* ctx);
+
+/* Registration::align(output, guess) — synchronous, host buffers.  src/tgt: n/m points with a
+ * stride in bytes (PCL PointXYZI: 32, float4: 16, the .bin record: 20); x, y, z are the first
+ * three floats of a point, intensity the fourth when stride >= 16.  guess: 16 floats
+ * column-major or NULL.  aligned_out (optional): n points written with out_stride_bytes,
+ * x, y, z = transformCloud(input, final), intensity copied when out_stride_bytes >= 16. */
+int icp4r_align(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_bytes, const float* tgt,
+                int32_t m, int32_t tgt_stride_bytes, const float* guess, const icp4r_params* params,
+                icp4r_result* out, float* aligned_out, int32_t out_stride_bytes);
+
+/* Many pairs, device-resident (inputs already in HBM), asynchronous on `hip_stream`
+ * (a hipStream_t; NULL = the context's stream).  results: device[npairs]. */
+int icp4r_align_batch_device(icp4r_ctx* ctx, const icp4r_batch* batch, const icp4r_params* params,
+                             icp4r_result* results, void* hip_stream);
+
+/* Many pairs from host buffers (float4 per point, concatenated), synchronous. */
+int icp4r_align_batch_host(icp4r_ctx* ctx, const float* src, const int64_t* src_off, const int32_t* src_n,
+                           const float* tgt, const int64_t* tgt_off, const int32_t* tgt_n, int32_t npairs,
+                           const float* guess, const icp4r_params* params, icp4r_result* results);
+
+/* Registration::getFitnessScore(max_range) for a given transform (host buffers). */
+int icp4r_fitness(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_bytes, const float* tgt,
+                  int32_t m, int32_t tgt_stride_bytes, const float* T, double max_range, double* fitness);
+
+/* CorrespondenceEstimation::determineCorrespondences at infinite distance: exact 1-NN of every
+ * query in the target (host buffers).  idx_out[n], d2_out[n]. */
+int icp4r_nearest(icp4r_ctx* ctx, const float* query, int32_t n, int32_t query_stride_bytes, const float* tgt,
+                  int32_t m, int32_t tgt_stride_bytes, int32_t* idx_out, float* d2_out);
+
+/* Synchronize the context's stream (or `hip_stream` if non-NULL). */
+int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream);
+
+/* Device-time accounting with HIP events on the launch stream (used by bench.py for the roofline):
+ * icp4r_kernel_time_ms: average duration of the NN-sweep kernel launches (the dominant kernel)
+ *                       recorded since the last reset, and how many there were;
+ * icp4r_batch_time_ms:  average duration of whole registration calls (all launches of a batch). */
+int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
+int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);
+int icp4r_kernel_time_reset(icp4r_ctx* ctx);
+
+/* Launch geometry the batch path picks for a shape (queries per lane, target splits, workgroups
+ * of the NN kernel) — exposed for tests and the benchmark report. */
+int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t* q, int32_t* splits, int64_t* nn_blocks);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ICP4R_H */

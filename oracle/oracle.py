@@ -1,0 +1,172 @@
+"""ctypes loader for the C oracle (oracle/icp_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+This is the checker and the CPU-baseline leg.  Only tests/, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it; the product path (icp4r) never does.
+Parity status: unpinned by the reference (no reference tests exist; PCL is not vendored) —
+pinned by analytic known-answer tests and an independent numpy/scipy twin.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libicp_oracle.so")
+
+NUM_F32, NUM_F64 = 0, 1
+NN_KDTREE, NN_BRUTE = 0, 1
+
+
+class OracleParams(C.Structure):
+    _fields_ = [
+        ("max_iterations", C.c_int32),
+        ("min_correspondences", C.c_int32),
+        ("max_correspondence_distance", C.c_double),
+        ("transformation_epsilon", C.c_double),
+        ("transformation_rotation_epsilon", C.c_double),
+        ("euclidean_fitness_epsilon", C.c_double),
+        ("mse_threshold_absolute", C.c_double),
+        ("max_iterations_similar_transforms", C.c_int32),
+        ("numerics", C.c_int32),
+        ("nn", C.c_int32),
+        ("compute_fitness", C.c_int32),
+        ("huber_delta", C.c_double),
+        ("fitness_max_range", C.c_double),
+    ]
+
+
+class OracleResult(C.Structure):
+    _fields_ = [
+        ("T", C.c_float * 16),
+        ("fitness", C.c_double),
+        ("iterations", C.c_int32),
+        ("converged", C.c_int32),
+        ("status", C.c_int32),
+        ("convergence_state", C.c_int32),
+        ("n_correspondences", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class OracleTrace(C.Structure):
+    _fields_ = [
+        ("T_inc", C.c_void_p),
+        ("T_final", C.c_void_p),
+        ("mse", C.c_void_p),
+        ("ncorr", C.c_void_p),
+        ("sigma", C.c_void_p),
+        ("mu_src", C.c_void_p),
+        ("mu_dst", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_params_default.argtypes = [C.POINTER(OracleParams)]
+        L.oracle_align.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                   C.c_void_p, C.POINTER(OracleParams), C.POINTER(OracleResult),
+                                   C.c_void_p, C.POINTER(OracleTrace)]
+        L.oracle_align.restype = C.c_int
+        L.oracle_nearest.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                     C.c_int32, C.c_void_p, C.c_void_p]
+        L.oracle_nearest.restype = C.c_int
+        L.oracle_fitness.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                     C.c_void_p, C.c_double, C.c_int32]
+        L.oracle_fitness.restype = C.c_double
+        L.oracle_kdtree_leaf_visits.restype = C.c_int64
+        _lib = L
+    return _lib
+
+
+def default_params(**kw) -> OracleParams:
+    p = OracleParams()
+    lib().oracle_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _cloud(a: np.ndarray):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if a.ndim != 2 or a.shape[1] < 3:
+        raise ValueError("cloud must be (N, >=3) float32")
+    return a, a.shape[0], a.shape[1]
+
+
+def align(src: np.ndarray, tgt: np.ndarray, guess: np.ndarray | None = None, trace: bool = False,
+          aligned: bool = False, **params):
+    """Run the restated PCL ICP.  Returns a dict with T (4x4, float32), fitness, iterations, ..."""
+    s, n, ss = _cloud(src)
+    t, m, ts = _cloud(tgt)
+    p = default_params(**params)
+    r = OracleResult()
+    g = None
+    if guess is not None:
+        g = np.ascontiguousarray(np.asarray(guess, np.float32).T.reshape(16))  # column-major
+    tr = None
+    bufs = {}
+    if trace:
+        it = max(1, p.max_iterations)
+        bufs = {
+            "T_inc": np.zeros((it, 16), np.float32), "T_final": np.zeros((it, 16), np.float32),
+            "mse": np.zeros(it, np.float64), "ncorr": np.zeros(it, np.int32),
+            "sigma": np.zeros((it, 9), np.float64), "mu_src": np.zeros((it, 3), np.float64),
+            "mu_dst": np.zeros((it, 3), np.float64),
+        }
+        tr = OracleTrace(*[bufs[k].ctypes.data for k in ("T_inc", "T_final", "mse", "ncorr", "sigma", "mu_src", "mu_dst")])
+    out = np.zeros((n, 4), np.float32) if aligned else None
+    lib().oracle_align(s.ctypes.data if n else None, n, ss, t.ctypes.data if m else None, m, ts,
+                       g.ctypes.data if g is not None else None, C.byref(p), C.byref(r),
+                       out.ctypes.data if out is not None else None, C.byref(tr) if tr else None)
+    res = {
+        "T": np.array(r.T, np.float32).reshape(4, 4).T.copy(),
+        "fitness": r.fitness, "iterations": r.iterations, "converged": bool(r.converged),
+        "status": r.status, "convergence_state": r.convergence_state,
+        "n_correspondences": r.n_correspondences,
+    }
+    if trace:
+        k = r.iterations
+        res["trace"] = {
+            "T_inc": bufs["T_inc"][:k].reshape(k, 4, 4).transpose(0, 2, 1).copy(),
+            "T_final": bufs["T_final"][:k].reshape(k, 4, 4).transpose(0, 2, 1).copy(),
+            "mse": bufs["mse"][:k].copy(), "ncorr": bufs["ncorr"][:k].copy(),
+            "sigma": bufs["sigma"][:k].reshape(k, 3, 3).copy(),
+            "mu_src": bufs["mu_src"][:k].copy(), "mu_dst": bufs["mu_dst"][:k].copy(),
+        }
+    if aligned:
+        res["aligned"] = out
+    return res
+
+
+def nearest(query: np.ndarray, tgt: np.ndarray, nn: int = NN_BRUTE):
+    q, n, qs = _cloud(query)
+    t, m, ts = _cloud(tgt)
+    idx = np.empty(n, np.int32)
+    d2 = np.empty(n, np.float32)
+    rc = lib().oracle_nearest(q.ctypes.data, n, qs, t.ctypes.data, m, ts, nn, idx.ctypes.data, d2.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle_nearest failed: {rc}")
+    return idx, d2
+
+
+def fitness(src: np.ndarray, tgt: np.ndarray, T: np.ndarray, max_range: float = np.finfo(np.float64).max,
+            nn: int = NN_KDTREE) -> float:
+    s, n, ss = _cloud(src)
+    t, m, ts = _cloud(tgt)
+    Tc = np.ascontiguousarray(np.asarray(T, np.float32).T.reshape(16))
+    return lib().oracle_fitness(s.ctypes.data, n, ss, t.ctypes.data, m, ts, Tc.ctypes.data, max_range, nn)

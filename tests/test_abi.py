@@ -1,0 +1,92 @@
+"""The C-ABI library: it loads without a GPU, exports every entry point include/icp4r/icp4r.h declares,
+and its host-only helpers behave (no GPU compute calls here)."""
+import ctypes as C
+import math
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int|void)\s+(icp4r_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    import icp4r
+
+    L = icp4r.load()
+    decl = header_functions()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(L, name), f"{name} declared in icp4r.h but not exported"
+    assert sorted(icp4r.EXPORTED_SYMBOLS) == decl
+
+
+def test_nm_shows_c_linkage():
+    import icp4r
+
+    out = subprocess.run(["nm", "-D", "--defined-only", icp4r.library_path], capture_output=True, text=True).stdout
+    for name in header_functions():
+        assert re.search(rf"\bT {name}$", out, re.M), name
+
+
+def test_params_default_matches_pcl():
+    import icp4r
+
+    p = icp4r.default_params()
+    assert p.max_iterations == 10
+    assert p.min_correspondences == 3
+    assert p.max_correspondence_distance == math.sqrt(sys.float_info.max)
+    assert p.transformation_epsilon == 0.0
+    assert p.transformation_rotation_epsilon == 0.0
+    assert p.euclidean_fitness_epsilon == -sys.float_info.max
+    assert p.mse_threshold_absolute == 1e-12
+    assert p.numerics == icp4r.NUMERICS_PCL
+    assert p.compute_fitness == 1
+    assert math.isinf(p.huber_delta)
+    assert p.fitness_max_range == sys.float_info.max
+    L = icp4r.load()
+    assert L.icp4r_abi_version() == 1
+    assert b"gfx950" in L.icp4r_version()
+
+
+def test_struct_layouts():
+    import icp4r
+
+    assert C.sizeof(icp4r.Result) == 96
+    assert C.sizeof(icp4r.Batch) == 8 * 8 + 16
+    assert icp4r.Result.fitness.offset == 64
+
+
+def test_plan_geometry():
+    import icp4r
+
+    big = icp4r.plan(1024, 8192, 8192)
+    assert big["splits"] == 1 and big["q"] == 16
+    single = icp4r.plan(1, 8192, 8192)
+    assert single["splits"] > 1 and single["nn_blocks"] >= 512
+    tiny = icp4r.plan(1, 10, 7)
+    assert tiny["q"] == 1 and tiny["splits"] == 1
+
+
+def test_fails_loudly_without_library(tmp_path, monkeypatch):
+    import icp4r
+
+    monkeypatch.setattr(icp4r, "_lib", None)
+    monkeypatch.setattr(icp4r, "library_path", str(tmp_path / "missing.so"))
+    with pytest.raises(icp4r.ICP4RError):
+        icp4r.load()
+
+
+def test_cpp_facade_compiles():
+    """include/icp4r/pcl_compat.hpp + a verbatim copy of the reference call block compile and link
+    against the library (running it needs the GPU: tests/test_gpu_parity.py)."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -1,0 +1,240 @@
+"""Parity of the HIP product (through the C ABI) with the oracle — needs a real MI355X.
+
+Bars (north_star): NN indices and d² bit-exact (integer/index work); per-pair transforms within
+1e-4 m / 1e-4 rad of the reference-faithful oracle on identical inputs; batch, split and repeated
+runs bit-identical to each other.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN_DIR, TOL_R, TOL_T, load_case_clouds, pose_err
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _pair(i, n, m=None):
+    from icp4r import synth
+
+    p = synth.make_pair(i, n, m)
+    return p.src_xyzi(), p.tgt_xyzi()
+
+
+# ---------------------------------------------------------------------------------------------- NN
+@pytest.mark.parametrize("which", [0, 1])
+def test_nn_bitexact_golden(gpu_ctx, oracle_mod, golden, which):
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    gi, gd = gpu_ctx.nearest(src, tgt)
+    oi, od = oracle_mod.nearest(src, tgt, oracle_mod.NN_BRUTE)
+    assert (gi == oi).all() and (gd == od).all()
+    rows = np.array(case["nn0_rows"])
+    assert (gi[rows] == np.array(case["nn0_idx_rows"])).all()
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (5, 3), (7, 1001), (1000, 4099), (4097, 8190), (3, 65540)])
+def test_nn_bitexact_shapes_and_ties(gpu_ctx, oracle_mod, n, m):
+    rng = np.random.default_rng(n * 31 + m)
+    tgt = rng.uniform(-80, 80, (m, 4)).astype(np.float32)
+    if m > 10:
+        tgt[m // 2: m // 2 + 5] = tgt[:5]  # duplicates: ties -> lowest index
+    q = rng.uniform(-90, 90, (n, 4)).astype(np.float32)
+    q[: min(n, 5)] = tgt[: min(n, 5)]
+    gi, gd = gpu_ctx.nearest(q, tgt)
+    oi, od = oracle_mod.nearest(q, tgt, oracle_mod.NN_BRUTE)
+    assert (gi == oi).all() and (gd == od).all()
+
+
+# ---------------------------------------------------------------------------------------------- ICP
+@pytest.mark.parametrize("which", [0, 1])
+def test_icp_pcl_numerics_vs_oracle(gpu_ctx, oracle_mod, golden, which):
+    import icp4r
+
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    it = case["max_iterations"]
+    r, _ = gpu_ctx.align(src, tgt, icp4r.default_params(max_iterations=it))
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=it)
+    assert r.status == 0 and r.iterations == o["iterations"] and bool(r.converged) == o["converged"]
+    dt, dr = pose_err(r.matrix(), o["T"])
+    assert dt <= TOL_T and dr <= TOL_R, (dt, dr)
+    assert abs(r.fitness - o["fitness"]) <= 1e-4 * o["fitness"]
+    # and against the independent numpy twin's golden answer
+    dt, dr = pose_err(r.matrix(), case["T"])
+    assert dt <= 3 * TOL_T and dr <= TOL_R, (dt, dr)
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_icp_f64_numerics_vs_oracle_f64(gpu_ctx, oracle_mod, golden, which):
+    import icp4r
+
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    it = case["max_iterations"]
+    r, _ = gpu_ctx.align(src, tgt, icp4r.default_params(max_iterations=it, numerics=icp4r.NUMERICS_F64))
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F64, max_iterations=it)
+    assert r.iterations == o["iterations"] == case["iterations"]
+    dt, dr = pose_err(r.matrix(), o["T"])
+    assert dt <= 2e-6 and dr <= 2e-6, (dt, dr)
+    dt, dr = pose_err(r.matrix(), case["T"])
+    assert dt <= 2e-6 and dr <= 2e-6, (dt, dr)
+    assert abs(r.fitness - case["fitness"]) <= 1e-6 * case["fitness"]
+
+
+@pytest.mark.parametrize("i", range(6))
+def test_icp_random_pairs_pcl_defaults(gpu_ctx, oracle_mod, i):
+    """PCL defaults (10 iterations, |ΔMSE| early stop live) on assorted shapes."""
+    import icp4r
+
+    n = [2048, 8192, 1000, 3001, 513, 6000][i]
+    m = [2048, 8192, 1500, 2999, 700, 8191][i]
+    src, tgt = _pair(100 + i, n, m)
+    r, out = gpu_ctx.align(src, tgt, icp4r.default_params(), want_aligned=True)
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True)
+    assert r.iterations == o["iterations"] and bool(r.converged) == o["converged"]
+    dt, dr = pose_err(r.matrix(), o["T"])
+    assert dt <= TOL_T and dr <= TOL_R, (dt, dr)
+    np.testing.assert_allclose(out[:, :3], o["aligned"][:, :3], atol=5e-3)
+    assert (out[:, 3] == src[:, 3]).all()
+
+
+def test_known_answers(gpu_ctx, golden):
+    import icp4r
+
+    for kat in golden["kat"]:
+        r, _ = gpu_ctx.align(np.array(kat["src"], np.float32), np.array(kat["tgt"], np.float32),
+                             icp4r.default_params(max_iterations=20))
+        dt, dr = pose_err(r.matrix(), kat["T_expect"])
+        assert dt < kat["tol_t"] and dr < kat["tol_r"], (kat["name"], dt, dr)
+
+
+# ---------------------------------------------------------------------------------------------- paths
+def _batch(pairs):
+    src = np.concatenate([p[0] for p in pairs]).astype(np.float32)
+    tgt = np.concatenate([p[1] for p in pairs]).astype(np.float32)
+    sn = np.array([len(p[0]) for p in pairs], np.int32)
+    tn = np.array([len(p[1]) for p in pairs], np.int32)
+    so = np.concatenate([[0], np.cumsum(sn)[:-1]]).astype(np.int64)
+    to = np.concatenate([[0], np.cumsum(tn)[:-1]]).astype(np.int64)
+    return src, so, sn, tgt, to, tn
+
+
+def test_batch_equals_single_calls(gpu_ctx):
+    import icp4r
+
+    shapes = [(8192, 8192), (2048, 2048), (1000, 1200), (37, 4000), (4096, 64), (8000, 8100), (3, 3), (700, 650)]
+    pairs = [_pair(200 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    p = icp4r.default_params(max_iterations=15)
+    res = gpu_ctx.align_batch_host(*_batch(pairs), params=p)
+    for k, (s, t) in enumerate(pairs):
+        r, _ = gpu_ctx.align(s, t, p)
+        assert (np.array(r.T, np.float32) == res[k]["T"]).all(), k
+        assert r.iterations == res[k]["iterations"] and r.fitness == res[k]["fitness"]
+
+
+def test_target_split_equals_unsplit(gpu_ctx):
+    """A single pair runs with the target split across workgroups; a 64-pair batch does not."""
+    import icp4r
+
+    s, t = _pair(300, 8192)
+    assert icp4r.plan(1, 8192, 8192)["splits"] > 1 and icp4r.plan(64, 8192, 8192)["splits"] == 1
+    p = icp4r.default_params(max_iterations=20)
+    r, _ = gpu_ctx.align(s, t, p)
+    res = gpu_ctx.align_batch_host(*_batch([(s, t)] * 64), params=p)
+    for k in range(64):
+        assert (res[k]["T"] == np.array(r.T, np.float32)).all()
+
+
+def test_repeatable_and_target_permutation_invariant(gpu_ctx):
+    import icp4r
+
+    s, t = _pair(400, 8192)
+    p = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0)
+    a, _ = gpu_ctx.align(s, t, p)
+    b, _ = gpu_ctx.align(s, t, p)
+    assert bytes(a) == bytes(b)
+    perm = np.random.default_rng(1).permutation(len(t))
+    c, _ = gpu_ctx.align(s, t[perm], p)
+    assert (np.array(a.T) == np.array(c.T)).all()  # same matched coordinates, same fold order
+
+
+# ---------------------------------------------------------------------------------------------- edges
+def test_error_and_option_paths(gpu_ctx, oracle_mod):
+    import icp4r
+
+    s, t = _pair(500, 2000)
+    r, _ = gpu_ctx.align(s, np.zeros((0, 4), np.float32))
+    assert r.status == icp4r.E_EMPTY and not r.converged and np.allclose(r.matrix(), np.eye(4))
+    r, _ = gpu_ctx.align(s[:2], t)
+    assert r.status == icp4r.E_TOO_FEW_CORR and not r.converged and r.convergence_state == 5
+    bad = s.copy()
+    bad[3, 2] = np.inf
+    r, _ = gpu_ctx.align(bad, t)
+    assert r.status == icp4r.E_NONFINITE
+    # correspondence rejection, max_iterations 0/1, guess, Huber (F64 vs oracle F64)
+    for kw in ({"max_correspondence_distance": 1.0}, {"max_iterations": 0}, {"max_iterations": 1},
+               {"transformation_epsilon": 1e-8}, {"euclidean_fitness_epsilon": 1e-3}):
+        r, _ = gpu_ctx.align(s, t, icp4r.default_params(**kw))
+        o = oracle_mod.align(s, t, numerics=oracle_mod.NUM_F32, **kw)
+        assert r.iterations == o["iterations"] and r.convergence_state == o["convergence_state"], kw
+        assert r.n_correspondences == o["n_correspondences"], kw
+        dt, dr = pose_err(r.matrix(), o["T"])
+        assert dt <= TOL_T and dr <= TOL_R, (kw, dt, dr)
+    G = np.eye(4, dtype=np.float32)
+    G[:3, 3] = [0.3, -0.2, 0.05]
+    r, _ = gpu_ctx.align(s, t, icp4r.default_params(), guess=G)
+    o = oracle_mod.align(s, t, guess=G, numerics=oracle_mod.NUM_F32)
+    dt, dr = pose_err(r.matrix(), o["T"])
+    assert r.iterations == o["iterations"] and dt <= TOL_T and dr <= TOL_R
+    for num, onum in ((icp4r.NUMERICS_F64, oracle_mod.NUM_F64), (icp4r.NUMERICS_PCL, oracle_mod.NUM_F32)):
+        r, _ = gpu_ctx.align(s, t, icp4r.default_params(huber_delta=0.5, numerics=num))
+        o = oracle_mod.align(s, t, huber_delta=0.5, numerics=onum)
+        dt, dr = pose_err(r.matrix(), o["T"])
+        assert dt <= TOL_T and dr <= TOL_R, (num, dt, dr)
+
+
+def test_fitness_entry_point(gpu_ctx, oracle_mod):
+    s, t = _pair(600, 3000)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.1, 0.2, -0.1]
+    for mr in (np.finfo(np.float64).max, 0.5):
+        g = gpu_ctx.fitness(s, t, T, mr)
+        o = oracle_mod.fitness(s, t, T, mr)
+        assert g == o
+
+
+# ---------------------------------------------------------------------------------------------- facade
+def test_pcl_facade_callsite(oracle_mod, golden):
+    """The node's call sequence compiled against pcl_compat.hpp, on the golden C1 scans."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    case = golden["cases"][0]
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "callsite")
+    out = subprocess.run([exe, os.path.join(GOLDEN_DIR, case["src_bin"]), os.path.join(GOLDEN_DIR, case["tgt_bin"])],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = {l.split()[0]: l for l in out.stdout.splitlines() if l.split()}
+    kv = dict(tok.split("=") for tok in lines["RESULT"].split()[1:])
+    T = np.array([float(v) for v in lines["T"].split()[1:]]).reshape(4, 4)
+    src, tgt = load_case_clouds(case)
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32)
+    assert int(kv["converged"]) == 1 and int(kv["iterations"]) == o["iterations"] == 10
+    assert int(kv["points"]) == len(src)
+    dt, dr = pose_err(T, o["T"])
+    assert dt <= TOL_T and dr <= TOL_R
+    assert abs(float(kv["score"]) - o["fitness"]) <= 1e-4 * o["fitness"]
+
+
+def test_kernel_timing_api(gpu_ctx):
+    import icp4r
+
+    gpu_ctx.reset_timers()
+    s, t = _pair(700, 2048)
+    gpu_ctx.align(s, t, icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1))
+    ms, k = gpu_ctx.kernel_time_ms()
+    bms, bk = gpu_ctx.batch_time_ms()
+    assert k == 6 and ms > 0 and bk == 1 and bms >= ms

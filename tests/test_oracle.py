@@ -1,0 +1,143 @@
+"""The C oracle (oracle/icp_oracle.c) against the golden fixtures and analytic known answers.
+
+The oracle is the checker of the HIP product; these tests pin it before it is trusted (the
+reference has no tests of its own: SURVEY.md §4, §8c).  CPU only.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN_DIR, TOL_R, TOL_T, load_case_clouds, pose_err
+
+
+def _digest(idx, d2):
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(idx, np.int32).tobytes())
+    h.update(np.ascontiguousarray(d2, np.float32).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_nn_iteration0_matches_golden(oracle_mod, golden, which):
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    for nn in (oracle_mod.NN_BRUTE, oracle_mod.NN_KDTREE):
+        idx, d2 = oracle_mod.nearest(src, tgt, nn)
+        assert _digest(idx, d2) == case["nn0_sha256"], f"nn mode {nn}"
+        rows = np.array(case["nn0_rows"])
+        assert (idx[rows] == np.array(case["nn0_idx_rows"])).all()
+        assert (d2[rows] == np.array(case["nn0_d2_rows"], np.float32)).all()
+        if "nn0_idx" in case:
+            assert (idx == np.array(case["nn0_idx"])).all()
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_icp_f64_matches_numpy_twin(oracle_mod, golden, which):
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    r = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F64, max_iterations=case["max_iterations"], trace=True)
+    assert r["status"] == 0
+    assert r["iterations"] == case["iterations"]
+    assert r["converged"] == case["converged"]
+    assert r["convergence_state"] == case["convergence_state"]
+    # same arithmetic up to double summation order: identical to ~float rounding
+    for k, Tk in enumerate(case["T_final_trace"]):
+        dt, dr = pose_err(r["trace"]["T_final"][k], Tk)
+        assert dt < 2e-6 and dr < 2e-6, (k, dt, dr)
+    np.testing.assert_allclose(r["trace"]["mu_src"][0], case["mu_src0"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(r["trace"]["mu_dst"][0], case["mu_dst0"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(r["trace"]["sigma"][0], case["sigma0"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(r["trace"]["mse"], case["mse_trace"], rtol=1e-9)
+    assert abs(r["fitness"] - case["fitness"]) <= 1e-9 * max(1.0, case["fitness"])
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_icp_pcl_float_within_bar_of_f64(oracle_mod, golden, which):
+    """PCL's float Umeyama vs the exact solve: the reference's own float noise (documented)."""
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    a = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=case["max_iterations"])
+    dt, dr = pose_err(a["T"], case["T"])
+    assert dt < 3 * TOL_T and dr < TOL_R, (dt, dr)
+
+
+def test_kdtree_equals_bruteforce_including_ties(oracle_mod):
+    rng = np.random.default_rng(3)
+    tgt = rng.uniform(-50, 50, (3000, 4)).astype(np.float32)
+    tgt[1500:1600] = tgt[100:200]  # exact duplicates -> ties must resolve to the lowest index
+    q = np.concatenate([rng.uniform(-60, 60, (2000, 4)).astype(np.float32), tgt[100:200]])
+    i1, d1 = oracle_mod.nearest(q, tgt, oracle_mod.NN_BRUTE)
+    i2, d2 = oracle_mod.nearest(q, tgt, oracle_mod.NN_KDTREE)
+    assert (i1 == i2).all() and (d1 == d2).all()
+    assert (i1[2000:] == np.arange(100, 200)).all()
+
+
+@pytest.mark.parametrize("num", [0, 1])
+def test_known_answers(oracle_mod, golden, num):
+    for kat in golden["kat"]:
+        src = np.array(kat["src"], np.float32)
+        tgt = np.array(kat["tgt"], np.float32)
+        r = oracle_mod.align(src, tgt, numerics=num, max_iterations=20)
+        dt, dr = pose_err(r["T"], kat["T_expect"])
+        assert dt < kat["tol_t"] and dr < kat["tol_r"], (kat["name"], dt, dr)
+
+
+def test_error_paths(oracle_mod):
+    rng = np.random.default_rng(5)
+    c = rng.uniform(-5, 5, (100, 4)).astype(np.float32)
+    # empty target: Registration::initCompute fails -> identity, not converged
+    r = oracle_mod.align(c, np.zeros((0, 4), np.float32))
+    assert r["status"] == -2 and not r["converged"] and np.allclose(r["T"], np.eye(4))
+    # fewer than 3 correspondences
+    r = oracle_mod.align(c[:2], c)
+    assert r["status"] == -3 and not r["converged"] and r["convergence_state"] == 5
+    # rejection by max correspondence distance -> too few
+    far = c.copy()
+    far[:, :3] += 1000
+    r = oracle_mod.align(far, c, max_correspondence_distance=1.0)
+    assert r["status"] == -3 and r["iterations"] == 0
+    # non-finite input rejected up front
+    bad = c.copy()
+    bad[7, 1] = np.nan
+    assert oracle_mod.align(bad, c)["status"] == -4
+
+
+def test_convergence_criteria(oracle_mod, golden):
+    case = golden["cases"][0]
+    src, tgt = load_case_clouds(case)
+    r = oracle_mod.align(src, tgt, max_iterations=1)
+    assert r["iterations"] == 1 and r["converged"] and r["convergence_state"] == 1
+    # max_iterations = 0: PCL's do/while still runs one iteration
+    r = oracle_mod.align(src, tgt, max_iterations=0)
+    assert r["iterations"] == 1 and r["converged"]
+    # identical clouds (the node's order-0 frame): exact solve -> X unchanged -> |ΔMSE| = 0 < 1e-12
+    # stops at iteration 2 with CONVERGENCE_CRITERIA_ABS_MSE.  The float solve's rounding instead
+    # moves X by ~1e-7 per iteration (MSE 0 -> 4e-11 -> ...), so it runs to the cap; T stays I.
+    r = oracle_mod.align(tgt, tgt, max_iterations=10, numerics=oracle_mod.NUM_F64)
+    assert r["converged"] and r["iterations"] == 2 and r["convergence_state"] == 3
+    r = oracle_mod.align(tgt, tgt, max_iterations=10, numerics=oracle_mod.NUM_F32)
+    assert r["converged"] and np.abs(r["T"] - np.eye(4)).max() < 1e-5
+
+
+def test_guess_applied(oracle_mod, golden):
+    case = golden["cases"][0]
+    src, tgt = load_case_clouds(case)
+    G = np.array(case["T"], np.float32)
+    r0 = oracle_mod.align(src, tgt, max_iterations=10)
+    r1 = oracle_mod.align(src, tgt, guess=G, max_iterations=10)
+    dt, dr = pose_err(r0["T"], r1["T"])
+    assert dt < 5e-3 and dr < 5e-3
+
+
+def test_sanitizer_build_runs():
+    """The oracle under ASan/UBSan (host-only sanitizers) on a small pair."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    od = os.path.join(root, "oracle")
+    r = subprocess.run(["make", "-s", "-C", od, "_build/oracle_asan"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(od, "_build", "oracle_asan")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
