@@ -43,7 +43,8 @@ def test_nn_bitexact_shapes_and_ties(gpu_ctx, oracle_mod, n, m):
     if m > 10:
         tgt[m // 2: m // 2 + 5] = tgt[:5]  # duplicates: ties -> lowest index
     q = rng.uniform(-90, 90, (n, 4)).astype(np.float32)
-    q[: min(n, 5)] = tgt[: min(n, 5)]
+    k = min(n, m, 5)
+    q[:k] = tgt[:k]
     gi, gd = gpu_ctx.nearest(q, tgt)
     oi, od = oracle_mod.nearest(q, tgt, oracle_mod.NN_BRUTE)
     assert (gi == oi).all() and (gd == od).all()
