@@ -63,7 +63,8 @@ def cpu_baseline(src, tgt, iters: int, budget_s: float) -> dict:
 
     done, t0 = 0, time.perf_counter()
     while done < len(src) and (time.perf_counter() - t0) < budget_s:
-        oracle.align(src[done], tgt[done], numerics=oracle.NUM_F32, max_iterations=iters, mse_threshold_absolute=-1.0)
+        oracle.align(src[done], tgt[done], numerics=oracle.NUM_F32, max_iterations=iters, mse_threshold_absolute=-1.0,
+                     transformation_epsilon=-1.0)
         done += 1
     dt = time.perf_counter() - t0
     cpu = "unknown"
@@ -110,7 +111,8 @@ def main():
     gathered = torch.zeros((world * P, 96), dtype=torch.uint8, device=dev)
 
     ctx = icp4r.Context(dev.index)
-    params = icp4r.default_params(max_iterations=args.iters, mse_threshold_absolute=-1.0)
+    # fixed work: 20 iterations for every pair (the |ΔMSE| and exact-identity stops disabled)
+    params = icp4r.default_params(max_iterations=args.iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
                         tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
                         max_src_n=n, max_tgt_n=n)
@@ -144,7 +146,11 @@ def main():
 
     # result check (outside the timed region): statuses, iteration counts, and pairs vs the oracle
     res = np.frombuffer(results.cpu().numpy().tobytes(), dtype=icp4r.RESULT_DTYPE)
-    ok = bool((res["status"] == 0).all() and (res["iterations"] == args.iters).all())
+    status_ok = bool((res["status"] == 0).all())
+    iters_ok = bool((res["iterations"] == args.iters).all())
+    diag = {"status_nonzero": int((res["status"] != 0).sum()), "iter_min": int(res["iterations"].min()),
+            "iter_max": int(res["iterations"].max()), "conv_states": sorted(set(int(v) for v in res["convergence_state"]))}
+    ok = status_ok and iters_ok
     check = []
     if rank == 0 and args.check > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -152,13 +158,14 @@ def main():
 
         for k in range(min(args.check, P)):
             o = oracle.align(src_h[k], tgt_h[k], numerics=oracle.NUM_F32, max_iterations=args.iters,
-                             mse_threshold_absolute=-1.0)
+                             mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
             T = res[k]["T"].reshape(4, 4).T.astype(np.float64)
             To = o["T"].astype(np.float64)
             M = T[:3, :3].T @ To[:3, :3]
             dr = float(np.arctan2(np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2,
                                   (np.trace(M) - 1) / 2))
-            check.append({"pair": k, "dt_m": float(np.abs(T[:3, 3] - To[:3, 3]).max()), "dr_rad": dr})
+            check.append({"pair": k, "dt_m": float(np.abs(T[:3, 3] - To[:3, 3]).max()), "dr_rad": dr,
+                          "bit_exact": bool((res[k]["T"].reshape(4, 4).T == o["T"]).all())})
         ok = ok and all(c["dt_m"] <= 1e-4 and c["dr_rad"] <= 1e-4 for c in check)
 
     total_pairs = world * P * args.steps
@@ -220,6 +227,7 @@ def main():
             "batch_device_ms": batch_ms,
             "parity_ok": ok,
             "parity_check": check,
+            "result_diag": diag,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

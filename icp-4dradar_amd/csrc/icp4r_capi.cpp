@@ -94,11 +94,13 @@ struct Plan {
 
 // Geometry of the NN sweep: Q queries per lane (fewer when pairs are few, so the grid still fills
 // 256 CUs), then split the target range until there are >= 2048 workgroups (8 per CU) while each
-// split keeps >= 256 targets.  Batches of 8k-point pairs end up at Q = 16, one split.
+// split keeps >= 256 targets.  Batches of 8k-point pairs end up at Q = 4, one split.  Q = 4 scalar
+// measured fastest on MI355X (tools/tune_sweep.py, profiles/tune_r01.jsonl): v_pk_*_f32 packing
+// gave nothing (same FP32 rate per FLOP on gfx950), larger Q lost occupancy.
 Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
     const int64_t want = 2048;
     Plan pl;
-    pl.q = kMaxQ;
+    pl.q = kDefaultQ;
     // tuning override (tools/tune_sweep.py): ICP4R_NN_Q=1|2|4|8|16 caps the queries per lane
     if (const char* e = getenv("ICP4R_NN_Q")) {
         const int v = atoi(e);
@@ -110,7 +112,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
     while ((int64_t)npairs * qblocks(pl.q) * pl.splits < want && max_m / (pl.splits * 2) >= 256 && pl.splits < 64)
         pl.splits *= 2;
     pl.blocks = (int64_t)npairs * qblocks(pl.q) * pl.splits;
-    pl.packed = nn_mode != ICP4R_NN_BRUTE && pl.q >= 2;
+    pl.packed = nn_mode == ICP4R_NN_BRUTE_PACKED && pl.q >= 2;
     return pl;
 }
 
@@ -564,6 +566,20 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t* q,
     if (q) *q = pl.q;
     if (splits) *splits = pl.splits;
     if (nn_blocks) *nn_blocks = pl.blocks;
+    return ICP4R_OK;
+}
+
+// Internal test hook (not part of the public ABI in icp4r.h): the device float Umeyama rotation of
+// k row-major 3x3 matrices, host buffers.
+int icp4r__test_rot_f32(icp4r_ctx* ctx, const float* sigma, float* R, int32_t k) {
+    if (!ctx || !sigma || !R || k <= 0) return fail(ICP4R_E_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(ctx->T.ensure((size_t)k * 9 * 4 * 2));
+    float* d = static_cast<float*>(ctx->T.p);
+    HIP_TRY(hipMemcpyAsync(d, sigma, (size_t)k * 36, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_rot_f32(d, d + 9 * (size_t)k, k, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(R, d + 9 * (size_t)k, (size_t)k * 36, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     return ICP4R_OK;
 }
 

@@ -10,7 +10,8 @@
 namespace icp4r {
 
 constexpr int kNNWG = 256;        // threads per NN workgroup (4 waves)
-constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_kernel
+constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_kernel (instantiated)
+constexpr int kDefaultQ = 4;      // default cap (tools/tune_sweep.py)
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential centroid fold
 
 constexpr int kNumericsPCL = ICP4R_NUMERICS_PCL;
@@ -81,6 +82,7 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
+hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);
 hipError_t launch_nn_query(const float4* q, int n, const float4* tgt, int m, const float* T, int32_t* idx, float* d2,
                            hipStream_t st);
 

@@ -290,21 +290,25 @@ constexpr int kUpdWaves = kUpdWG / 64;
 constexpr int kFoldCh = 7;  // fold chains: s.xyz, d.xyz, weight (== validity when unweighted)
 
 template <int NUM> struct MomLayout;
-template <> struct MomLayout<kNumericsPCL> {  // Σ w·(d-μd)(s-μs)ᵀ [9], Σ d², |C|
-    static constexpr int N = 11, MSE = 9, CNT = 10;
+template <> struct MomLayout<kNumericsPCL> {  // |C| only: every other sum is a sequential fold
+    static constexpr int N = 1, CNT = 0;
 };
 template <> struct MomLayout<kNumericsF64> {  // Σ w·d·sᵀ [9], Σ w·s [3], Σ w·d [3], Σ w, Σ d², |C|
     static constexpr int N = 18, MSE = 16, CNT = 17;
 };
 
 struct UpdShared {
-    float fold[kFoldCh][kFoldChunk];
+    float fold[kFoldCh + 2][kFoldChunk];  // pass A: 7 float chains; pass B: s'xyz, d'xyz, w
+    double dfold[kFoldChunk];             // pass A: d² (MSE chain, double)
     double red[kUpdWaves * 20];
     double mom[20];
     double sigma[9], ms[3], md[3];
     SvdWork svd;
+    SvdWorkF svdf;
+    float sigmaf[9];
     float mean[6];
     float one_over_n;
+    double mse_sum;
     float T_inc[16];
     int32_t flag;  // 0 continue, 1 error (no transform), 2 converged after this transform
 };
@@ -312,7 +316,7 @@ struct UpdShared {
 // Thread 0: count check, Umeyama solve, final := T_inc * final, hasConverged (all in LDS/state).
 template <int NUM>
 __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
-    constexpr int I_MSE = MomLayout<NUM>::MSE, I_CNT = MomLayout<NUM>::CNT;
+    constexpr int I_CNT = MomLayout<NUM>::CNT;
     const int cnt = (int)sh.mom[I_CNT];
     st.ncorr = cnt;
     if (cnt < kp.min_corr) {
@@ -325,19 +329,20 @@ __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
     }
     float* Tinc = sh.T_inc;
     mat4_identity(Tinc);
+    double mse;
     if constexpr (NUM == kNumericsPCL) {
-        // sigma = one_over_n * Σ (d - μd)(s - μs)ᵀ ; R rounded to float (Matrix4f); t in float:
-        // Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean        (Eigen umeyama, Scalar = float)
-        const double oon = (double)sh.one_over_n;
-        for (int k = 0; k < 9; ++k) sh.sigma[k] = sh.mom[k] * oon;
-        umeyama_rotation(sh.sigma, sh.svd);
+        // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (the fold above), float SVD,
+        // R as Matrix4f, Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean.
+        for (int k = 0; k < 9; ++k) sh.sigmaf[k] = sh.one_over_n * sh.sigmaf[k];
+        umeyama_rotation_f32(sh.sigmaf, sh.svdf);
         for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) Tinc[j * 4 + i] = (float)sh.svd.R[i * 3 + j];
-            float rs = Tinc[0 * 4 + i] * sh.mean[0];
-            rs = Tinc[1 * 4 + i] * sh.mean[1] + rs;
-            rs = Tinc[2 * 4 + i] * sh.mean[2] + rs;
+            for (int j = 0; j < 3; ++j) Tinc[j * 4 + i] = sh.svdf.R[i * 3 + j];
+            float rs = sh.svdf.R[i * 3 + 0] * sh.mean[0];
+            rs = sh.svdf.R[i * 3 + 1] * sh.mean[1] + rs;
+            rs = sh.svdf.R[i * 3 + 2] * sh.mean[2] + rs;
             Tinc[12 + i] = sh.mean[3 + i] - rs;
         }
+        mse = sh.mse_sum / (double)cnt;  // calculateMSE: sequential double sum / |C|
     } else {
         const double sw = sh.mom[15];
         for (int k = 0; k < 3; ++k) {
@@ -352,11 +357,11 @@ __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
             for (int j = 0; j < 3; ++j) Tinc[j * 4 + i] = (float)R[i * 3 + j];
             Tinc[12 + i] = (float)(sh.md[i] - (R[i * 3 + 0] * sh.ms[0] + R[i * 3 + 1] * sh.ms[1] + R[i * 3 + 2] * sh.ms[2]));
         }
+        mse = sh.mom[MomLayout<kNumericsF64>::MSE] / (double)cnt;
     }
     for (int k = 0; k < 16; ++k) st.T_inc[k] = Tinc[k];
     mat4_mul_f(Tinc, st.final_T, st.final_T);  // final_transformation_ = transformation_ * final
     st.iterations += 1;
-    const double mse = sh.mom[I_MSE] / (double)cnt;
     ConvState cs;
     cs.prev_mse = st.prev_mse;
     cs.similar = st.similar;
@@ -372,7 +377,7 @@ __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
 template <int NUM>
 __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) {
     constexpr int NM = MomLayout<NUM>::N;
-    constexpr int I_MSE = MomLayout<NUM>::MSE, I_CNT = MomLayout<NUM>::CNT;
+    constexpr int I_CNT = MomLayout<NUM>::CNT;
     __shared__ UpdShared sh;
     const int p = blockIdx.x;
     PairState& st = w.state[p];
@@ -390,18 +395,26 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
     for (int k = 0; k < NM; ++k) mom[k] = 0.0;
 
     if constexpr (NUM == kNumericsPCL) {
-        // (1) centroids: the sequential float fold Eigen 3.3's rowwise().sum() performs, in
-        //     correspondence (= source index) order.  Rejected correspondences contribute +0.0f,
-        //     which leaves a float fold unchanged.  LDS chunks; lane c of wave 0 owns chain c.
-        float acc = 0.0f;
+        // Bit-exact float restatement of TransformationEstimationSVD (use_umeyama, Scalar = float)
+        // and calculateMSE: every sum is the sequential fold the reference performs, in
+        // correspondence (= source index) order, by one lane per chain of wave 0 over LDS chunks.
+        //  pass A: Σs, Σd (Eigen 3.3 rowwise().sum(): fold from the first element == fold from -0.0f;
+        //          Huber: fold of w·x from +0), Σw (== |C| unweighted), Σd² in double (MSE).
+        //  pass B: Σ d'_a s'_b (sigma, float, from +0) over the float-demeaned points.
+        // Rejected correspondences contribute the fold's identity (-0.0f / +0), i.e. nothing.
         const int lane = tid & 63, wave = tid >> 6;
+        const float ident = weighted ? 0.0f : -0.0f;
+        float acc = (lane < 6) ? ident : 0.0f;
+        double dacc = 0.0;
+        double cntd = 0.0;
         for (int base = 0; base < n; base += kFoldChunk) {
             for (int o = tid; o < kFoldChunk && base + o < n; o += kUpdWG) {
                 const int i = base + o;
                 float d2;
                 int j;
                 merge_nn(w, slot0 + i, d2, j);
-                float wt = 0.f, sx = 0.f, sy = 0.f, sz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
+                float wt = 0.f, sx = ident, sy = ident, sz = ident, dx = ident, dy = ident, dz = ident;
+                double dd = 0.0;
                 if (!(d2 > kp.max_d2)) {
                     const float4 s = X[i];
                     const float4 d = tgt[j];
@@ -414,32 +427,32 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
                         sx = s.x; sy = s.y; sz = s.z;
                         dx = d.x; dy = d.y; dz = d.z;
                     }
+                    dd = (double)d2;
+                    cntd += 1.0;
                 }
                 sh.fold[0][o] = sx; sh.fold[1][o] = sy; sh.fold[2][o] = sz;
                 sh.fold[3][o] = dx; sh.fold[4][o] = dy; sh.fold[5][o] = dz;
                 sh.fold[6][o] = wt;
+                sh.dfold[o] = dd;
             }
             __syncthreads();
-            if (wave == 0 && lane < kFoldCh) {
+            if (wave == 0 && lane < 8) {
                 const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
-                const float* f = sh.fold[lane];
-                int k = 0;
-                for (; k + 4 <= len; k += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(f + k);
-                    acc = acc + v.x;
-                    acc = acc + v.y;
-                    acc = acc + v.z;
-                    acc = acc + v.w;
+                if (lane < kFoldCh) {
+                    const float* f = sh.fold[lane];
+                    for (int k = 0; k < len; ++k) acc = acc + f[k];
+                } else {
+                    for (int k = 0; k < len; ++k) dacc = dacc + sh.dfold[k];
                 }
-                for (; k < len; ++k) acc = acc + f[k];
             }
             __syncthreads();
         }
+        mom[I_CNT] = cntd;
         if (wave == 0 && lane < kFoldCh) sh.fold[lane][0] = acc;
+        if (wave == 0 && lane == 7) sh.mse_sum = dacc;
         __syncthreads();
         if (tid == 0) {
-            // unweighted: one_over_n = 1/(float)n, n = |C| (the fold of 1.0f is exact);
-            // Huber: 1/Σw (float fold) — as oracle/icp_oracle.c umeyama_f32.
+            // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
             const float one_over_n = 1.0f / sh.fold[6][0];
             sh.one_over_n = one_over_n;
             for (int c = 0; c < 6; ++c) sh.mean[c] = sh.fold[c][0] * one_over_n;
@@ -447,23 +460,41 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
         __syncthreads();
         const float msx = sh.mean[0], msy = sh.mean[1], msz = sh.mean[2];
         const float mdx = sh.mean[3], mdy = sh.mean[4], mdz = sh.mean[5];
-        // (2) cross-covariance of the float-demeaned points, summed in double
-        for (int i = tid; i < n; i += kUpdWG) {
-            float d2;
-            int j;
-            merge_nn(w, slot0 + i, d2, j);
-            if (d2 > kp.max_d2) continue;
-            const float4 s = X[i];
-            const float4 d = tgt[j];
-            const double wt = weighted ? (double)(float)huber_w(d2, kp.huber_delta) : 1.0;
-            const double s0 = (double)(s.x - msx), s1 = (double)(s.y - msy), s2 = (double)(s.z - msz);
-            const double w0 = wt * (double)(d.x - mdx), w1 = wt * (double)(d.y - mdy), w2 = wt * (double)(d.z - mdz);
-            mom[0] += w0 * s0; mom[1] += w0 * s1; mom[2] += w0 * s2;
-            mom[3] += w1 * s0; mom[4] += w1 * s1; mom[5] += w1 * s2;
-            mom[6] += w2 * s0; mom[7] += w2 * s1; mom[8] += w2 * s2;
-            mom[I_MSE] += (double)d2;
-            mom[I_CNT] += 1.0;
+        float sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b)
+        const int ca = lane / 3, cb = lane % 3;
+        for (int base = 0; base < n; base += kFoldChunk) {
+            for (int o = tid; o < kFoldChunk && base + o < n; o += kUpdWG) {
+                const int i = base + o;
+                float d2;
+                int j;
+                merge_nn(w, slot0 + i, d2, j);
+                float wt = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, d0 = 0.f, d1 = 0.f, dv2 = 0.f;
+                if (!(d2 > kp.max_d2)) {
+                    const float4 s = X[i];
+                    const float4 d = tgt[j];
+                    s0 = s.x - msx; s1 = s.y - msy; s2 = s.z - msz;
+                    d0 = d.x - mdx; d1 = d.y - mdy; dv2 = d.z - mdz;
+                    wt = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
+                }
+                sh.fold[0][o] = s0; sh.fold[1][o] = s1; sh.fold[2][o] = s2;
+                sh.fold[3][o] = d0; sh.fold[4][o] = d1; sh.fold[5][o] = dv2;
+                sh.fold[6][o] = wt;
+            }
+            __syncthreads();
+            if (wave == 0 && lane < 9) {
+                const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
+                const float* fa = sh.fold[3 + ca];
+                const float* fb = sh.fold[cb];
+                if (weighted) {
+                    const float* fw = sh.fold[6];
+                    for (int k = 0; k < len; ++k) sacc = sacc + fw[k] * fa[k] * fb[k];
+                } else {
+                    for (int k = 0; k < len; ++k) sacc = fa[k] * fb[k] + sacc;
+                }
+            }
+            __syncthreads();
         }
+        if (wave == 0 && lane < 9) sh.sigmaf[lane] = sacc;
     } else {
         for (int i = tid; i < n; i += kUpdWG) {
             float d2;
@@ -481,7 +512,7 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
             mom[9] += wt * s0; mom[10] += wt * s1; mom[11] += wt * s2;
             mom[12] += w0; mom[13] += w1; mom[14] += w2;
             mom[15] += wt;
-            mom[I_MSE] += (double)d2;
+            mom[MomLayout<kNumericsF64>::MSE] += (double)d2;
             mom[I_CNT] += 1.0;
         }
     }
@@ -523,26 +554,35 @@ __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs 
 // finish_kernel: fitness = mean of d² over d² <= max_range (double), results, aligned output.
 constexpr int kFinWG = 256;
 __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) {
-    __shared__ double red[(kFinWG / 64) * 2];
-    __shared__ double tot[2];
     const int p = blockIdx.x;
     const PairState& st = w.state[p];
     const int n = a.src_n[p];
     const int64_t slot0 = (int64_t)p * w.x_stride;
     const bool have = st.phase != kPhaseInvalid && a.kp.compute_fitness && n > 0;
-    double f[2] = {0.0, 0.0};
+    // Registration::getFitnessScore: sequential double sum over points with d² <= max_range, in
+    // index order (one lane over LDS chunks), so the score is bit-identical to the reference loop.
+    __shared__ double chunk[kFoldChunk];
+    double fsum = 0.0, fcnt = 0.0;
     if (have) {
-        for (int i = threadIdx.x; i < n; i += kFinWG) {
-            float d2;
-            int j;
-            merge_nn(w, slot0 + i, d2, j);
-            if ((double)d2 <= a.kp.fit_max_range) {
-                f[0] += (double)d2;
-                f[1] += 1.0;
+        for (int base = 0; base < n; base += kFoldChunk) {
+            for (int o = threadIdx.x; o < kFoldChunk && base + o < n; o += kFinWG) {
+                float d2;
+                int j;
+                merge_nn(w, slot0 + base + o, d2, j);
+                chunk[o] = ((double)d2 <= a.kp.fit_max_range) ? (double)d2 : -1.0;
             }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
+                for (int k = 0; k < len; ++k)
+                    if (chunk[k] >= 0.0) {
+                        fsum = fsum + chunk[k];
+                        fcnt += 1.0;
+                    }
+            }
+            __syncthreads();
         }
     }
-    block_sum<2, kFinWG / 64>(f, red, tot);
     if (a.aligned && st.phase != kPhaseInvalid) {
         const float4* src = a.src + a.src_off[p];
         const float4* X = w.X + (int64_t)p * w.x_stride;
@@ -556,7 +596,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     if (threadIdx.x == 0) {
         Result r;
         for (int k = 0; k < 16; ++k) r.T[k] = st.final_T[k];
-        r.fitness = (have && tot[1] > 0) ? tot[0] / tot[1] : DBL_MAX;
+        r.fitness = (have && fcnt > 0) ? fsum / fcnt : DBL_MAX;
         r.iterations = st.iterations;
         r.converged = st.phase == kPhaseConverged ? 1 : 0;
         r.status = st.status;
@@ -592,6 +632,20 @@ __global__ __launch_bounds__(256) void nn_query_kernel(const float4* __restrict_
         idx[i] = bi[0];
         d2[i] = best[0];
     }
+}
+
+// Test hook: the device float Umeyama rotation for k sigma matrices (one thread each).
+__global__ void rot_f32_kernel(const float* sigma, float* R, int k) {
+    __shared__ SvdWorkF ws[64];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= k) return;
+    umeyama_rotation_f32(sigma + 9 * i, ws[threadIdx.x]);
+    for (int e = 0; e < 9; ++e) R[9 * i + e] = ws[threadIdx.x].R[e];
+}
+
+hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st) {
+    hipLaunchKernelGGL(rot_f32_kernel, dim3((k + 63) / 64), dim3(64), 0, st, sigma, R, k);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

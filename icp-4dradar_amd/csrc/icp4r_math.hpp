@@ -159,9 +159,11 @@ __device__ inline void svd3(const double* A, SvdWork& w) {
         U[1 * 3 + 1] = c1 / nn;
         U[2 * 3 + 1] = c2 / nn;
     }
-    U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
-    U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
-    U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+    if (rank <= 2) {  // complete U only when sigma is rank-deficient
+        U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
+        U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
+        U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+    }
 }
 
 __device__ inline double det3(const double* M) {
@@ -175,6 +177,125 @@ __device__ inline void umeyama_rotation(const double* sigma, SvdWork& w) {
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)
             w.R[i * 3 + j] = w.U[i * 3 + 0] * w.V[j * 3 + 0] + w.U[i * 3 + 1] * w.V[j * 3 + 1] + d2 * w.U[i * 3 + 2] * w.V[j * 3 + 2];
+}
+
+// ---- 3x3 SVD + Umeyama rotation in FLOAT (PCL numerics) -------------------------------------
+// Same one-sided Jacobi as svd3() with every operation in float and in the operation order of
+// oracle/icp_oracle.c svd3_f32 / rot_f32 / det3_f32, so the rotation the PCL-numerics path produces
+// is bit-identical to the float restatement of PCL's TransformationEstimationSVD (Scalar = float).
+// float '/' and sqrtf are correctly rounded on the device (HIP default), like SSE on the host.
+struct SvdWorkF {
+    float W[9], V[9], U[9], S[3], Vs[9], Ws[9], R[9];
+    int ord[3];
+};
+
+__host__ __device__ inline void svd3_f32(const float* A, SvdWorkF& w) {
+    float* W = w.W;
+    float* V = w.V;
+    float* U = w.U;
+    float* S = w.S;
+    for (int k = 0; k < 9; ++k) W[k] = A[k];
+    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+#pragma nounroll
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        float off = 0;
+#pragma nounroll
+        for (int r = 0; r < 3; ++r) {
+            const int p = r == 2 ? 1 : 0, q = r == 0 ? 1 : 2;
+            float al = 0, be = 0, ga = 0;
+            for (int k = 0; k < 3; ++k) {
+                al += W[k * 3 + p] * W[k * 3 + p];
+                be += W[k * 3 + q] * W[k * 3 + q];
+                ga += W[k * 3 + p] * W[k * 3 + q];
+            }
+            if (ga == 0) continue;
+            float nrm = sqrtf(al * be);
+            if (nrm == 0) continue;
+            float rel = fabsf(ga) / nrm;
+            if (rel > off) off = rel;
+            if (rel <= 1e-7f) continue;
+            float zeta = (be - al) / (2 * ga);
+            float t = (zeta >= 0 ? 1.0f : -1.0f) / (fabsf(zeta) + sqrtf(1.0f + zeta * zeta));
+            float c = 1.0f / sqrtf(1.0f + t * t);
+            float s = c * t;
+            for (int k = 0; k < 3; ++k) {
+                float wp = W[k * 3 + p], wq = W[k * 3 + q];
+                W[k * 3 + p] = c * wp - s * wq;
+                W[k * 3 + q] = s * wp + c * wq;
+                float vp = V[k * 3 + p], vq = V[k * 3 + q];
+                V[k * 3 + p] = c * vp - s * vq;
+                V[k * 3 + q] = s * vp + c * vq;
+            }
+        }
+        if (off <= 1e-7f) break;
+    }
+    float sv[3];
+    for (int c = 0; c < 3; ++c)
+        sv[c] = sqrtf(W[0 * 3 + c] * W[0 * 3 + c] + W[1 * 3 + c] * W[1 * 3 + c] + W[2 * 3 + c] * W[2 * 3 + c]);
+    int* ord = w.ord;
+    for (int c = 0; c < 3; ++c) ord[c] = c;
+    for (int i = 0; i < 3; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (sv[ord[j]] > sv[ord[i]]) {
+                int tt = ord[i];
+                ord[i] = ord[j];
+                ord[j] = tt;
+            }
+    for (int c = 0; c < 3; ++c) {
+        S[c] = sv[ord[c]];
+        for (int k = 0; k < 3; ++k) {
+            w.Vs[k * 3 + c] = V[k * 3 + ord[c]];
+            w.Ws[k * 3 + c] = W[k * 3 + ord[c]];
+        }
+    }
+    for (int k = 0; k < 9; ++k) V[k] = w.Vs[k];
+    int rank = 0;
+    for (int c = 0; c < 3; ++c)
+        if (S[c] > 1e-6f * (S[0] > 0 ? S[0] : 1.0f) && S[c] > 0) rank = c + 1;
+    for (int c = 0; c < rank; ++c)
+        for (int k = 0; k < 3; ++k) U[k * 3 + c] = w.Ws[k * 3 + c] / S[c];
+    if (rank == 0) {
+        for (int k = 0; k < 9; ++k) U[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+        return;
+    }
+    if (rank == 1) {
+        int ax = 0;
+        float amin = fabsf(U[0]);
+        for (int k = 1; k < 3; ++k)
+            if (fabsf(U[k * 3]) < amin) {
+                amin = fabsf(U[k * 3]);
+                ax = k;
+            }
+        const float e0 = ax == 0 ? 1.0f : 0.0f, e1 = ax == 1 ? 1.0f : 0.0f, e2 = ax == 2 ? 1.0f : 0.0f;
+        float c0 = U[1 * 3] * e2 - U[2 * 3] * e1;
+        float c1 = U[2 * 3] * e0 - U[0 * 3] * e2;
+        float c2 = U[0 * 3] * e1 - U[1 * 3] * e0;
+        float nn = sqrtf(c0 * c0 + c1 * c1 + c2 * c2);
+        U[0 * 3 + 1] = c0 / nn;
+        U[1 * 3 + 1] = c1 / nn;
+        U[2 * 3 + 1] = c2 / nn;
+    }
+    if (rank <= 2) {  // complete U only when sigma is rank-deficient
+        U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
+        U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
+        U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+    }
+}
+
+__host__ __device__ inline float det3_f32(const float* M) {
+    return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+__host__ __device__ inline void umeyama_rotation_f32(const float* sigma, SvdWorkF& w) {
+    svd3_f32(sigma, w);
+    float d[3] = {1.0f, 1.0f, 1.0f};
+    if (det3_f32(w.U) * det3_f32(w.V) < 0) d[2] = -1.0f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0;
+            for (int k = 0; k < 3; ++k) acc += w.U[i * 3 + k] * d[k] * w.V[j * 3 + k];
+            w.R[i * 3 + j] = acc;
+        }
 }
 
 // ---- convergence: DefaultConvergenceCriteria<float>::hasConverged ------------------------------

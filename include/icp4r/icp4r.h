@@ -55,10 +55,10 @@ typedef enum icp4r_convergence_state {
 } icp4r_convergence_state;
 
 /* Umeyama arithmetic.
- * PCL: centroids by the sequential float fold Eigen 3.3 performs (bit-identical to PCL when
- *      the correspondences are), cross-covariance of the float-demeaned points summed in double,
- *      3x3 SVD in double, R and t rounded to float as Matrix4f.  Matches PCL's float ICP to
- *      ~1e-6 m: the default, and what the ≤1e-4 parity bar is stated against.
+ * PCL: PCL's Scalar = float Umeyama restated operation by operation: centroids and the 3x3
+ *      cross-covariance as the sequential float folds Eigen 3.3 performs, float one-sided Jacobi
+ *      SVD, R and t as Matrix4f, MSE and fitness as sequential double sums.  Bit-identical to the
+ *      float restatement in oracle/ (tests assert equal bits); the default.
  * F64: every moment summed in double (more accurate than PCL; differs from it by PCL's own
  *      float-centroid noise, up to ~2e-4 m on 8k-point clouds). */
 typedef enum icp4r_numerics { ICP4R_NUMERICS_PCL = 0, ICP4R_NUMERICS_F64 = 1 } icp4r_numerics;
@@ -66,7 +66,7 @@ typedef enum icp4r_numerics { ICP4R_NUMERICS_PCL = 0, ICP4R_NUMERICS_F64 = 1 } i
 /* Correspondence search.  All modes return the exact nearest neighbour under FLANN's
  * L2_Simple<float> distance ((dx*dx + dy*dy) + dz*dz, float, unfused); ties -> lowest index. */
 typedef enum icp4r_nn_mode {
-    ICP4R_NN_AUTO = 0,         /* pick per shape (currently ICP4R_NN_BRUTE_PACKED)                   */
+    ICP4R_NN_AUTO = 0,         /* pick per shape (currently ICP4R_NN_BRUTE)                          */
     ICP4R_NN_BRUTE = 1,        /* exhaustive scan, target streamed through the scalar cache, FP32    */
     ICP4R_NN_BRUTE_PACKED = 2  /* same scan, two queries per v_pk_{add,mul}_f32 (identical results) */
 } icp4r_nn_mode;

@@ -833,3 +833,6 @@ int oracle_align(const float* src, int32_t n, int32_t src_stride, const float* t
     free(X); free(cq); free(cm); free(cd);
     return status;
 }
+
+/* test hook: the float Umeyama rotation of a 3x3 sigma (row-major) */
+void oracle_rot_f32(const float* sigma, float* R) { rot_f32(sigma, R); }

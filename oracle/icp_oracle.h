@@ -90,6 +90,9 @@ double oracle_fitness(const float* src, int32_t n, int32_t src_stride,
                       const float* tgt, int32_t m, int32_t tgt_stride,
                       const float* T_colmajor, double max_range, int32_t nn_mode);
 
+/* Test hook: float Umeyama rotation R = U diag(1,1,s) V^T of a row-major 3x3 sigma. */
+void oracle_rot_f32(const float* sigma, float* R);
+
 /* Statistics of the last kd-tree search (for the CPU-baseline report). */
 int64_t oracle_kdtree_leaf_visits(void);
 

@@ -69,7 +69,7 @@ def test_plan_geometry():
     import icp4r
 
     big = icp4r.plan(1024, 8192, 8192)
-    assert big["splits"] == 1 and big["q"] == 16
+    assert big["splits"] == 1 and big["q"] == 4
     single = icp4r.plan(1, 8192, 8192)
     assert single["splits"] > 1 and single["nn_blocks"] >= 512
     tiny = icp4r.plan(1, 10, 7)
@@ -90,3 +90,12 @@ def test_cpp_facade_compiles():
     against the library (running it needs the GPU: tests/test_gpu_parity.py)."""
     r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_device_float_umeyama_matches_oracle_on_host():
+    """icp4r_math.hpp's float SVD/rotation compiled for the host == the oracle's, bit for bit."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "_build", "svd_host_check")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout

@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--points", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--qs", default="16,8,4")
+    ap.add_argument("--qs", default="8,4,2,1")
     ap.add_argument("--child", action="store_true")
     args = ap.parse_args()
     if args.child:
