@@ -98,10 +98,11 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     import icp4r
+    from icp4r import dist as idist
 
     n = args.points
     P = args.pairs
-    first = rank * P
+    first = idist.shard(rank, world, P).start
     src_h, tgt_h = make_shard(first, P, n)
     src = torch.from_numpy(src_h.reshape(-1, 4)).to(dev)
     tgt = torch.from_numpy(tgt_h.reshape(-1, 4)).to(dev)
@@ -121,7 +122,7 @@ def main():
     def step():
         ctx.align_batch_device(batch, params, results.data_ptr(), stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, results)
+            idist.gather_results(results, world, out=gathered)
 
     for _ in range(args.warmup):
         step()
