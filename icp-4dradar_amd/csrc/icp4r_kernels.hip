@@ -283,6 +283,82 @@ __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int f
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sequential folds over an LDS chunk, one lane per chain.  The order of the additions is exactly
+// the reference loop's; the loads are issued 16 ahead (ds_read_b128) so the chain runs at the
+// dependent-add latency instead of the LDS round trip per element.
+__device__ __forceinline__ float fold_f32(const float* f, int len, float acc) {
+    int k = 0;
+    for (; k + 16 <= len; k += 16) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(f + k + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc = acc + v[u].x;
+            acc = acc + v[u].y;
+            acc = acc + v[u].z;
+            acc = acc + v[u].w;
+        }
+    }
+    for (; k < len; ++k) acc = acc + f[k];
+    return acc;
+}
+
+__device__ __forceinline__ double fold_f64(const double* f, int len, double acc) {
+    int k = 0;
+    for (; k + 8 <= len; k += 8) {
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const double2*>(f + k + 2 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc = acc + v[u].x;
+            acc = acc + v[u].y;
+        }
+    }
+    for (; k < len; ++k) acc = acc + f[k];
+    return acc;
+}
+
+// sigma chain: acc = a*b + acc (oracle umeyama_f32, unweighted)
+__device__ __forceinline__ float fold_prod_f32(const float* fa, const float* fb, int len, float acc) {
+    int k = 0;
+    for (; k + 8 <= len; k += 8) {
+        float4 a[2], b[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            a[u] = *reinterpret_cast<const float4*>(fa + k + 4 * u);
+            b[u] = *reinterpret_cast<const float4*>(fb + k + 4 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            acc = a[u].x * b[u].x + acc;
+            acc = a[u].y * b[u].y + acc;
+            acc = a[u].z * b[u].z + acc;
+            acc = a[u].w * b[u].w + acc;
+        }
+    }
+    for (; k < len; ++k) acc = fa[k] * fb[k] + acc;
+    return acc;
+}
+
+// Huber sigma chain: acc = acc + (w*a)*b (oracle umeyama_f32, weighted)
+__device__ __forceinline__ float fold_wprod_f32(const float* fw, const float* fa, const float* fb, int len, float acc) {
+    int k = 0;
+    for (; k + 4 <= len; k += 4) {
+        const float4 w = *reinterpret_cast<const float4*>(fw + k);
+        const float4 a = *reinterpret_cast<const float4*>(fa + k);
+        const float4 b = *reinterpret_cast<const float4*>(fb + k);
+        acc = acc + w.x * a.x * b.x;
+        acc = acc + w.y * a.y * b.y;
+        acc = acc + w.z * a.z * b.z;
+        acc = acc + w.w * a.w * b.w;
+    }
+    for (; k < len; ++k) acc = acc + fw[k] * fa[k] * fb[k];
+    return acc;
+}
+
+// ---------------------------------------------------------------------------------------------
 // update_kernel<NUM>: one workgroup per active pair: correspondences -> moments -> solve ->
 // convergence -> X := T_inc * X (in place, float, PCL transformCloud order).
 constexpr int kUpdWG = 512;
@@ -439,10 +515,9 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
             if (wave == 0 && lane < 8) {
                 const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
                 if (lane < kFoldCh) {
-                    const float* f = sh.fold[lane];
-                    for (int k = 0; k < len; ++k) acc = acc + f[k];
+                    acc = fold_f32(sh.fold[lane], len, acc);
                 } else {
-                    for (int k = 0; k < len; ++k) dacc = dacc + sh.dfold[k];
+                    dacc = fold_f64(sh.dfold, len, dacc);
                 }
             }
             __syncthreads();
@@ -485,12 +560,10 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
                 const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
                 const float* fa = sh.fold[3 + ca];
                 const float* fb = sh.fold[cb];
-                if (weighted) {
-                    const float* fw = sh.fold[6];
-                    for (int k = 0; k < len; ++k) sacc = sacc + fw[k] * fa[k] * fb[k];
-                } else {
-                    for (int k = 0; k < len; ++k) sacc = fa[k] * fb[k] + sacc;
-                }
+                if (weighted)
+                    sacc = fold_wprod_f32(sh.fold[6], fa, fb, len, sacc);
+                else
+                    sacc = fold_prod_f32(fa, fb, len, sacc);
             }
             __syncthreads();
         }
@@ -574,7 +647,19 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
             __syncthreads();
             if (threadIdx.x == 0) {
                 const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
-                for (int k = 0; k < len; ++k)
+                int k = 0;
+                for (; k + 8 <= len; k += 8) {  // loads hoisted ahead of the dependent adds
+                    double v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = chunk[k + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (v[u] >= 0.0) {
+                            fsum = fsum + v[u];
+                            fcnt += 1.0;
+                        }
+                }
+                for (; k < len; ++k)
                     if (chunk[k] >= 0.0) {
                         fsum = fsum + chunk[k];
                         fcnt += 1.0;

@@ -76,8 +76,9 @@ def main():
         out["hbm_bytes_per_nn_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
         n, P = a.points, a.pairs
         out["algorithmic_bytes_per_nn_launch"] = P * (n * 16 + n * 16 + n * 8)  # X read, target read, (d2, idx) write
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-        json.dump(out, f, indent=1)
+    if a.fetch or a.write:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+            json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
