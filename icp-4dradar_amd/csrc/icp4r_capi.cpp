@@ -76,39 +76,58 @@ struct icp4r_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // staging for the host-buffer entry points
-    DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, idx, d2, T;
+    DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace
-    DevBuf X, nn_d2, nn_idx, state;
+    DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm;
     std::vector<EventPair> nn_events, batch_events;
     size_t nn_used = 0, batch_used = 0;
+    DevBuf evals;  // u64: distance evaluations of the NN kernels since the last reset
 };
 
 namespace {
 
 struct Plan {
     int q;
-    bool packed;  // v_pk_* FP32 sweep (two queries per register pair)
-    int splits;
+    bool packed;  // brute force: v_pk_* FP32 sweep (two queries per register pair)
+    int splits;   // brute force: target splits
+    bool pruned;  // Morton-block pruned exact search
+    int leaf;     // pruned: targets per block
     int64_t blocks;
 };
 
-// Geometry of the NN sweep: Q queries per lane (fewer when pairs are few, so the grid still fills
-// 256 CUs), then split the target range until there are >= 2048 workgroups (8 per CU) while each
-// split keeps >= 256 targets.  Batches of 8k-point pairs end up at Q = 4, one split.  Q = 4 scalar
-// measured fastest on MI355X (tools/tune_sweep.py, profiles/tune_r01.jsonl): v_pk_*_f32 packing
-// gave nothing (same FP32 rate per FLOP on gfx950), larger Q lost occupancy.
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+// Geometry of the NN pass.
+//  * pruned (ICP4R_NN_AUTO when the target has >= kPrunedMinM points, or ICP4R_NN_PRUNED): Q queries
+//    per lane, 64*Q Morton-contiguous queries per wave; Q shrinks while the grid has < 8192 waves
+//    (a single 8k pair runs at Q = 1: 128 waves), leaf = 16 targets per block.
+//  * brute force: Q queries per lane (fewer when pairs are few, so the grid still fills 256 CUs),
+//    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
+//    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/tune_sweep.py, profiles/tune_r01.jsonl).
+// Tuning overrides (tools/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
 Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
-    const int64_t want = 2048;
     Plan pl;
-    pl.q = kDefaultQ;
-    // tuning override (tools/tune_sweep.py): ICP4R_NN_Q=1|2|4|8|16 caps the queries per lane
-    if (const char* e = getenv("ICP4R_NN_Q")) {
-        const int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) pl.q = v;
-    }
-    auto qblocks = [&](int q) { return (int64_t)((max_n + kNNWG * q - 1) / (kNNWG * q)); };
-    while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) < want) pl.q /= 2;
+    pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
+    pl.packed = false;
     pl.splits = 1;
+    pl.leaf = 0;
+    const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
+    pl.q = (qcap == 1 || qcap == 2 || qcap == 4 || qcap == 8 || qcap == 16) ? qcap
+                                                                             : (pl.pruned ? kDefaultPrunedQ : kDefaultQ);
+    auto qblocks = [&](int q) { return (int64_t)((max_n + kNNWG * q - 1) / (kNNWG * q)); };
+    if (pl.pruned) {
+        if (pl.q > 4) pl.q = 4;
+        const int leaf = env_int("ICP4R_LEAF", kDefaultLeaf);
+        pl.leaf = (leaf == 16 || leaf == 32) ? leaf : kDefaultLeaf;
+        while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) * (kNNWG / 64) < 8192) pl.q /= 2;
+        pl.blocks = (int64_t)npairs * qblocks(pl.q);
+        return pl;
+    }
+    const int64_t want = 2048;
+    while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) < want) pl.q /= 2;
     while ((int64_t)npairs * qblocks(pl.q) * pl.splits < want && max_m / (pl.splits * 2) >= 256 && pl.splits < 64)
         pl.splits *= 2;
     pl.blocks = (int64_t)npairs * qblocks(pl.q) * pl.splits;
@@ -133,7 +152,8 @@ int make_kparams(const icp4r_params* p, KParams* kp) {
     if (p->max_iterations < 0) return fail(ICP4R_E_INVALID, "max_iterations must be >= 0");
     if (p->numerics != ICP4R_NUMERICS_PCL && p->numerics != ICP4R_NUMERICS_F64)
         return fail(ICP4R_E_INVALID, "unknown numerics mode %d", p->numerics);
-    if (p->nn_mode != ICP4R_NN_AUTO && p->nn_mode != ICP4R_NN_BRUTE && p->nn_mode != ICP4R_NN_BRUTE_PACKED)
+    if (p->nn_mode != ICP4R_NN_AUTO && p->nn_mode != ICP4R_NN_BRUTE && p->nn_mode != ICP4R_NN_BRUTE_PACKED &&
+        p->nn_mode != ICP4R_NN_PRUNED)
         return fail(ICP4R_E_INVALID, "unknown nn_mode %d", p->nn_mode);
     if (!(p->huber_delta > 0)) return fail(ICP4R_E_INVALID, "huber_delta must be > 0 (+inf disables)");
     memset(kp, 0, sizeof(*kp));
@@ -183,50 +203,137 @@ int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
     return ICP4R_OK;
 }
 
+// Size the workspace for a plan and fill WorkArgs.
+int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, hipStream_t st, WorkArgs& w) {
+    const int64_t x_stride = ((max_n > 0 ? max_n : 1) + 3) & ~3;
+    const int64_t slots = (int64_t)npairs * x_stride;
+    HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
+    HIP_TRY(ctx->nn_key.ensure((size_t)slots * sizeof(NNKey)));
+    HIP_TRY(ctx->state.ensure((size_t)npairs * sizeof(PairState)));
+    memset(&w, 0, sizeof(w));
+    w.X = static_cast<float4*>(ctx->X.p);
+    w.nn_key = static_cast<NNKey*>(ctx->nn_key.p);
+    w.state = static_cast<PairState*>(ctx->state.p);
+    w.x_stride = x_stride;
+    w.splits = pl.splits;
+    if (!ctx->evals.p) {
+        HIP_TRY(ctx->evals.ensure(sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, sizeof(uint64_t), st));
+    }
+    w.evals = static_cast<unsigned long long*>(ctx->evals.p);
+    if (pl.pruned) {
+        const int64_t span = (int64_t)pl.leaf * kSuper;
+        w.leaf = pl.leaf;
+        w.t_stride = ((max_m > 0 ? max_m : 1) + span - 1) / span * span;
+        w.b_stride = w.t_stride / pl.leaf;
+        w.sb_stride = w.b_stride / kSuper;
+        HIP_TRY(ctx->tsort.ensure((size_t)npairs * w.t_stride * sizeof(float4)));
+        HIP_TRY(ctx->tinv.ensure((size_t)npairs * w.t_stride * sizeof(int32_t)));
+        HIP_TRY(ctx->tbox.ensure((size_t)npairs * 2 * w.b_stride * sizeof(float4)));
+        HIP_TRY(ctx->sbox.ensure((size_t)npairs * 2 * w.sb_stride * sizeof(float4)));
+        HIP_TRY(ctx->sperm.ensure((size_t)slots * sizeof(int32_t)));
+        w.tsort = static_cast<float4*>(ctx->tsort.p);
+        w.tinv = static_cast<int32_t*>(ctx->tinv.p);
+        w.tbox = static_cast<float4*>(ctx->tbox.p);
+        w.sbox = static_cast<float4*>(ctx->sbox.p);
+        w.sperm = static_cast<int32_t*>(ctx->sperm.p);
+    }
+    return ICP4R_OK;
+}
+
+// One NN pass over every active pair (timed with events: the roofline's kernel).
+int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
+            int fitness_pass, int first, hipStream_t st) {
+    EventPair* ne;
+    int r;
+    if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
+    HIP_TRY(hipEventRecord(ne->start, st));
+    if (pl.pruned) {
+        HIP_TRY(launch_nn_pruned(pl.q, a, w, npairs, max_n, fitness_pass, first, st));
+    } else {
+        if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));
+        HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n, fitness_pass, st));
+    }
+    HIP_TRY(hipEventRecord(ne->stop, st));
+    return ICP4R_OK;
+}
+
 // The whole registration of a device-resident batch as one stream-ordered launch sequence.
 int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m, int max_iterations,
               int nn_mode, hipStream_t st) {
     if (npairs <= 0) return ICP4R_OK;
-    const Plan pl = make_plan(npairs, max_n > 0 ? max_n : 1, max_m, nn_mode);
-    const int64_t x_stride = ((max_n > 0 ? max_n : 1) + 3) & ~3;
-    const int64_t slots = (int64_t)npairs * x_stride;
-    HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
-    HIP_TRY(ctx->nn_d2.ensure((size_t)slots * pl.splits * sizeof(float)));
-    HIP_TRY(ctx->nn_idx.ensure((size_t)slots * pl.splits * sizeof(int32_t)));
-    HIP_TRY(ctx->state.ensure((size_t)npairs * sizeof(PairState)));
+    const int mn = max_n > 0 ? max_n : 1;
+    const Plan pl = make_plan(npairs, mn, max_m, nn_mode);
     WorkArgs w;
-    w.X = static_cast<float4*>(ctx->X.p);
-    w.nn_d2 = static_cast<float*>(ctx->nn_d2.p);
-    w.nn_idx = static_cast<int32_t*>(ctx->nn_idx.p);
-    w.state = static_cast<PairState*>(ctx->state.p);
-    w.x_stride = x_stride;
-    w.slot_stride = slots;
-    w.splits = pl.splits;
-    EventPair* be;
     int rc;
+    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, st, w))) return rc;
+    EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
     HIP_TRY(launch_init(a, w, npairs, st));
+    if (pl.pruned) HIP_TRY(launch_index(a, w, npairs, st));
     // PCL's do { ... } while (!converged): at least one iteration even for max_iterations == 0.
     const int iters = max_iterations > 0 ? max_iterations : 1;
     for (int it = 0; it < iters; ++it) {
-        EventPair* ne;
-        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
-        HIP_TRY(hipEventRecord(ne->start, st));
-        HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n > 0 ? max_n : 1, 0, st));
-        HIP_TRY(hipEventRecord(ne->stop, st));
+        if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
         HIP_TRY(launch_update(a, w, npairs, st));
     }
     if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
-    if (a.kp.compute_fitness) {
-        EventPair* ne;
-        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
-        HIP_TRY(hipEventRecord(ne->start, st));
-        HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n > 0 ? max_n : 1, 1, st));
-        HIP_TRY(hipEventRecord(ne->stop, st));
-    }
+    if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, a, w, npairs, mn, 1, 0, st))) return rc;
     HIP_TRY(launch_finish(a, w, npairs, st));
     HIP_TRY(hipEventRecord(be->stop, st));
+    return ICP4R_OK;
+}
+
+// Exact 1-NN of n host queries (optionally transformed by T, column-major) in a host target: the
+// registration's own NN path (init = transformCloud(query, T); index; one NN pass), keys copied
+// back.  Used by icp4r_nearest and icp4r_fitness.
+int nearest_keys(icp4r_ctx* ctx, const float* query, int32_t n, int32_t qstride, const float* tgt, int32_t m,
+                 int32_t tstride, const float* T, std::vector<NNKey>& keys) {
+    std::vector<float> hq, ht;
+    pack_host(query, n, qstride, hq);
+    pack_host(tgt, m, tstride, ht);
+    hipStream_t st = ctx->stream;
+    const int64_t zero64 = 0;
+    HIP_TRY(ctx->src.ensure(hq.size() * 4));
+    HIP_TRY(ctx->tgt.ensure(ht.size() * 4));
+    HIP_TRY(ctx->src_off.ensure(16));
+    HIP_TRY(ctx->tgt_off.ensure(16));
+    HIP_TRY(ctx->src_n.ensure(16));
+    HIP_TRY(ctx->tgt_n.ensure(16));
+    HIP_TRY(ctx->guess.ensure(64));
+    HIP_TRY(ctx->results.ensure(sizeof(icp4r_result)));
+    HIP_TRY(hipMemcpyAsync(ctx->src.p, hq.data(), hq.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_n.p, &n, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_n.p, &m, 4, hipMemcpyHostToDevice, st));
+    if (T) HIP_TRY(hipMemcpyAsync(ctx->guess.p, T, 64, hipMemcpyHostToDevice, st));
+    PairArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = static_cast<const float4*>(ctx->src.p);
+    a.tgt = static_cast<const float4*>(ctx->tgt.p);
+    a.src_off = static_cast<const int64_t*>(ctx->src_off.p);
+    a.tgt_off = static_cast<const int64_t*>(ctx->tgt_off.p);
+    a.src_n = static_cast<const int32_t*>(ctx->src_n.p);
+    a.tgt_n = static_cast<const int32_t*>(ctx->tgt_n.p);
+    a.guess = T ? static_cast<const float*>(ctx->guess.p) : nullptr;
+    a.results = static_cast<Result*>(ctx->results.p);
+    int rc;
+    if ((rc = make_kparams(nullptr, &a.kp))) return rc;
+    const Plan pl = make_plan(1, n, m, ICP4R_NN_AUTO);
+    WorkArgs w;
+    if ((rc = setup_work(ctx, pl, 1, n, m, st, w))) return rc;
+    HIP_TRY(launch_init(a, w, 1, st));
+    if (pl.pruned) HIP_TRY(launch_index(a, w, 1, st));
+    if ((rc = nn_pass(ctx, pl, a, w, 1, n, 0, 1, st))) return rc;
+    PairState ps;
+    keys.resize((size_t)n);
+    HIP_TRY(hipMemcpyAsync(&ps, w.state, sizeof(ps), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(keys.data(), w.nn_key, (size_t)n * sizeof(NNKey), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (ps.phase == kPhaseInvalid) return fail(ps.status, "non-finite coordinate in the query or target cloud");
     return ICP4R_OK;
 }
 
@@ -246,7 +353,7 @@ int events_avg(std::vector<EventPair>& v, size_t used, double* avg_ms) {
 
 extern "C" {
 
-const char* icp4r_version(void) { return "icp4r 0.1.0 (gfx950, HIP)"; }
+const char* icp4r_version(void) { return "icp4r 0.2.0 (gfx950, HIP)"; }
 int icp4r_abi_version(void) { return ICP4R_ABI_VERSION; }
 const char* icp4r_last_error(void) { return g_last_error.c_str(); }
 
@@ -297,8 +404,8 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
-                      &ctx->aligned, &ctx->results, &ctx->idx, &ctx->d2, &ctx->T, &ctx->X, &ctx->nn_d2,
-                      &ctx->nn_idx, &ctx->state})
+                      &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->batch_events})
         for (auto& ev : *v) {
@@ -473,21 +580,12 @@ int icp4r_nearest(icp4r_ctx* ctx, const float* query, int32_t n, int32_t query_s
     if (m == 0) return fail(ICP4R_E_EMPTY, "empty target");
     if (n == 0) return ICP4R_OK;
     HIP_TRY(hipSetDevice(ctx->device));
-    std::vector<float> hq, ht;
-    pack_host(query, n, query_stride_bytes, hq);
-    pack_host(tgt, m, tgt_stride_bytes, ht);
-    hipStream_t st = ctx->stream;
-    HIP_TRY(ctx->src.ensure(hq.size() * 4));
-    HIP_TRY(ctx->tgt.ensure(ht.size() * 4));
-    HIP_TRY(ctx->idx.ensure((size_t)n * 4));
-    HIP_TRY(ctx->d2.ensure((size_t)n * 4));
-    HIP_TRY(hipMemcpyAsync(ctx->src.p, hq.data(), hq.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_nn_query(static_cast<const float4*>(ctx->src.p), n, static_cast<const float4*>(ctx->tgt.p), m,
-                             nullptr, static_cast<int32_t*>(ctx->idx.p), static_cast<float*>(ctx->d2.p), st));
-    HIP_TRY(hipMemcpyAsync(idx_out, ctx->idx.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(d2_out, ctx->d2.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<NNKey> keys;
+    if ((rc = nearest_keys(ctx, query, n, query_stride_bytes, tgt, m, tgt_stride_bytes, nullptr, keys))) return rc;
+    for (int32_t i = 0; i < n; ++i) {
+        idx_out[i] = key_idx(keys[i]);
+        d2_out[i] = key_d2(keys[i]);
+    }
     return ICP4R_OK;
 }
 
@@ -501,31 +599,18 @@ int icp4r_fitness(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_strid
     if (m == 0) return fail(ICP4R_E_EMPTY, "empty target");
     if (n == 0) return ICP4R_OK;
     HIP_TRY(hipSetDevice(ctx->device));
-    std::vector<float> hs, ht, d2((size_t)n);
-    pack_host(src, n, src_stride_bytes, hs);
-    pack_host(tgt, m, tgt_stride_bytes, ht);
-    hipStream_t st = ctx->stream;
-    HIP_TRY(ctx->src.ensure(hs.size() * 4));
-    HIP_TRY(ctx->tgt.ensure(ht.size() * 4));
-    HIP_TRY(ctx->idx.ensure((size_t)n * 4));
-    HIP_TRY(ctx->d2.ensure((size_t)n * 4));
-    HIP_TRY(ctx->T.ensure(64));
-    HIP_TRY(hipMemcpyAsync(ctx->src.p, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->T.p, T, 64, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_nn_query(static_cast<const float4*>(ctx->src.p), n, static_cast<const float4*>(ctx->tgt.p), m,
-                             static_cast<const float*>(ctx->T.p), static_cast<int32_t*>(ctx->idx.p),
-                             static_cast<float*>(ctx->d2.p), st));
-    HIP_TRY(hipMemcpyAsync(d2.data(), ctx->d2.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<NNKey> keys;
+    if ((rc = nearest_keys(ctx, src, n, src_stride_bytes, tgt, m, tgt_stride_bytes, T, keys))) return rc;
     // Registration::getFitnessScore: sequential double sum over points with d2 <= max_range
     double sum = 0.0;
     int nr = 0;
-    for (int32_t i = 0; i < n; ++i)
-        if (d2[i] <= max_range) {
-            sum += d2[i];
+    for (int32_t i = 0; i < n; ++i) {
+        const float d2 = key_d2(keys[i]);
+        if (d2 <= max_range) {
+            sum += d2;
             ++nr;
         }
+    }
     *fitness = nr > 0 ? sum / nr : DBL_MAX;
     return ICP4R_OK;
 }
@@ -557,15 +642,33 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
     ctx->nn_used = 0;
     ctx->batch_used = 0;
+    if (ctx->evals.p) {
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemset(ctx->evals.p, 0, sizeof(uint64_t)));
+    }
     return ICP4R_OK;
 }
 
-int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t* q, int32_t* splits, int64_t* nn_blocks) {
-    if (npairs <= 0 || max_src_n < 0 || max_tgt_n < 0) return fail(ICP4R_E_INVALID, "bad shape");
-    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n);
-    if (q) *q = pl.q;
-    if (splits) *splits = pl.splits;
-    if (nn_blocks) *nn_blocks = pl.blocks;
+int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out) {
+    if (npairs <= 0 || max_src_n < 0 || max_tgt_n < 0 || !out) return fail(ICP4R_E_INVALID, "bad shape");
+    if (nn_mode < ICP4R_NN_AUTO || nn_mode > ICP4R_NN_PRUNED) return fail(ICP4R_E_INVALID, "unknown nn_mode %d", nn_mode);
+    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode);
+    out->pruned = pl.pruned ? 1 : 0;
+    out->q = pl.q;
+    out->splits = pl.splits;
+    out->leaf = pl.leaf;
+    out->nn_blocks = pl.blocks;
+    return ICP4R_OK;
+}
+
+int icp4r_nn_evaluations(icp4r_ctx* ctx, uint64_t* evaluations) {
+    if (!ctx || !evaluations) return fail(ICP4R_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    uint64_t v = 0;
+    if (ctx->evals.p) HIP_TRY(hipMemcpy(&v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
+    *evaluations = v;
     return ICP4R_OK;
 }
 

@@ -11,14 +11,19 @@ namespace icp4r {
 
 constexpr int kNNWG = 256;        // threads per NN workgroup (4 waves)
 constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_kernel (instantiated)
-constexpr int kDefaultQ = 4;      // default cap (tools/tune_sweep.py)
+constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.py)
+constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
+constexpr int kDefaultLeaf = 16;    // pruned: targets per block
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential centroid fold
+constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
+constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
 
 constexpr int kNumericsPCL = ICP4R_NUMERICS_PCL;
 constexpr int kNumericsF64 = ICP4R_NUMERICS_F64;
 constexpr int kStatusEmpty = ICP4R_E_EMPTY;
 constexpr int kStatusTooFewCorr = ICP4R_E_TOO_FEW_CORR;
 constexpr int kStatusNonFinite = ICP4R_E_NONFINITE;
+constexpr int kStatusInvalid = ICP4R_E_INVALID;
 
 // per-pair loop phase
 constexpr int kPhaseActive = 0;     // iterating
@@ -65,25 +70,48 @@ struct PairState {
     int32_t ncorr;
 };
 
-// Workspace: X (input_transformed) and the NN results, pair p at [p * x_stride, ...).
+// NN result of one query: (float bits of d² << 32) | target index.  d² >= 0, so the unsigned order
+// of the keys is the lexicographic (d², index) order; the minimum key is PCL's answer (nearest
+// target, lowest index among equal distances) whatever order the targets are visited in.
+using NNKey = uint64_t;
+__host__ __device__ inline float key_d2(NNKey k) {
+    union {
+        uint32_t u;
+        float f;
+    } c;
+    c.u = (uint32_t)(k >> 32);
+    return c.f;
+}
+__host__ __device__ inline int32_t key_idx(NNKey k) { return (int32_t)(uint32_t)k; }
+
+// Workspace, pair p at [p * stride, ...) of each array.
 struct WorkArgs {
-    float4* X;
-    float* nn_d2;       // [splits][npairs * x_stride]
-    int32_t* nn_idx;    // [splits][npairs * x_stride]
+    float4* X;          // input_transformed [npairs * x_stride]
+    NNKey* nn_key;      // per-query NN key   [npairs * x_stride]; splits > 1 merge by atomicMin
     PairState* state;   // [npairs]
     int64_t x_stride;   // >= max source points per pair
-    int64_t slot_stride;  // npairs * x_stride
-    int32_t splits;     // target splits per pair (1 for batches; >1 for single-pair latency)
+    int32_t splits;     // brute force: target splits per pair (1 for batches; >1 for single-pair latency)
+    int32_t leaf;       // pruned: targets per block (16 or 32); 0 = brute force
+    // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):
+    float4* tsort;      // [npairs * t_stride] targets in Morton-cell order, .w = original index bits;
+                        // positions [m, t_stride) repeat the last target (harmless duplicates)
+    int32_t* tinv;      // [npairs * t_stride] original target index -> sorted position
+    float4* tbox;       // [npairs * 2 * b_stride] per block: lo, hi (empty blocks: +inf, -inf)
+    float4* sbox;       // [npairs * 2 * sb_stride] per superblock of kSuper blocks: lo, hi
+    int32_t* sperm;     // [npairs * x_stride] source indices in Morton-cell order
+    int64_t t_stride, b_stride, sb_stride;
+    unsigned long long* evals;  // distance evaluations of valid queries (one atomic per wave / workgroup)
 };
 
 hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
                      int fitness_pass, hipStream_t st);
+hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
+hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
+                            int first, hipStream_t st);
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);
-hipError_t launch_nn_query(const float4* q, int n, const float4* tgt, int m, const float* T, int32_t* idx, float* d2,
-                           hipStream_t st);
 
 }  // namespace icp4r

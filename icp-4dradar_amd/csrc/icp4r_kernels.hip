@@ -4,22 +4,26 @@
 // sequence of launches on one stream (no host synchronisation, per-pair early-exit flags):
 //
 //   init_kernel                      validate, X := guess * src (or src), final := guess
+//   index_kernel                     (pruned mode) Morton counting sort of target and source,
+//                                    target block / superblock bounding boxes
 //   repeat max_iterations times:
-//     nn_kernel<Q>                   exact 1-NN of every X_i in the pair's target      (HOT: FP32 VALU)
+//     nn_pruned_kernel<Q,B>          exact 1-NN of every X_i in the pair's target      (HOT: FP32 VALU)
+//       or nn_kernel<Q>              (brute force: small targets / ICP4R_NN_BRUTE)
 //     update_kernel<NUM>             correspondences -> Umeyama moments -> 3x3 solve ->
 //                                    hasConverged -> X := T_inc * X in place (PCL transformCloud)
 //   fitness_prep_kernel              X := final * src
-//   nn_kernel<Q>                     fitness pass (getFitnessScore)
+//   NN pass                          fitness pass (getFitnessScore)
 //   finish_kernel                    mean d² over d² <= max_range, results, aligned output
 //
-// The hot kernel holds Q queries per lane in VGPRs and streams the target cloud through the SCALAR
-// cache: the target address is wave-uniform, so each target point lands in SGPRs and is broadcast
-// to 64 lanes x Q queries with no LDS traffic and no VGPRs.  Per (query, target) the VALU executes
-// 3 sub + 3 mul + 2 add (FLANN's L2_Simple, unfused) + 1 cmp + 2 cndmask.  Splitting the serial
-// solve into its own kernel keeps the sweep at <= 128 VGPRs (4 waves/SIMD).
+// Both NN kernels hold Q queries per lane in VGPRs and stream targets through the SCALAR cache:
+// the target address is wave-uniform, so each target point lands in SGPRs and is broadcast to
+// 64 lanes x Q queries with no LDS traffic and no VGPRs.  Per (query, target) the VALU executes
+// 3 sub + 3 mul + 2 add (FLANN's L2_Simple, unfused) and a compare/select.  Every NN result is a
+// u64 key (d² bits, target index) whose minimum is PCL's answer (lowest index among ties), so
+// pruning, visiting order and target splits cannot change it.
 //
-// Determinism: fixed-order reductions only (xor-butterfly per wave, waves in index order, splits
-// in index order); no float atomics.  NN ties resolve to the lowest target index.
+// Determinism: fixed-order reductions only (xor-butterfly per wave, waves in index order, the
+// PCL-numerics folds sequential in source order); no float atomics.
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -167,19 +171,16 @@ __device__ __forceinline__ double huber_w(float d2, double delta) {
     return r <= delta ? 1.0 : delta / r;
 }
 
-// Per-query NN result merged over target splits: lexicographic (d², index) minimum == the
-// unsplit sweep's answer (lowest index among equal distances).
-__device__ __forceinline__ void merge_nn(const WorkArgs& w, int64_t slot, float& d2, int& idx) {
-    d2 = w.nn_d2[slot];
-    idx = w.nn_idx[slot];
-    for (int s = 1; s < w.splits; ++s) {
-        const float d = w.nn_d2[slot + (int64_t)s * w.slot_stride];
-        const int j = w.nn_idx[slot + (int64_t)s * w.slot_stride];
-        if (d < d2 || (d == d2 && j < idx)) {
-            d2 = d;
-            idx = j;
-        }
-    }
+// Per-query NN result: one key (splits were merged by atomicMin on the key, i.e. the lexicographic
+// (d², index) minimum == the unsplit sweep's answer).
+__device__ __forceinline__ void load_nn(const WorkArgs& w, int64_t slot, float& d2, int& idx) {
+    const NNKey k = w.nn_key[slot];
+    d2 = key_d2(k);
+    idx = key_idx(k);
+}
+
+__device__ __forceinline__ NNKey make_key(float d2, uint32_t idx) {
+    return ((NNKey)__float_as_uint(d2) << 32) | idx;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -187,7 +188,7 @@ __device__ __forceinline__ void merge_nn(const WorkArgs& w, int64_t slot, float&
 constexpr int kInitWG = 256;
 __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     __shared__ float Tg[16];
-    __shared__ int ident;
+    __shared__ int ident, invalid;
     const int p = blockIdx.x;
     const int tid = threadIdx.x;
     const int n = a.src_n[p], m = a.tgt_n[p];
@@ -218,19 +219,23 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
         st.conv_state = 0;
         st.iterations = 0;
         st.ncorr = 0;
-        if (m <= 0 || bad) {
+        // counts above the batch's declared max_src_n / max_tgt_n would overrun the workspace strides
+        const bool too_big = n > w.x_stride || (w.leaf > 0 && m > w.t_stride);
+        if (m <= 0 || bad || too_big) {
             // Registration::initCompute fails (no target) -> align returns; final stays identity.
             mat4_identity(st.final_T);
             st.phase = kPhaseInvalid;
-            st.status = m <= 0 ? kStatusEmpty : kStatusNonFinite;
+            st.status = too_big ? kStatusInvalid : m <= 0 ? kStatusEmpty : kStatusNonFinite;
+            invalid = 1;
         } else {
             for (int k = 0; k < 16; ++k) st.final_T[k] = Tg[k];  // final_transformation_ = guess
             st.phase = kPhaseActive;
             st.status = 0;
+            invalid = 0;
         }
     }
     __syncthreads();
-    if (m <= 0 || bad) return;
+    if (invalid) return;
     float4* X = w.X + (int64_t)p * w.x_stride;
     const bool id = ident != 0;
     for (int i = tid; i < n; i += kInitWG) {
@@ -243,7 +248,9 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
 
 // ---------------------------------------------------------------------------------------------
 // nn_kernel<Q>: blockIdx.x = query block (WG*Q queries), blockIdx.y = pair, blockIdx.z = target
-// split.  Writes the (d², index) of each query's nearest target in the split's index range.
+// split.  Writes the key of each query's nearest target in the split's index range; with several
+// splits the keys are merged by a u64 atomicMin into a 0xFF..-initialised array (exact: the
+// minimum key is the lexicographic (d², index) minimum, independent of arrival order).
 template <int Q, bool PACKED>
 __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int fitness_pass) {
     const int p = blockIdx.y;
@@ -271,15 +278,272 @@ __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int f
             nn_sweep_packed<Q>(x, y, z, a.tgt + uload(a.tgt_off + p), j0, j1, best, bi);
     else
         nn_sweep<Q>(x, y, z, a.tgt + uload(a.tgt_off + p), j0, j1, best, bi);
-    const int64_t slot0 = (int64_t)s * w.slot_stride + (int64_t)p * w.x_stride;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    if (threadIdx.x == 0)
+        atomicAdd(w.evals, (unsigned long long)(j1 - j0) * (unsigned long long)min(n - base, kNNWG * Q));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int i = base + threadIdx.x + q * kNNWG;
         if (i < n) {
-            w.nn_d2[slot0 + i] = best[q];
-            w.nn_idx[slot0 + i] = bi[q];
+            const NNKey k = make_key(best[q], (uint32_t)bi[q]);
+            if (w.splits > 1)
+                atomicMin(reinterpret_cast<unsigned long long*>(key + i), (unsigned long long)k);
+            else
+                key[i] = k;
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// index_kernel: the pruned search's per-pair index (once per registration; the target never moves
+// and a rigid motion keeps the source's spatial order).  blockIdx.x = pair, blockIdx.y = 0 target /
+// 1 source.  A counting sort over 2^14 Morton cells of the cloud's bounding box (x, y: 32 cells,
+// z: 16 — radar scans are flat) in LDS; order inside a cell is whatever the LDS atomics give, which
+// is fine: the search is exact for any order, the order only decides how well blocks prune.
+constexpr int kIdxWG = 1024;
+constexpr int kIdxWaves = kIdxWG / 64;
+constexpr int kCellBins = 1 << 14;
+
+__device__ __forceinline__ uint32_t cell_code(float x, float y, float z, const float* lo, const float* sc) {
+    const int cx = min(31, max(0, (int)((x - lo[0]) * sc[0])));
+    const int cy = min(31, max(0, (int)((y - lo[1]) * sc[1])));
+    const int cz = min(15, max(0, (int)((z - lo[2]) * sc[2])));
+    uint32_t c = 0;
+#pragma unroll
+    for (int b = 4; b >= 0; --b) {  // interleave, most significant level first: x y z per level
+        c = (c << 1) | ((cx >> b) & 1);
+        c = (c << 1) | ((cy >> b) & 1);
+        if (b < 4) c = (c << 1) | ((cz >> b) & 1);
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
+    __shared__ uint32_t bins[kCellBins];
+    __shared__ float red[kIdxWaves][6];
+    __shared__ uint32_t wsum[kIdxWaves];
+    __shared__ float lo_s[3], sc_s[3];
+    const int p = blockIdx.x;
+    const bool is_tgt = blockIdx.y == 0;
+    if (w.state[p].phase == kPhaseInvalid) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
+    if (n <= 0) return;
+    const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
+    // 1. bounding box
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = tid; i < n; i += kIdxWG) {
+        const float4 v = pts[i];
+        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
+        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], off, 64));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off, 64));
+        }
+    if (lane == 0)
+        for (int k = 0; k < 3; ++k) {
+            red[wave][k] = mn[k];
+            red[wave][3 + k] = mx[k];
+        }
+    for (int b = tid; b < kCellBins; b += kIdxWG) bins[b] = 0;
+    __syncthreads();
+    if (tid < 3) {
+        float l = INFINITY, h = -INFINITY;
+        for (int v = 0; v < kIdxWaves; ++v) {
+            l = fminf(l, red[v][tid]);
+            h = fmaxf(h, red[v][3 + tid]);
+        }
+        const float cells = tid == 2 ? 16.0f : 32.0f;
+        lo_s[tid] = l;
+        sc_s[tid] = h > l ? cells / (h - l) : 0.0f;
+    }
+    __syncthreads();
+    float lo[3] = {lo_s[0], lo_s[1], lo_s[2]}, sc[3] = {sc_s[0], sc_s[1], sc_s[2]};
+    // 2. histogram of cell codes
+    for (int i = tid; i < n; i += kIdxWG) {
+        const float4 v = pts[i];
+        atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
+    }
+    __syncthreads();
+    // 3. exclusive scan: thread t owns bins [16 t, 16 t + 16)
+    constexpr int per = kCellBins / kIdxWG;
+    uint32_t loc[per], run = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        loc[k] = run;
+        run += bins[tid * per + k];
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int v = 0; v < wave; ++v) wbase += wsum[v];
+    const uint32_t tbase = wbase + incl - run;
+#pragma unroll
+    for (int k = 0; k < per; ++k) bins[tid * per + k] = tbase + loc[k];
+    __syncthreads();
+    // 4. scatter
+    if (is_tgt) {
+        float4* ts = w.tsort + (int64_t)p * w.t_stride;
+        int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+        for (int i = tid; i < n; i += kIdxWG) {
+            const float4 v = pts[i];
+            const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
+            ts[pos] = make_float4(v.x, v.y, v.z, __uint_as_float((uint32_t)i));
+            tinv[i] = (int32_t)pos;
+        }
+        __threadfence();
+        __syncthreads();
+        // 5. tail duplicates, block boxes, superblock boxes
+        const float4 last = ts[n - 1];
+        for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = last;
+        const int B = w.leaf;
+        const int nb = (n + B - 1) / B;
+        float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+        for (int b = tid; b < w.b_stride; b += kIdxWG) {
+            float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+            if (b < nb) {
+                const int e = min(n, (b + 1) * B);
+                for (int k = b * B; k < e; ++k) {
+                    const float4 v = ts[k];
+                    l.x = fminf(l.x, v.x); l.y = fminf(l.y, v.y); l.z = fminf(l.z, v.z);
+                    h.x = fmaxf(h.x, v.x); h.y = fmaxf(h.y, v.y); h.z = fmaxf(h.z, v.z);
+                }
+            }
+            tb[2 * b] = l;
+            tb[2 * b + 1] = h;
+        }
+        __threadfence();
+        __syncthreads();
+        float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
+        for (int s = tid; s < w.sb_stride; s += kIdxWG) {
+            float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+            for (int b = s * kSuper; b < (s + 1) * kSuper; ++b) {
+                const float4 bl = tb[2 * b], bh = tb[2 * b + 1];
+                l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
+                h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
+            }
+            sbx[2 * s] = l;
+            sbx[2 * s + 1] = h;
+        }
+    } else {
+        int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
+        for (int i = tid; i < n; i += kIdxWG) {
+            const float4 v = pts[i];
+            sp[atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u)] = i;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// nn_pruned_kernel<Q, B>: exact 1-NN with block pruning.  Each wave owns 64*Q source points that
+// are contiguous in Morton order (a compact region), keeps their best key in VGPRs, and walks the
+// target superblocks outward from the one holding its seed match.  A (super)block is swept only if
+// some query's box lower bound can reach its current best; the sweep itself is the scalar-cache
+// stream of nn_sweep with the comparison on the full (d², index) key, so the answer is exactly the
+// brute-force one (PCL semantics, lowest index among ties) whatever the visiting order.
+//
+// Pruning is conservative in float: the bound is computed in float and shrunk by 2^-16 before the
+// `<=` test, which covers the few-ulp rounding of both the bound and l2_simple's d².  Seeds: the
+// previous NN of the same query (iterations > 0 and the fitness pass: the source moved by one small
+// increment, so the old match is nearly as close); iteration 0: the target at the same relative
+// Morton position.
+constexpr float kLbShrink = 1.0f - 1.0f / 65536.0f;
+
+template <int Q>
+__device__ __forceinline__ bool box_needed(const v4f lo, const v4f hi, const float (&x)[Q], const float (&y)[Q],
+                                           const float (&z)[Q], const NNKey (&best)[Q]) {
+    bool need = false;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
+        const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
+        const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
+        const float lb = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+        need = need || (lb * kLbShrink <= key_d2(best[q]));
+    }
+    return __any(need);
+}
+
+template <int Q, int B>
+__device__ __forceinline__ void sweep_block(cv4f_ptr blk, const float (&x)[Q], const float (&y)[Q], const float (&z)[Q],
+                                            NNKey (&best)[Q]) {
+#pragma unroll
+    for (int t = 0; t < B; t += 4) {
+        const v4f c[4] = {blk[t], blk[t + 1], blk[t + 2], blk[t + 3]};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t ti = __float_as_uint(c[u].w);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const NNKey kn = make_key(l2_simple(x[q], y[q], z[q], c[u].x, c[u].y, c[u].z), ti);
+                best[q] = kn < best[q] ? kn : best[q];
+            }
+        }
+    }
+}
+
+template <int Q, int B>
+__global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+    const int p = blockIdx.y;
+    const int phase = uload(&w.state[p].phase);
+    if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
+    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int base = (blockIdx.x * (kNNWG / 64) + wave) * (64 * Q);
+    if (base >= n) return;
+    const float4* X = w.X + (int64_t)p * w.x_stride;
+    const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const float4* tgt = a.tgt + uload(a.tgt_off + p);
+    const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
+    float x[Q], y[Q], z[Q];
+    NNKey best[Q];
+    int orig[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int s0 = base + lane + q * 64;
+        const int s = min(s0, n - 1);  // lanes past the end repeat the last query (not written)
+        const int o = sperm[s];
+        orig[q] = s0 < n ? o : -1;
+        const float4 v = X[o];
+        x[q] = v.x;
+        y[q] = v.y;
+        z[q] = v.z;
+        const uint32_t j = first ? __float_as_uint(tsg[((int64_t)s * m) / n].w) : (uint32_t)key_idx(key[o]);
+        const float4 t = tgt[j];
+        best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
+    }
+    const int nb = (m + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
+    const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
+    const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (B * kSuper);
+    const cv4f_ptr ts = as_const(tsg);
+    const cv4f_ptr tb = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
+    const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
+    int up = sb0, dn = sb0 - 1, swept = 0;
+    for (int k = 0; k < nsb; ++k) {
+        const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
+        if (!box_needed<Q>(sbx[2 * sb], sbx[2 * sb + 1], x, y, z, best)) continue;
+        for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {  // blocks past nb have empty boxes
+            if (!box_needed<Q>(tb[2 * b], tb[2 * b + 1], x, y, z, best)) continue;
+            sweep_block<Q, B>(ts + (int64_t)b * B, x, y, z, best);
+            ++swept;
+        }
+    }
+    if (lane == 0)
+        atomicAdd(w.evals, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        if (orig[q] >= 0) key[orig[q]] = best[q];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -488,7 +752,7 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
                 const int i = base + o;
                 float d2;
                 int j;
-                merge_nn(w, slot0 + i, d2, j);
+                load_nn(w, slot0 + i, d2, j);
                 float wt = 0.f, sx = ident, sy = ident, sz = ident, dx = ident, dy = ident, dz = ident;
                 double dd = 0.0;
                 if (!(d2 > kp.max_d2)) {
@@ -542,7 +806,7 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
                 const int i = base + o;
                 float d2;
                 int j;
-                merge_nn(w, slot0 + i, d2, j);
+                load_nn(w, slot0 + i, d2, j);
                 float wt = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, d0 = 0.f, d1 = 0.f, dv2 = 0.f;
                 if (!(d2 > kp.max_d2)) {
                     const float4 s = X[i];
@@ -572,7 +836,7 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
         for (int i = tid; i < n; i += kUpdWG) {
             float d2;
             int j;
-            merge_nn(w, slot0 + i, d2, j);
+            load_nn(w, slot0 + i, d2, j);
             if (d2 > kp.max_d2) continue;
             const float4 s = X[i];
             const float4 d = tgt[j];
@@ -641,7 +905,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
             for (int o = threadIdx.x; o < kFoldChunk && base + o < n; o += kFinWG) {
                 float d2;
                 int j;
-                merge_nn(w, slot0 + base + o, d2, j);
+                load_nn(w, slot0 + base + o, d2, j);
                 chunk[o] = ((double)d2 <= a.kp.fit_max_range) ? (double)d2 : -1.0;
             }
             __syncthreads();
@@ -692,33 +956,6 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Standalone exact 1-NN (icp4r_nearest / icp4r_fitness): one query per thread, optional transform.
-__global__ __launch_bounds__(256) void nn_query_kernel(const float4* __restrict__ q, int n, const float4* tgt, int m,
-                                                       const float* __restrict__ T, int32_t* __restrict__ idx,
-                                                       float* __restrict__ d2) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    float x[1], y[1], z[1];
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < n) s = q[i];
-    if (T) {
-        float Tl[16];
-        for (int k = 0; k < 16; ++k) Tl[k] = T[k];
-        xform_pt(Tl, s.x, s.y, s.z, x[0], y[0], z[0]);
-    } else {
-        x[0] = s.x;
-        y[0] = s.y;
-        z[0] = s.z;
-    }
-    float best[1];
-    int bi[1];
-    nn_sweep<1>(x, y, z, tgt, 0, m, best, bi);
-    if (i < n) {
-        idx[i] = bi[0];
-        d2[i] = best[0];
-    }
-}
-
 // Test hook: the device float Umeyama rotation for k sigma matrices (one thread each).
 __global__ void rot_f32_kernel(const float* sigma, float* R, int k) {
     __shared__ SvdWorkF ws[64];
@@ -766,6 +1003,37 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
     return hipGetLastError();
 }
 
+hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
+    hipLaunchKernelGGL(index_kernel, dim3(npairs, 2), dim3(kIdxWG), 0, st, a, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
+                            int first, hipStream_t st) {
+    const int per_block = kNNWG * q;
+    const dim3 grid((max_n + per_block - 1) / per_block, npairs), block(kNNWG);
+#define ICP4R_PR_CASE(QQ, BB) hipLaunchKernelGGL((nn_pruned_kernel<QQ, BB>), grid, block, 0, st, a, w, fitness_pass, first)
+    if (w.leaf == 16) {
+        switch (q) {
+            case 1: ICP4R_PR_CASE(1, 16); break;
+            case 2: ICP4R_PR_CASE(2, 16); break;
+            case 4: ICP4R_PR_CASE(4, 16); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else if (w.leaf == 32) {
+        switch (q) {
+            case 1: ICP4R_PR_CASE(1, 32); break;
+            case 2: ICP4R_PR_CASE(2, 32); break;
+            case 4: ICP4R_PR_CASE(4, 32); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        return hipErrorInvalidValue;
+    }
+#undef ICP4R_PR_CASE
+    return hipGetLastError();
+}
+
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     if (a.kp.numerics == kNumericsPCL)
         hipLaunchKernelGGL(update_kernel<kNumericsPCL>, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
@@ -781,13 +1049,6 @@ hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs,
 
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     hipLaunchKernelGGL(finish_kernel, dim3(npairs), dim3(kFinWG), 0, st, a, w);
-    return hipGetLastError();
-}
-
-hipError_t launch_nn_query(const float4* q, int n, const float4* tgt, int m, const float* T, int32_t* idx, float* d2,
-                           hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(nn_query_kernel, dim3((n + 255) / 256), dim3(256), 0, st, q, n, tgt, m, T, idx, d2);
     return hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ library_path = os.path.join(HERE, "_lib", "libicp4r.so")
 
 OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 NUMERICS_PCL, NUMERICS_F64 = 0, 1
-NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED = 0, 1, 2
+NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED, NN_PRUNED = 0, 1, 2, 3
 DBL_MAX = sys.float_info.max
 
 _STATUS = {OK: "ICP4R_OK", E_INVALID: "ICP4R_E_INVALID", E_EMPTY: "ICP4R_E_EMPTY",
@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
-    "icp4r_kernel_time_reset", "icp4r_plan",
+    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_evaluations",
 ]
 
 
@@ -103,6 +103,11 @@ class Batch(C.Structure):
     ]
 
 
+class PlanInfo(C.Structure):
+    _fields_ = [("pruned", C.c_int32), ("q", C.c_int32), ("splits", C.c_int32), ("leaf", C.c_int32),
+                ("nn_blocks", C.c_int64)]
+
+
 assert C.sizeof(Result) == 96
 RESULT_DTYPE = np.dtype([("T", np.float32, 16), ("fitness", np.float64), ("iterations", np.int32),
                          ("converged", np.int32), ("status", np.int32), ("convergence_state", np.int32),
@@ -138,7 +143,8 @@ def load():
         "icp4r_kernel_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_batch_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_kernel_time_reset": (C.c_int, [vp]),
-        "icp4r_plan": (C.c_int, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
+        "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
+        "icp4r_nn_evaluations": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -270,11 +276,18 @@ class Context:
     def reset_timers(self):
         _check(self._lib.icp4r_kernel_time_reset(self._h), "icp4r_kernel_time_reset")
 
+    def nn_evaluations(self) -> int:
+        """Distance evaluations (query x target) of the NN kernels since the last reset_timers()."""
+        v = C.c_uint64()
+        _check(self._lib.icp4r_nn_evaluations(self._h, C.byref(v)), "icp4r_nn_evaluations")
+        return v.value
 
-def plan(npairs: int, max_src_n: int, max_tgt_n: int) -> dict:
-    q, s, b = C.c_int32(), C.c_int32(), C.c_int64()
-    _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, C.byref(q), C.byref(s), C.byref(b)), "icp4r_plan")
-    return {"q": q.value, "splits": s.value, "nn_blocks": b.value}
+
+def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO) -> dict:
+    info = PlanInfo()
+    _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, nn_mode, C.byref(info)), "icp4r_plan")
+    return {"pruned": bool(info.pruned), "q": info.q, "splits": info.splits, "leaf": info.leaf,
+            "nn_blocks": info.nn_blocks}
 
 
 _default_ctx: Context | None = None

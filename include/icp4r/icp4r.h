@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ICP4R_ABI_VERSION 1
+#define ICP4R_ABI_VERSION 2
 
 typedef enum icp4r_status {
     ICP4R_OK = 0,
@@ -66,9 +66,10 @@ typedef enum icp4r_numerics { ICP4R_NUMERICS_PCL = 0, ICP4R_NUMERICS_F64 = 1 } i
 /* Correspondence search.  All modes return the exact nearest neighbour under FLANN's
  * L2_Simple<float> distance ((dx*dx + dy*dy) + dz*dz, float, unfused); ties -> lowest index. */
 typedef enum icp4r_nn_mode {
-    ICP4R_NN_AUTO = 0,         /* pick per shape (currently ICP4R_NN_BRUTE)                          */
+    ICP4R_NN_AUTO = 0,         /* PRUNED when the largest target has >= 512 points, else BRUTE      */
     ICP4R_NN_BRUTE = 1,        /* exhaustive scan, target streamed through the scalar cache, FP32    */
-    ICP4R_NN_BRUTE_PACKED = 2  /* same scan, two queries per v_pk_{add,mul}_f32 (identical results) */
+    ICP4R_NN_BRUTE_PACKED = 2, /* same scan, two queries per v_pk_{add,mul}_f32 (identical results) */
+    ICP4R_NN_PRUNED = 3        /* Morton-ordered target blocks with bounding boxes, exact search     */
 } icp4r_nn_mode;
 
 typedef struct icp4r_params {
@@ -165,9 +166,21 @@ int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
 int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);
 int icp4r_kernel_time_reset(icp4r_ctx* ctx);
 
-/* Launch geometry the batch path picks for a shape (queries per lane, target splits, workgroups
- * of the NN kernel) — exposed for tests and the benchmark report. */
-int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t* q, int32_t* splits, int64_t* nn_blocks);
+/* Distance evaluations (query x target) the NN kernels performed since the last
+ * icp4r_kernel_time_reset — the algorithmic work behind the roofline's `achieved` (the pruned
+ * search evaluates a small fraction of n*m; brute force exactly n*m per pair and pass).
+ * Synchronises the context's device. */
+int icp4r_nn_evaluations(icp4r_ctx* ctx, uint64_t* evaluations);
+
+/* Launch geometry the batch path picks for a shape — exposed for tests and the benchmark report. */
+typedef struct icp4r_plan_info {
+    int32_t pruned;     /* 1: ICP4R_NN_PRUNED kernel, 0: brute force                 */
+    int32_t q;          /* queries per lane                                          */
+    int32_t splits;     /* brute force: target splits per pair                       */
+    int32_t leaf;       /* pruned: targets per block                                 */
+    int64_t nn_blocks;  /* workgroups of one NN launch                               */
+} icp4r_plan_info;
+int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);
 
 #ifdef __cplusplus
 }

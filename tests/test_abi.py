@@ -53,7 +53,7 @@ def test_params_default_matches_pcl():
     assert math.isinf(p.huber_delta)
     assert p.fitness_max_range == sys.float_info.max
     L = icp4r.load()
-    assert L.icp4r_abi_version() == 1
+    assert L.icp4r_abi_version() == 2
     assert b"gfx950" in L.icp4r_version()
 
 
@@ -68,12 +68,17 @@ def test_struct_layouts():
 def test_plan_geometry():
     import icp4r
 
-    big = icp4r.plan(1024, 8192, 8192)
-    assert big["splits"] == 1 and big["q"] == 4
-    single = icp4r.plan(1, 8192, 8192)
-    assert single["splits"] > 1 and single["nn_blocks"] >= 512
-    tiny = icp4r.plan(1, 10, 7)
-    assert tiny["q"] == 1 and tiny["splits"] == 1
+    big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, 2 queries per lane, 16-target blocks
+    assert big["pruned"] and big["q"] == 2 and big["leaf"] == 16 and big["splits"] == 1
+    single = icp4r.plan(1, 8192, 8192)  # C2: one query per lane to fill more waves
+    assert single["pruned"] and single["q"] == 1 and single["nn_blocks"] == 32
+    brute = icp4r.plan(1024, 8192, 8192, icp4r.NN_BRUTE)
+    assert not brute["pruned"] and brute["q"] == 4 and brute["splits"] == 1
+    bsingle = icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)
+    assert bsingle["splits"] > 1 and bsingle["nn_blocks"] >= 512
+    tiny = icp4r.plan(1, 10, 7)  # small target: brute force
+    assert not tiny["pruned"] and tiny["q"] == 1 and tiny["splits"] == 1
+    assert icp4r.plan(1, 10, 7, icp4r.NN_PRUNED)["pruned"]
 
 
 def test_fails_loudly_without_library(tmp_path, monkeypatch):

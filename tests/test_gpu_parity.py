@@ -36,7 +36,8 @@ def test_nn_bitexact_golden(gpu_ctx, oracle_mod, golden, which):
     assert (gi[rows] == np.array(case["nn0_idx_rows"])).all()
 
 
-@pytest.mark.parametrize("n,m", [(1, 1), (5, 3), (7, 1001), (1000, 4099), (4097, 8190), (3, 65540)])
+@pytest.mark.parametrize("n,m", [(1, 1), (5, 3), (7, 1001), (1000, 4099), (4097, 8190), (3, 65540), (20000, 511),
+                                 (9000, 70001)])
 def test_nn_bitexact_shapes_and_ties(gpu_ctx, oracle_mod, n, m):
     rng = np.random.default_rng(n * 31 + m)
     tgt = rng.uniform(-80, 80, (m, 4)).astype(np.float32)
@@ -48,6 +49,27 @@ def test_nn_bitexact_shapes_and_ties(gpu_ctx, oracle_mod, n, m):
     gi, gd = gpu_ctx.nearest(q, tgt)
     oi, od = oracle_mod.nearest(q, tgt, oracle_mod.NN_BRUTE)
     assert (gi == oi).all() and (gd == od).all()
+
+
+def _lattice(rng, side, spacing=0.5):
+    g = np.stack(np.meshgrid(*[np.arange(side, dtype=np.float32) * spacing] * 3, indexing="ij"), -1).reshape(-1, 3)
+    g = g[rng.permutation(len(g))]  # lowest index is not the first visited in Morton order
+    return np.concatenate([g, np.zeros((len(g), 1), np.float32)], 1)
+
+
+@pytest.mark.parametrize("side", [9, 16])
+def test_nn_lattice_ties_lowest_index(gpu_ctx, oracle_mod, side):
+    """Integer lattices: most queries sit at exactly equal distance from 2, 4 or 8 targets (exact
+    float ties) — the pruned search must still return the lowest target index."""
+    rng = np.random.default_rng(side)
+    tgt = _lattice(rng, side)
+    q = tgt.copy()
+    q[:, :3] += np.float32(0.25)  # equidistant from 8 lattice points in the interior
+    q[::3, 0] += np.float32(-0.25)  # 4-way ties
+    q[::5, 1] += np.float32(-0.25)  # 2-way ties
+    gi, gd = gpu_ctx.nearest(q, tgt)
+    oi, od = oracle_mod.nearest(q, tgt, oracle_mod.NN_BRUTE)
+    assert (gd == od).all() and (gi == oi).all()
 
 
 # ---------------------------------------------------------------------------------------------- ICP
@@ -140,16 +162,78 @@ def test_batch_equals_single_calls(gpu_ctx):
 
 
 def test_target_split_equals_unsplit(gpu_ctx):
-    """A single pair runs with the target split across workgroups; a 64-pair batch does not."""
+    """Brute force: a single pair runs with the target split across workgroups (atomicMin merge of
+    the keys); a 64-pair batch does not."""
     import icp4r
 
     s, t = _pair(300, 8192)
-    assert icp4r.plan(1, 8192, 8192)["splits"] > 1 and icp4r.plan(64, 8192, 8192)["splits"] == 1
-    p = icp4r.default_params(max_iterations=20)
+    assert icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)["splits"] > 1
+    assert icp4r.plan(64, 8192, 8192, icp4r.NN_BRUTE)["splits"] == 1
+    p = icp4r.default_params(max_iterations=20, nn_mode=icp4r.NN_BRUTE)
     r, _ = gpu_ctx.align(s, t, p)
     res = gpu_ctx.align_batch_host(*_batch([(s, t)] * 64), params=p)
     for k in range(64):
         assert (res[k]["T"] == np.array(r.T, np.float32)).all()
+
+
+@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map"])
+def test_nn_modes_identical(gpu_ctx, case):
+    """Pruned, brute-force and packed searches produce bit-identical registrations (T, fitness,
+    iterations, aligned cloud) — the pruned index changes only which targets are evaluated."""
+    import icp4r
+
+    guess = None
+    if case == "c2":
+        pairs = [_pair(310, 8192)]
+    elif case == "ragged":
+        shapes = [(8192, 8192), (2048, 600), (1000, 1200), (37, 4000), (4096, 64), (8000, 8100), (3, 700)]
+        pairs = [_pair(320 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    elif case == "far_guess":  # iteration-0 seeds far from the answer
+        pairs = [_pair(330, 4096)]
+        g = np.eye(4, dtype=np.float32)
+        g[:3, 3] = [7.0, -5.0, 1.0]
+        c, sn = np.cos(0.4), np.sin(0.4)
+        g[:2, :2] = [[c, -sn], [sn, c]]
+        guess = g
+    elif case == "lattice":
+        rng = np.random.default_rng(7)
+        t = _lattice(rng, 14)
+        sr = t.copy()
+        sr[:, :3] += np.float32(0.25)
+        pairs = [(sr, t)]
+    else:
+        from icp4r import synth
+
+        mp = synth.make_map_pair(1)
+        pairs = [(mp.src_xyzi()[:4096], mp.tgt_xyzi())]
+    p = dict(max_iterations=12, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    if len(pairs) == 1:
+        s, t = pairs[0]
+        out = {}
+        for mode in (icp4r.NN_PRUNED, icp4r.NN_BRUTE, icp4r.NN_BRUTE_PACKED):
+            r, al = gpu_ctx.align(s, t, icp4r.default_params(nn_mode=mode, **p), guess=guess, want_aligned=True)
+            out[mode] = (bytes(r), al.tobytes())
+        assert out[icp4r.NN_PRUNED] == out[icp4r.NN_BRUTE] == out[icp4r.NN_BRUTE_PACKED]
+    else:
+        res = {mode: gpu_ctx.align_batch_host(*_batch(pairs), params=icp4r.default_params(nn_mode=mode, **p))
+               for mode in (icp4r.NN_PRUNED, icp4r.NN_BRUTE)}
+        assert res[icp4r.NN_PRUNED].tobytes() == res[icp4r.NN_BRUTE].tobytes()
+
+
+def test_pruned_evaluates_fewer_pairs(gpu_ctx):
+    """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer."""
+    import icp4r
+
+    s, t = _pair(340, 8192)
+    p = dict(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, compute_fitness=0)
+    gpu_ctx.reset_timers()
+    gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_BRUTE, **p))
+    brute = gpu_ctx.nn_evaluations()
+    assert brute == 5 * len(s) * len(t)
+    gpu_ctx.reset_timers()
+    gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_PRUNED, **p))
+    pruned = gpu_ctx.nn_evaluations()
+    assert 0 < pruned < 0.3 * brute
 
 
 def test_repeatable_and_target_permutation_invariant(gpu_ctx):

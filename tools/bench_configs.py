@@ -38,6 +38,7 @@ def run(name, src, tgt, params, oparams, reps=5):
         walls.append(time.perf_counter() - t0)
     dev_ms, k = ctx.batch_time_ms()
     nn_ms, nk = ctx.kernel_time_ms()
+    evals = ctx.nn_evaluations() / max(nk, 1)
     t0 = time.perf_counter()
     o = oracle.align(src, tgt, **oparams)
     cpu_s = time.perf_counter() - t0
@@ -45,6 +46,7 @@ def run(name, src, tgt, params, oparams, reps=5):
     line = {"config": name, "n": len(src), "m": len(tgt), "iterations": r.iterations,
             "gpu_device_ms": dev_ms, "gpu_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
             "nn_kernel_avg_ms": nn_ms, "nn_launches_per_call": nk // max(k, 1),
+            "nn_evals_per_launch": evals, "nn_evaluated_fraction": evals / (len(src) * len(tgt)),
             "plan": icp4r.plan(1, len(src), len(tgt)),
             "cpu_oracle_ms_1thread": 1e3 * cpu_s, "speedup_device_vs_cpu": 1e3 * cpu_s / dev_ms,
             "bit_exact_vs_oracle": bit_exact}
