@@ -78,7 +78,7 @@ struct icp4r_ctx {
     // staging for the host-buffer entry points
     DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace
-    DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm;
+    DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks;
     std::vector<EventPair> nn_events, batch_events;
     size_t nn_used = 0, batch_used = 0;
     DevBuf evals;  // u64: distance evaluations of the NN kernels since the last reset
@@ -170,6 +170,7 @@ int make_kparams(const icp4r_params* p, KParams* kp) {
     kp->max_d2 = max_d2_threshold(p->max_correspondence_distance);
     kp->huber_delta = p->huber_delta;
     kp->fit_max_range = p->fitness_max_range;
+    kp->need_mse = (p->mse_threshold_absolute > 0 || p->euclidean_fitness_epsilon > 0) ? 1 : 0;
     return ICP4R_OK;
 }
 
@@ -204,7 +205,8 @@ int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
 }
 
 // Size the workspace for a plan and fill WorkArgs.
-int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, hipStream_t st, WorkArgs& w) {
+int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, bool corr, hipStream_t st,
+               WorkArgs& w) {
     const int64_t x_stride = ((max_n > 0 ? max_n : 1) + 3) & ~3;
     const int64_t slots = (int64_t)npairs * x_stride;
     HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
@@ -221,6 +223,14 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, sizeof(uint64_t), st));
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
+    if (env_int("ICP4R_PHASE_TICKS", 0)) {
+        HIP_TRY(ctx->ticks.ensure(8 * sizeof(uint64_t)));
+        w.ticks = static_cast<uint64_t*>(ctx->ticks.p);
+    }
+    if (corr) {
+        HIP_TRY(ctx->corr.ensure((size_t)slots * 2 * sizeof(float4)));
+        w.corr = static_cast<float4*>(ctx->corr.p);
+    }
     if (pl.pruned) {
         const int64_t span = (int64_t)pl.leaf * kSuper;
         w.leaf = pl.leaf;
@@ -266,7 +276,8 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     const Plan pl = make_plan(npairs, mn, max_m, nn_mode);
     WorkArgs w;
     int rc;
-    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, st, w))) return rc;
+    const bool pcl = a.kp.numerics == kNumericsPCL;
+    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl, st, w))) return rc;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
@@ -276,7 +287,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     const int iters = max_iterations > 0 ? max_iterations : 1;
     for (int it = 0; it < iters; ++it) {
         if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
-        HIP_TRY(launch_update(a, w, npairs, st));
+        HIP_TRY(launch_update(a, w, npairs, mn, pcl && !pl.pruned, st));
     }
     if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
     if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, a, w, npairs, mn, 1, 0, st))) return rc;
@@ -324,7 +335,7 @@ int nearest_keys(icp4r_ctx* ctx, const float* query, int32_t n, int32_t qstride,
     if ((rc = make_kparams(nullptr, &a.kp))) return rc;
     const Plan pl = make_plan(1, n, m, ICP4R_NN_AUTO);
     WorkArgs w;
-    if ((rc = setup_work(ctx, pl, 1, n, m, st, w))) return rc;
+    if ((rc = setup_work(ctx, pl, 1, n, m, false, st, w))) return rc;
     HIP_TRY(launch_init(a, w, 1, st));
     if (pl.pruned) HIP_TRY(launch_index(a, w, 1, st));
     if ((rc = nn_pass(ctx, pl, a, w, 1, n, 0, 1, st))) return rc;
@@ -405,7 +416,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals})
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->batch_events})
         for (auto& ev : *v) {
@@ -669,6 +680,17 @@ int icp4r_nn_evaluations(icp4r_ctx* ctx, uint64_t* evaluations) {
     uint64_t v = 0;
     if (ctx->evals.p) HIP_TRY(hipMemcpy(&v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
     *evaluations = v;
+    return ICP4R_OK;
+}
+
+// Internal debug hook (not in icp4r.h): the last fold_update phase timestamps of pair 0 (100 MHz
+// ticks; needs ICP4R_PHASE_TICKS=1 in the environment when the registration ran).
+int icp4r__debug_ticks(icp4r_ctx* ctx, uint64_t* out, int32_t k) {
+    if (!ctx || !out || k <= 0 || k > 8) return fail(ICP4R_E_INVALID, "bad arguments");
+    if (!ctx->ticks.p) return fail(ICP4R_E_INVALID, "phase ticks not enabled (ICP4R_PHASE_TICKS=1)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, ctx->ticks.p, (size_t)k * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return ICP4R_OK;
 }
 

@@ -14,7 +14,7 @@ constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_ke
 constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.py)
 constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
-constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential centroid fold
+constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
 constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
 
@@ -41,6 +41,8 @@ struct KParams {
     float max_d2;          // reject a correspondence iff d2 > max_d2 (float image of max_dist^2)
     double huber_delta;    // +inf: unweighted (PCL)
     double fit_max_range;  // getFitnessScore(max_range): keep d2 <= max_range
+    int32_t need_mse;      // 0 when no MSE criterion can fire (both thresholds <= 0): the MSE only
+                           // feeds those two '<' tests, so its sequential sum is skipped
 };
 
 struct PairArgs {
@@ -100,7 +102,10 @@ struct WorkArgs {
     float4* sbox;       // [npairs * 2 * sb_stride] per superblock of kSuper blocks: lo, hi
     int32_t* sperm;     // [npairs * x_stride] source indices in Morton-cell order
     int64_t t_stride, b_stride, sb_stride;
-    unsigned long long* evals;  // distance evaluations of valid queries (one atomic per wave / workgroup)
+    float4* corr;       // PCL numerics: [npairs * x_stride * 2] per source point {s.xyz, w}, {d.xyz, d²}
+    unsigned long long* evals;
+    uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
+                        // boundaries of pair 0 — start, pass A, pass B, solve, transform  // distance evaluations of valid queries (one atomic per wave / workgroup)
 };
 
 hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
@@ -109,7 +114,8 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
                             int first, hipStream_t st);
-hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
+hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
+                         hipStream_t st);
 hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);

@@ -183,6 +183,20 @@ __device__ __forceinline__ NNKey make_key(float d2, uint32_t idx) {
     return ((NNKey)__float_as_uint(d2) << 32) | idx;
 }
 
+// Correspondence records (PCL numerics): per source point, in source-index order (the fold order),
+// two float4 at corr + (p*x_stride + i)*2: {s.xyz (the transformed source point searched with),
+// w (Huber weight, 1 unweighted)}, {d.xyz (its nearest target), d² (float, as FLANN returned it)}.
+// Written by the pruned NN kernel's tail, or by corr_kernel after a brute-force pass.
+__device__ __forceinline__ void write_corr(const WorkArgs& w, const PairArgs& a, int p, int i, float sx, float sy,
+                                           float sz, NNKey k, const float4* tgt) {
+    float4* C = w.corr + ((int64_t)p * w.x_stride + i) * 2;
+    const float d2 = key_d2(k);
+    const float4 t = tgt[key_idx(k)];
+    const float wt = a.kp.huber_delta < INFINITY ? (float)huber_w(d2, a.kp.huber_delta) : 1.0f;
+    C[0] = make_float4(sx, sy, sz, wt);
+    C[1] = make_float4(t.x, t.y, t.z, d2);
+}
+
 // ---------------------------------------------------------------------------------------------
 // init_kernel: one workgroup per pair.
 constexpr int kInitWG = 256;
@@ -474,6 +488,18 @@ __device__ __forceinline__ bool box_needed(const v4f lo, const v4f hi, const flo
     return __any(need);
 }
 
+// Coarse (wave-uniform) test: distance between the (super)block box and the box of all the wave's
+// queries against the largest best d² of the wave — a few VALU ops on uniform values instead of
+// Q per-query tests; only (super)blocks that pass it get the per-query test.
+__device__ __forceinline__ bool box_maybe(const v4f lo, const v4f hi, const float (&qlo)[3], const float (&qhi)[3],
+                                          float qmax) {
+    const float gx = fmaxf(fmaxf(lo.x - qhi[0], qlo[0] - hi.x), 0.0f);
+    const float gy = fmaxf(fmaxf(lo.y - qhi[1], qlo[1] - hi.y), 0.0f);
+    const float gz = fmaxf(fmaxf(lo.z - qhi[2], qlo[2] - hi.z), 0.0f);
+    const float lb = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+    return lb * kLbShrink <= qmax;
+}
+
 template <int Q, int B>
 __device__ __forceinline__ void sweep_block(cv4f_ptr blk, const float (&x)[Q], const float (&y)[Q], const float (&z)[Q],
                                             NNKey (&best)[Q]) {
@@ -523,6 +549,33 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
         const float4 t = tgt[j];
         best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
     }
+    // the wave's query box and its largest seed distance (uniform; best only shrinks from here on)
+    float qlo[3], qhi[3], qmax = 0.0f;
+    qlo[0] = qhi[0] = x[0];
+    qlo[1] = qhi[1] = y[0];
+    qlo[2] = qhi[2] = z[0];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        qlo[0] = fminf(qlo[0], x[q]); qhi[0] = fmaxf(qhi[0], x[q]);
+        qlo[1] = fminf(qlo[1], y[q]); qhi[1] = fmaxf(qhi[1], y[q]);
+        qlo[2] = fminf(qlo[2], z[q]); qhi[2] = fmaxf(qhi[2], z[q]);
+        qmax = fmaxf(qmax, key_d2(best[q]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
+            qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
+        }
+        qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
+        qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
+    }
+    qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
     const int nb = (m + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
     const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
     const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (B * kSuper);
@@ -532,115 +585,92 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
     int up = sb0, dn = sb0 - 1, swept = 0;
     for (int k = 0; k < nsb; ++k) {
         const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
-        if (!box_needed<Q>(sbx[2 * sb], sbx[2 * sb + 1], x, y, z, best)) continue;
+        const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+        if (!box_maybe(slo, shi, qlo, qhi, qmax) || !box_needed<Q>(slo, shi, x, y, z, best)) continue;
         for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {  // blocks past nb have empty boxes
-            if (!box_needed<Q>(tb[2 * b], tb[2 * b + 1], x, y, z, best)) continue;
+            const v4f blo = tb[2 * b], bhi = tb[2 * b + 1];
+            if (!box_maybe(blo, bhi, qlo, qhi, qmax) || !box_needed<Q>(blo, bhi, x, y, z, best)) continue;
             sweep_block<Q, B>(ts + (int64_t)b * B, x, y, z, best);
             ++swept;
         }
     }
     if (lane == 0)
         atomicAdd(w.evals, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
+    if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence arrays
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (orig[q] >= 0) write_corr(w, a, p, orig[q], x[q], y[q], z[q], best[q], tgt);
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         if (orig[q] >= 0) key[orig[q]] = best[q];
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sequential folds over an LDS chunk, one lane per chain.  The order of the additions is exactly
-// the reference loop's; the loads are issued 16 ahead (ds_read_b128) so the chain runs at the
-// dependent-add latency instead of the LDS round trip per element.
-__device__ __forceinline__ float fold_f32(const float* f, int len, float acc) {
+// Sequential folds over an LDS chunk, one lane per chain: acc = acc + f[k] for k in [0, len), in
+// that order — exactly the reference loop.  Groups of 32 floats are read 32 elements ahead in two
+// explicit register sets (a/b ping-pong) so the chain runs at the dependent-add latency instead of
+// waiting on each LDS round trip.  TAcc = float (the float chains) or double (MSE / fitness: the
+// float values are widened, as PCL's double accumulators do).
+template <typename TAcc>
+__device__ __forceinline__ void add_group(TAcc& acc, const float4 (&g)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        acc = acc + (TAcc)g[u].x;
+        acc = acc + (TAcc)g[u].y;
+        acc = acc + (TAcc)g[u].z;
+        acc = acc + (TAcc)g[u].w;
+    }
+}
+
+__device__ __forceinline__ void load_group(float4 (&g)[8], const float* f) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) g[u] = *reinterpret_cast<const float4*>(f + 4 * u);
+}
+
+template <typename TAcc>
+__device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
     int k = 0;
-    for (; k + 16 <= len; k += 16) {
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(f + k + 4 * u);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            acc = acc + v[u].x;
-            acc = acc + v[u].y;
-            acc = acc + v[u].z;
-            acc = acc + v[u].w;
+    if (len >= 32) {
+        float4 a[8], b[8];
+        load_group(a, f);
+        int apos = 0;  // where `a` was loaded from
+        // sched_barrier: keep each prefetch ahead of the adds it overlaps (the scheduler would
+        // otherwise sink the loads down to their first use and expose the LDS latency again)
+        for (; k + 64 <= len; k += 64) {
+            load_group(b, f + k + 32);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group(acc, a);
+            apos = (k + 96 <= len) ? k + 64 : k;  // next group, or a harmless re-read
+            load_group(a, f + apos);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group(acc, b);
+        }
+        if (k + 32 <= len) {
+            if (apos != k) load_group(a, f + k);
+            add_group(acc, a);
+            k += 32;
         }
     }
-    for (; k < len; ++k) acc = acc + f[k];
+    for (; k < len; ++k) acc = acc + (TAcc)f[k];
     return acc;
 }
 
-__device__ __forceinline__ double fold_f64(const double* f, int len, double acc) {
-    int k = 0;
-    for (; k + 8 <= len; k += 8) {
-        double2 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const double2*>(f + k + 2 * u);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            acc = acc + v[u].x;
-            acc = acc + v[u].y;
-        }
-    }
-    for (; k < len; ++k) acc = acc + f[k];
-    return acc;
-}
-
-// sigma chain: acc = a*b + acc (oracle umeyama_f32, unweighted)
-__device__ __forceinline__ float fold_prod_f32(const float* fa, const float* fb, int len, float acc) {
-    int k = 0;
-    for (; k + 8 <= len; k += 8) {
-        float4 a[2], b[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            a[u] = *reinterpret_cast<const float4*>(fa + k + 4 * u);
-            b[u] = *reinterpret_cast<const float4*>(fb + k + 4 * u);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            acc = a[u].x * b[u].x + acc;
-            acc = a[u].y * b[u].y + acc;
-            acc = a[u].z * b[u].z + acc;
-            acc = a[u].w * b[u].w + acc;
-        }
-    }
-    for (; k < len; ++k) acc = fa[k] * fb[k] + acc;
-    return acc;
-}
-
-// Huber sigma chain: acc = acc + (w*a)*b (oracle umeyama_f32, weighted)
-__device__ __forceinline__ float fold_wprod_f32(const float* fw, const float* fa, const float* fb, int len, float acc) {
-    int k = 0;
-    for (; k + 4 <= len; k += 4) {
-        const float4 w = *reinterpret_cast<const float4*>(fw + k);
-        const float4 a = *reinterpret_cast<const float4*>(fa + k);
-        const float4 b = *reinterpret_cast<const float4*>(fb + k);
-        acc = acc + w.x * a.x * b.x;
-        acc = acc + w.y * a.y * b.y;
-        acc = acc + w.z * a.z * b.z;
-        acc = acc + w.w * a.w * b.w;
-    }
-    for (; k < len; ++k) acc = acc + fw[k] * fa[k] * fb[k];
-    return acc;
+// Brute-force path: the correspondence arrays from the merged NN keys (the pruned kernel writes
+// them itself).
+__global__ __launch_bounds__(256) void corr_kernel(PairArgs a, WorkArgs w) {
+    const int p = blockIdx.y;
+    if (uload(&w.state[p].phase) != kPhaseActive) return;
+    const int n = uload(a.src_n + p);
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 s = w.X[(int64_t)p * w.x_stride + i];
+    write_corr(w, a, p, i, s.x, s.y, s.z, w.nn_key[(int64_t)p * w.x_stride + i], a.tgt + uload(a.tgt_off + p));
 }
 
 // ---------------------------------------------------------------------------------------------
-// update_kernel<NUM>: one workgroup per active pair: correspondences -> moments -> solve ->
-// convergence -> X := T_inc * X (in place, float, PCL transformCloud order).
-constexpr int kUpdWG = 512;
-constexpr int kUpdWaves = kUpdWG / 64;
-constexpr int kFoldCh = 7;  // fold chains: s.xyz, d.xyz, weight (== validity when unweighted)
-
-template <int NUM> struct MomLayout;
-template <> struct MomLayout<kNumericsPCL> {  // |C| only: every other sum is a sequential fold
-    static constexpr int N = 1, CNT = 0;
-};
-template <> struct MomLayout<kNumericsF64> {  // Σ w·d·sᵀ [9], Σ w·s [3], Σ w·d [3], Σ w, Σ d², |C|
-    static constexpr int N = 18, MSE = 16, CNT = 17;
-};
-
-struct UpdShared {
-    float fold[kFoldCh + 2][kFoldChunk];  // pass A: 7 float chains; pass B: s'xyz, d'xyz, w
-    double dfold[kFoldChunk];             // pass A: d² (MSE chain, double)
-    double red[kUpdWaves * 20];
+// The 3x3 solve and convergence test of one pair (thread 0), shared by both numerics.
+struct SolveShared {
     double mom[20];
     double sigma[9], ms[3], md[3];
     SvdWork svd;
@@ -653,9 +683,16 @@ struct UpdShared {
     int32_t flag;  // 0 continue, 1 error (no transform), 2 converged after this transform
 };
 
-// Thread 0: count check, Umeyama solve, final := T_inc * final, hasConverged (all in LDS/state).
+template <int NUM> struct MomLayout;
+template <> struct MomLayout<kNumericsPCL> {  // |C| only: every other sum is a sequential fold
+    static constexpr int N = 1, CNT = 0;
+};
+template <> struct MomLayout<kNumericsF64> {  // Σ w·d·sᵀ [9], Σ w·s [3], Σ w·d [3], Σ w, Σ d², |C|
+    static constexpr int N = 18, MSE = 16, CNT = 17;
+};
+
 template <int NUM>
-__device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
+__device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
     constexpr int I_CNT = MomLayout<NUM>::CNT;
     const int cnt = (int)sh.mom[I_CNT];
     st.ncorr = cnt;
@@ -671,7 +708,7 @@ __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
     mat4_identity(Tinc);
     double mse;
     if constexpr (NUM == kNumericsPCL) {
-        // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (the fold above), float SVD,
+        // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (the fold), float SVD,
         // R as Matrix4f, Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean.
         for (int k = 0; k < 9; ++k) sh.sigmaf[k] = sh.one_over_n * sh.sigmaf[k];
         umeyama_rotation_f32(sh.sigmaf, sh.svdf);
@@ -714,11 +751,199 @@ __device__ void solve_pair(UpdShared& sh, PairState& st, const KParams& kp) {
     sh.flag = conv ? 2 : 0;
 }
 
-template <int NUM>
-__global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) {
-    constexpr int NM = MomLayout<NUM>::N;
-    constexpr int I_CNT = MomLayout<NUM>::CNT;
-    __shared__ UpdShared sh;
+// transformCloud(*input_transformed, *input_transformed, transformation_) by the whole workgroup.
+template <int WG>
+__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds) {
+    float Tl[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) Tl[k] = T_lds[k];
+    for (int i = threadIdx.x; i < n; i += WG) {
+        float4 s = X[i];
+        xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
+        X[i] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fold_update_kernel (PCL numerics): one workgroup per active pair.  Bit-exact float restatement
+// of TransformationEstimationSVD (use_umeyama, Scalar = float) and calculateMSE: every sum is the
+// sequential fold the reference performs, in correspondence (= source index) order, one lane per
+// chain, over LDS chunks that the filler waves stage from the correspondence arrays while the
+// fold lanes consume the previous chunk (double buffer: a fold never waits for a gather).
+//  pass A: wave 0 lanes 0..6: Σs, Σd (Eigen 3.3 rowwise().sum(): fold from the first element ==
+//          fold from -0.0f; Huber: fold of w·x from +0) and Σw (== |C| unweighted);
+//          wave 1 lane 0: Σd² in double (MSE) — only when an MSE criterion is live (KParams::
+//          need_mse), else wave 1 fills too.  Fillers: waves 2, 3.
+//  pass B: wave 0 lanes 0..8: sigma(a, b) = Σ d'_a s'_b (float, from +0) over the float-demeaned
+//          points; the fillers (waves 1..3) form the products (a*b, Huber (w*a)*b) so every chain is
+//          a plain sum — IEEE addition is commutative, so p + acc == a*b + acc bit for bit.
+// Rejected correspondences contribute the fold's identity (-0.0f / +0), i.e. nothing.
+constexpr int kFoldWG = 256;
+constexpr int kFoldWaves = kFoldWG / 64;
+constexpr int kFoldChunkP = 512;
+
+struct FoldShared {
+    float buf[2][9][kFoldChunkP];
+    float res[8];
+    int32_t cnt[kFoldWaves];
+    SolveShared s;
+};
+
+__global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkArgs w) {
+    __shared__ FoldShared sh;
+    const int p = blockIdx.x;
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.src_n[p];
+    const int64_t xs = w.x_stride;
+    const float4* C = w.corr + (int64_t)p * xs * 2;
+    const KParams& kp = a.kp;
+    const bool weighted = kp.huber_delta < INFINITY;
+    const bool mse = kp.need_mse != 0;  // wave 1 runs the MSE chain in pass A, else it fills
+    const float ident = weighted ? 0.0f : -0.0f;
+    const int nch = (n + kFoldChunkP - 1) / kFoldChunkP;
+    const int fill0 = mse ? 128 : 64;  // first filler thread of pass A
+
+    const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
+    if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
+    // ---- pass A
+    int cnt = 0;
+    // Fillers issue every load of their (at most kPerA) elements before the first LDS store, so a
+    // chunk costs one global round trip, not one per element.
+    constexpr int kPerA = (kFoldChunkP + (kFoldWG - 128) - 1) / (kFoldWG - 128);
+    auto fill_a = [&](int c) {  // waves 2, 3 (and 1 without the MSE chain)
+        float(*b)[kFoldChunkP] = sh.buf[c & 1];
+        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
+        float4 r[kPerA][2];
+#pragma unroll
+        for (int e = 0; e < kPerA; ++e) {
+            const int i = base + min(tid - fill0 + e * nf, len - 1);
+            r[e][0] = C[2 * i];
+            r[e][1] = C[2 * i + 1];
+        }
+#pragma unroll
+        for (int e = 0; e < kPerA; ++e) {
+            const int o = tid - fill0 + e * nf;
+            if (o >= len) break;
+            const float d2 = r[e][1].w;
+            const float sv[6] = {r[e][0].x, r[e][0].y, r[e][0].z, r[e][1].x, r[e][1].y, r[e][1].z};
+            float v[6], wt = 0.0f, dd = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v[k] = ident;
+            if (!(d2 > kp.max_d2)) {
+                wt = r[e][0].w;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) v[k] = weighted ? wt * sv[k] : sv[k];
+                dd = d2;
+                ++cnt;
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) b[k][o] = v[k];
+            b[6][o] = wt;
+            b[7][o] = dd;
+        }
+    };
+    float acc = (lane < 6) ? ident : 0.0f;
+    double dacc = 0.0;
+    if (tid >= fill0 && nch > 0) fill_a(0);
+    for (int c = 0; c < nch; ++c) {
+        __syncthreads();
+        const int len = min(kFoldChunkP, n - c * kFoldChunkP);
+        if (wave == 0) {
+            if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], len, acc);
+        } else if (tid < fill0) {
+            if (lane == 0) dacc = fold_seq<double>(sh.buf[c & 1][7], len, dacc);
+        } else if (c + 1 < nch) {
+            fill_a(c + 1);
+        }
+    }
+    // |C|: exact integer reduction of the fillers' counts
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0) sh.cnt[wave] = cnt;
+    if (wave == 0 && lane < 7) sh.res[lane] = acc;
+    if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
+    __syncthreads();
+    if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+        int total = 0;
+        for (int k = 0; k < kFoldWaves; ++k) total += sh.cnt[k];
+        sh.s.mom[0] = (double)total;
+        // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
+        const float one_over_n = 1.0f / sh.res[6];
+        sh.s.one_over_n = one_over_n;
+        for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
+    }
+    __syncthreads();
+
+    // ---- pass B
+    const float ms[3] = {sh.s.mean[0], sh.s.mean[1], sh.s.mean[2]};
+    const float md[3] = {sh.s.mean[3], sh.s.mean[4], sh.s.mean[5]};
+    constexpr int kFillB = kFoldWG - 64, kPerB = (kFoldChunkP + kFillB - 1) / kFillB;
+    auto fill_b = [&](int c) {  // waves 1..3
+        float(*b)[kFoldChunkP] = sh.buf[c & 1];
+        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
+        float4 r[kPerB][2];
+#pragma unroll
+        for (int e = 0; e < kPerB; ++e) {
+            const int i = base + min(tid - 64 + e * kFillB, len - 1);
+            r[e][0] = C[2 * i];
+            r[e][1] = C[2 * i + 1];
+        }
+#pragma unroll
+        for (int e = 0; e < kPerB; ++e) {
+            const int o = tid - 64 + e * kFillB;
+            if (o >= len) break;
+            float sv[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f}, wt = 0.f;
+            if (!(r[e][1].w > kp.max_d2)) {
+                sv[0] = r[e][0].x - ms[0];
+                sv[1] = r[e][0].y - ms[1];
+                sv[2] = r[e][0].z - ms[2];
+                dv[0] = r[e][1].x - md[0];
+                dv[1] = r[e][1].y - md[1];
+                dv[2] = r[e][1].z - md[2];
+                wt = r[e][0].w;
+            }
+#pragma unroll
+            for (int ra = 0; ra < 3; ++ra)
+#pragma unroll
+                for (int rb = 0; rb < 3; ++rb) b[ra * 3 + rb][o] = weighted ? (wt * dv[ra]) * sv[rb] : dv[ra] * sv[rb];
+        }
+    };
+    float sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b)
+    if (wave >= 1 && nch > 0) fill_b(0);
+    for (int c = 0; c < nch; ++c) {
+        __syncthreads();
+        if (wave == 0) {
+            if (lane < 9) sacc = fold_seq<float>(sh.buf[c & 1][lane], min(kFoldChunkP, n - c * kFoldChunkP), sacc);
+        } else if (c + 1 < nch) {
+            fill_b(c + 1);
+        }
+    }
+    if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sacc;
+    __syncthreads();
+    if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) solve_pair<kNumericsPCL>(sh.s, st, kp);
+    __syncthreads();
+    if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
+    if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
+    transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
+    __syncthreads();
+    if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---------------------------------------------------------------------------------------------
+// update_kernel (F64 numerics): one workgroup per active pair: correspondences -> double moments
+// (fixed-order block reduction) -> solve -> convergence -> X := T_inc * X.
+constexpr int kUpdWG = 512;
+constexpr int kUpdWaves = kUpdWG / 64;
+
+__global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs w) {
+    constexpr int NM = MomLayout<kNumericsF64>::N;
+    constexpr int I_CNT = MomLayout<kNumericsF64>::CNT;
+    __shared__ SolveShared sh;
+    __shared__ double red[kUpdWaves * NM];
     const int p = blockIdx.x;
     PairState& st = w.state[p];
     if (st.phase != kPhaseActive) return;
@@ -729,143 +954,33 @@ __global__ __launch_bounds__(kUpdWG) void update_kernel(PairArgs a, WorkArgs w) 
     const int64_t slot0 = (int64_t)p * w.x_stride;
     const KParams& kp = a.kp;
     const bool weighted = kp.huber_delta < INFINITY;
-
     double mom[NM];
 #pragma unroll
     for (int k = 0; k < NM; ++k) mom[k] = 0.0;
-
-    if constexpr (NUM == kNumericsPCL) {
-        // Bit-exact float restatement of TransformationEstimationSVD (use_umeyama, Scalar = float)
-        // and calculateMSE: every sum is the sequential fold the reference performs, in
-        // correspondence (= source index) order, by one lane per chain of wave 0 over LDS chunks.
-        //  pass A: Σs, Σd (Eigen 3.3 rowwise().sum(): fold from the first element == fold from -0.0f;
-        //          Huber: fold of w·x from +0), Σw (== |C| unweighted), Σd² in double (MSE).
-        //  pass B: Σ d'_a s'_b (sigma, float, from +0) over the float-demeaned points.
-        // Rejected correspondences contribute the fold's identity (-0.0f / +0), i.e. nothing.
-        const int lane = tid & 63, wave = tid >> 6;
-        const float ident = weighted ? 0.0f : -0.0f;
-        float acc = (lane < 6) ? ident : 0.0f;
-        double dacc = 0.0;
-        double cntd = 0.0;
-        for (int base = 0; base < n; base += kFoldChunk) {
-            for (int o = tid; o < kFoldChunk && base + o < n; o += kUpdWG) {
-                const int i = base + o;
-                float d2;
-                int j;
-                load_nn(w, slot0 + i, d2, j);
-                float wt = 0.f, sx = ident, sy = ident, sz = ident, dx = ident, dy = ident, dz = ident;
-                double dd = 0.0;
-                if (!(d2 > kp.max_d2)) {
-                    const float4 s = X[i];
-                    const float4 d = tgt[j];
-                    if (weighted) {
-                        wt = (float)huber_w(d2, kp.huber_delta);
-                        sx = wt * s.x; sy = wt * s.y; sz = wt * s.z;
-                        dx = wt * d.x; dy = wt * d.y; dz = wt * d.z;
-                    } else {
-                        wt = 1.0f;
-                        sx = s.x; sy = s.y; sz = s.z;
-                        dx = d.x; dy = d.y; dz = d.z;
-                    }
-                    dd = (double)d2;
-                    cntd += 1.0;
-                }
-                sh.fold[0][o] = sx; sh.fold[1][o] = sy; sh.fold[2][o] = sz;
-                sh.fold[3][o] = dx; sh.fold[4][o] = dy; sh.fold[5][o] = dz;
-                sh.fold[6][o] = wt;
-                sh.dfold[o] = dd;
-            }
-            __syncthreads();
-            if (wave == 0 && lane < 8) {
-                const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
-                if (lane < kFoldCh) {
-                    acc = fold_f32(sh.fold[lane], len, acc);
-                } else {
-                    dacc = fold_f64(sh.dfold, len, dacc);
-                }
-            }
-            __syncthreads();
-        }
-        mom[I_CNT] = cntd;
-        if (wave == 0 && lane < kFoldCh) sh.fold[lane][0] = acc;
-        if (wave == 0 && lane == 7) sh.mse_sum = dacc;
-        __syncthreads();
-        if (tid == 0) {
-            // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
-            const float one_over_n = 1.0f / sh.fold[6][0];
-            sh.one_over_n = one_over_n;
-            for (int c = 0; c < 6; ++c) sh.mean[c] = sh.fold[c][0] * one_over_n;
-        }
-        __syncthreads();
-        const float msx = sh.mean[0], msy = sh.mean[1], msz = sh.mean[2];
-        const float mdx = sh.mean[3], mdy = sh.mean[4], mdz = sh.mean[5];
-        float sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b)
-        const int ca = lane / 3, cb = lane % 3;
-        for (int base = 0; base < n; base += kFoldChunk) {
-            for (int o = tid; o < kFoldChunk && base + o < n; o += kUpdWG) {
-                const int i = base + o;
-                float d2;
-                int j;
-                load_nn(w, slot0 + i, d2, j);
-                float wt = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, d0 = 0.f, d1 = 0.f, dv2 = 0.f;
-                if (!(d2 > kp.max_d2)) {
-                    const float4 s = X[i];
-                    const float4 d = tgt[j];
-                    s0 = s.x - msx; s1 = s.y - msy; s2 = s.z - msz;
-                    d0 = d.x - mdx; d1 = d.y - mdy; dv2 = d.z - mdz;
-                    wt = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
-                }
-                sh.fold[0][o] = s0; sh.fold[1][o] = s1; sh.fold[2][o] = s2;
-                sh.fold[3][o] = d0; sh.fold[4][o] = d1; sh.fold[5][o] = dv2;
-                sh.fold[6][o] = wt;
-            }
-            __syncthreads();
-            if (wave == 0 && lane < 9) {
-                const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
-                const float* fa = sh.fold[3 + ca];
-                const float* fb = sh.fold[cb];
-                if (weighted)
-                    sacc = fold_wprod_f32(sh.fold[6], fa, fb, len, sacc);
-                else
-                    sacc = fold_prod_f32(fa, fb, len, sacc);
-            }
-            __syncthreads();
-        }
-        if (wave == 0 && lane < 9) sh.sigmaf[lane] = sacc;
-    } else {
-        for (int i = tid; i < n; i += kUpdWG) {
-            float d2;
-            int j;
-            load_nn(w, slot0 + i, d2, j);
-            if (d2 > kp.max_d2) continue;
-            const float4 s = X[i];
-            const float4 d = tgt[j];
-            const double wt = weighted ? huber_w(d2, kp.huber_delta) : 1.0;
-            const double s0 = s.x, s1 = s.y, s2 = s.z;
-            const double w0 = wt * (double)d.x, w1 = wt * (double)d.y, w2 = wt * (double)d.z;
-            mom[0] += w0 * s0; mom[1] += w0 * s1; mom[2] += w0 * s2;
-            mom[3] += w1 * s0; mom[4] += w1 * s1; mom[5] += w1 * s2;
-            mom[6] += w2 * s0; mom[7] += w2 * s1; mom[8] += w2 * s2;
-            mom[9] += wt * s0; mom[10] += wt * s1; mom[11] += wt * s2;
-            mom[12] += w0; mom[13] += w1; mom[14] += w2;
-            mom[15] += wt;
-            mom[MomLayout<kNumericsF64>::MSE] += (double)d2;
-            mom[I_CNT] += 1.0;
-        }
-    }
-    block_sum<NM, kUpdWaves>(mom, sh.red, sh.mom);
-    if (tid == 0) solve_pair<NUM>(sh, st, kp);
-    __syncthreads();
-    if (sh.flag == 1) return;  // error: PCL breaks before transforming
-    // transformCloud(*input_transformed, *input_transformed, transformation_)
-    float Tl[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) Tl[k] = sh.T_inc[k];
     for (int i = tid; i < n; i += kUpdWG) {
-        float4 s = X[i];
-        xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
-        X[i] = s;
+        float d2;
+        int j;
+        load_nn(w, slot0 + i, d2, j);
+        if (d2 > kp.max_d2) continue;
+        const float4 s = X[i];
+        const float4 d = tgt[j];
+        const double wt = weighted ? huber_w(d2, kp.huber_delta) : 1.0;
+        const double s0 = s.x, s1 = s.y, s2 = s.z;
+        const double w0 = wt * (double)d.x, w1 = wt * (double)d.y, w2 = wt * (double)d.z;
+        mom[0] += w0 * s0; mom[1] += w0 * s1; mom[2] += w0 * s2;
+        mom[3] += w1 * s0; mom[4] += w1 * s1; mom[5] += w1 * s2;
+        mom[6] += w2 * s0; mom[7] += w2 * s1; mom[8] += w2 * s2;
+        mom[9] += wt * s0; mom[10] += wt * s1; mom[11] += wt * s2;
+        mom[12] += w0; mom[13] += w1; mom[14] += w2;
+        mom[15] += wt;
+        mom[MomLayout<kNumericsF64>::MSE] += (double)d2;
+        mom[I_CNT] += 1.0;
     }
+    block_sum<NM, kUpdWaves>(mom, red, sh.mom);
+    if (tid == 0) solve_pair<kNumericsF64>(sh, st, kp);
+    __syncthreads();
+    if (sh.flag == 1) return;
+    transform_pair<kUpdWG>(X, n, sh.T_inc);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -897,40 +1012,40 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     const int64_t slot0 = (int64_t)p * w.x_stride;
     const bool have = st.phase != kPhaseInvalid && a.kp.compute_fitness && n > 0;
     // Registration::getFitnessScore: sequential double sum over points with d² <= max_range, in
-    // index order (one lane over LDS chunks), so the score is bit-identical to the reference loop.
-    __shared__ double chunk[kFoldChunk];
-    double fsum = 0.0, fcnt = 0.0;
+    // index order, by wave 0 lane 0 over LDS chunks that waves 1..3 stage (double buffer); points
+    // beyond max_range contribute +0 (a no-op on the non-negative running sum); the count is an
+    // exact integer reduction.  Bit-identical to the reference loop.
+    __shared__ float chunk[2][kFoldChunkP];
+    __shared__ int32_t fcnt_w[kFinWG / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double fsum = 0.0;
+    int fcnt = 0;
     if (have) {
-        for (int base = 0; base < n; base += kFoldChunk) {
-            for (int o = threadIdx.x; o < kFoldChunk && base + o < n; o += kFinWG) {
-                float d2;
-                int j;
-                load_nn(w, slot0 + base + o, d2, j);
-                chunk[o] = ((double)d2 <= a.kp.fit_max_range) ? (double)d2 : -1.0;
+        const int nch = (n + kFoldChunkP - 1) / kFoldChunkP;
+        auto fill = [&](int c) {
+            const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
+            for (int o = threadIdx.x - 64; o < len; o += kFinWG - 64) {
+                const float d2 = key_d2(w.nn_key[slot0 + base + o]);
+                const bool in = (double)d2 <= a.kp.fit_max_range;
+                chunk[c & 1][o] = in ? d2 : 0.0f;
+                fcnt += in ? 1 : 0;
             }
+        };
+        if (wave >= 1) fill(0);
+        for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (threadIdx.x == 0) {
-                const int len = (n - base) < kFoldChunk ? (n - base) : kFoldChunk;
-                int k = 0;
-                for (; k + 8 <= len; k += 8) {  // loads hoisted ahead of the dependent adds
-                    double v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = chunk[k + u];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        if (v[u] >= 0.0) {
-                            fsum = fsum + v[u];
-                            fcnt += 1.0;
-                        }
-                }
-                for (; k < len; ++k)
-                    if (chunk[k] >= 0.0) {
-                        fsum = fsum + chunk[k];
-                        fcnt += 1.0;
-                    }
+            if (wave == 0) {
+                if (lane == 0) fsum = fold_seq<double>(chunk[c & 1], min(kFoldChunkP, n - c * kFoldChunkP), fsum);
+            } else if (c + 1 < nch) {
+                fill(c + 1);
             }
-            __syncthreads();
         }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) fcnt += __shfl_xor(fcnt, off, 64);
+        if (lane == 0) fcnt_w[wave] = fcnt;
+        __syncthreads();
+        fcnt = 0;
+        for (int k = 0; k < kFinWG / 64; ++k) fcnt += fcnt_w[k];
     }
     if (a.aligned && st.phase != kPhaseInvalid) {
         const float4* src = a.src + a.src_off[p];
@@ -1034,11 +1149,14 @@ hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npa
     return hipGetLastError();
 }
 
-hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
-    if (a.kp.numerics == kNumericsPCL)
-        hipLaunchKernelGGL(update_kernel<kNumericsPCL>, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
-    else
-        hipLaunchKernelGGL(update_kernel<kNumericsF64>, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
+hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr, hipStream_t st) {
+    if (a.kp.numerics == kNumericsPCL) {
+        if (need_corr)
+            hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
+        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w);
+    } else {
+        hipLaunchKernelGGL(update_f64_kernel, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
+    }
     return hipGetLastError();
 }
 

@@ -55,17 +55,25 @@ def run(name, src, tgt, params, oparams, reps=5):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="C1,C2,C5")
+    only = ap.parse_args().only.split(",")
     # C1: the reference-default CPU config (PCL defaults, 10 iterations, early stop live)
     p = synth.make_pair(0, 2048)
-    run("C1", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(), {"numerics": oracle.NUM_F32})
+    if "C1" in only:
+        run("C1", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(), {"numerics": oracle.NUM_F32})
     fixed = dict(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     # C2: single 8k pair, 20 iterations
     p = synth.make_pair(1, 8192)
-    run("C2", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed))
+    if "C2" in only:
+        run("C2", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed))
     # C5: 8k scan vs 64k map (10 accumulated scans)
     p = synth.make_map_pair(0)
-    run("C5", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed),
-        reps=3)
+    if "C5" in only:
+        run("C5", p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed),
+            reps=3)
 
 
 if __name__ == "__main__":
