@@ -91,6 +91,7 @@ struct Plan {
     bool packed;  // brute force: v_pk_* FP32 sweep (two queries per register pair)
     int splits;   // brute force: target splits
     bool pruned;  // Morton-block pruned exact search
+    bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
     int leaf;     // pruned: targets per block
     int64_t blocks;
 };
@@ -112,6 +113,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
+    pl.lds = false;
     pl.splits = 1;
     pl.leaf = 0;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
@@ -124,6 +126,14 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
         pl.leaf = (leaf == 16 || leaf == 32) ? leaf : kDefaultLeaf;
         while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) * (kNNWG / 64) < 8192) pl.q /= 2;
         pl.blocks = (int64_t)npairs * qblocks(pl.q);
+        // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides)
+        const int lds = env_int("ICP4R_NN_LDS", -1);
+        const bool fits = pl.leaf == 16 && max_m <= kLdsMaxTargets;
+        pl.lds = fits && (lds == 1 || (lds < 0 && npairs >= kLdsMinPairs));
+        if (pl.lds) {
+            pl.q = 2;
+            pl.blocks = npairs;
+        }
         return pl;
     }
     const int64_t want = 2048;
@@ -258,7 +268,9 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
     int r;
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
     HIP_TRY(hipEventRecord(ne->start, st));
-    if (pl.pruned) {
+    if (pl.lds) {
+        HIP_TRY(launch_nn_lds(a, w, npairs, fitness_pass, first, st));
+    } else if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));
@@ -669,6 +681,8 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
     out->q = pl.q;
     out->splits = pl.splits;
     out->leaf = pl.leaf;
+    out->lds = pl.lds ? 1 : 0;
+    out->reserved = 0;
     out->nn_blocks = pl.blocks;
     return ICP4R_OK;
 }

@@ -54,6 +54,17 @@ __device__ __forceinline__ T uload(const T* p) {
     return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
 }
 
+// XCD-aware work mapping.  Workgroups are dispatched round-robin over the 8 XCDs (linear id mod 8),
+// each with its own L2.  Remap linear id L of `total` so that XCD x receives the contiguous work
+// range [x*per + min(x, rem), ...): every workgroup of a pair then runs on one XCD, and a pair's
+// target index / correspondence records are fetched into one L2 instead of eight.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+    const int per = total / kXcds, rem = total % kXcds;
+    const int xcd = L % kXcds, slot = L / kXcds;
+    return xcd * per + min(xcd, rem) + slot;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Exact brute-force 1-NN of Q register-resident queries per lane over targets [j0, j1) of a
 // wave-uniform target array; increasing index order and strict '<' => lowest index wins ties.
@@ -203,7 +214,7 @@ constexpr int kInitWG = 256;
 __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     __shared__ float Tg[16];
     __shared__ int ident, invalid;
-    const int p = blockIdx.x;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
     const int tid = threadIdx.x;
     const int n = a.src_n[p], m = a.tgt_n[p];
     const float4* src = a.src + a.src_off[p];
@@ -337,8 +348,9 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     __shared__ float red[kIdxWaves][6];
     __shared__ uint32_t wsum[kIdxWaves];
     __shared__ float lo_s[3], sc_s[3];
-    const int p = blockIdx.x;
-    const bool is_tgt = blockIdx.y == 0;
+    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * 2);
+    const int p = g >> 1;
+    const bool is_tgt = (g & 1) == 0;
     if (w.state[p].phase == kPhaseInvalid) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
@@ -520,12 +532,13 @@ __device__ __forceinline__ void sweep_block(cv4f_ptr blk, const float (&x)[Q], c
 
 template <int Q, int B>
 __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
-    const int p = blockIdx.y;
+    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int p = g / gridDim.x, qb = g - p * gridDim.x;
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int base = (blockIdx.x * (kNNWG / 64) + wave) * (64 * Q);
+    const int base = (qb * (kNNWG / 64) + wave) * (64 * Q);
     if (base >= n) return;
     const float4* X = w.X + (int64_t)p * w.x_stride;
     const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
@@ -604,6 +617,179 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
 #pragma unroll
     for (int q = 0; q < Q; ++q)
         if (orig[q] >= 0) key[orig[q]] = best[q];
+}
+
+// ---------------------------------------------------------------------------------------------
+// nn_lds_kernel: the batched exact 1-NN (many pairs, targets <= kLdsTargets).  One workgroup per
+// pair keeps the pair's whole Morton-sorted target set in LDS (128 KB; the block / superblock
+// boxes are wave-uniform and stream through the scalar cache).  Each wave owns 64*Q Morton-contiguous queries and, instead of sweeping every
+// block that ANY of its queries might need (nn_pruned_kernel), tests blocks per query and appends
+// the (query, block) pairs that pass to a per-wave ring of work items; every 64 items are
+// evaluated one per lane (16 targets from LDS each) and merged with an LDS atomicMin on the
+// (d², index) key.  The evaluations drop from the wave's union of needed blocks to each query's
+// own needs; the answer is the same exact minimum (PCL semantics, lowest index among ties).
+constexpr int kLdsTargets = 8192;
+constexpr int kLdsLeaf = 16;
+constexpr int kLdsWG = 1024;
+constexpr int kLdsWaves = kLdsWG / 64;
+constexpr int kLdsQ = 2;
+constexpr int kRing = 128;  // work items per wave (<= 63 pending + 64 appended per query slot)
+
+struct LdsNN {
+    v4f tl[kLdsTargets];
+    unsigned long long best[kLdsWaves][64 * kLdsQ];
+    uint32_t items[kLdsWaves][kRing];
+};
+
+__global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+    constexpr int Q = kLdsQ;
+    __shared__ LdsNN sh;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    const int phase = uload(&w.state[p].phase);
+    if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
+    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    if (n <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
+    {  // stage the pair's sorted targets into LDS
+        const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
+        const int nt = nsb * kSuper * kLdsLeaf;
+        for (int i = tid; i < nt; i += kLdsWG) sh.tl[i] = tsg[i];
+    }
+    __syncthreads();
+    const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
+    const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
+    const float4* X = w.X + (int64_t)p * w.x_stride;
+    const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const float4* tgt = a.tgt + uload(a.tgt_off + p);
+    unsigned long long* bestl = sh.best[wave];
+    uint32_t* ring = sh.items[wave];
+    unsigned long long evals = 0;
+
+    for (int base = wave * 64 * Q; base < n; base += kLdsWaves * 64 * Q) {
+        float x[Q], y[Q], z[Q];
+        NNKey best[Q];
+        int orig[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int s0 = base + lane + q * 64;
+            const int s = min(s0, n - 1);
+            const int o = sperm[s];
+            orig[q] = s0 < n ? o : -1;
+            const float4 v = X[o];
+            x[q] = v.x;
+            y[q] = v.y;
+            z[q] = v.z;
+            const uint32_t j = first ? __float_as_uint(sh.tl[((int64_t)s * m) / n].w) : (uint32_t)key_idx(key[o]);
+            const float4 t = tgt[j];
+            best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
+            bestl[q * 64 + lane] = best[q];
+        }
+        float qlo[3], qhi[3], qmax = 0.0f;
+        qlo[0] = qhi[0] = x[0];
+        qlo[1] = qhi[1] = y[0];
+        qlo[2] = qhi[2] = z[0];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            qlo[0] = fminf(qlo[0], x[q]); qhi[0] = fmaxf(qhi[0], x[q]);
+            qlo[1] = fminf(qlo[1], y[q]); qhi[1] = fmaxf(qhi[1], y[q]);
+            qlo[2] = fminf(qlo[2], z[q]); qhi[2] = fmaxf(qhi[2], z[q]);
+            qmax = fmaxf(qmax, key_d2(best[q]));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
+                qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
+            }
+            qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
+            qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
+        }
+        qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
+
+        // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
+        uint32_t head = 0, tail = 0;
+        auto drain = [&](uint32_t cnt) {
+            const bool act = (uint32_t)lane < cnt;
+            const uint32_t it = ring[(head + lane) & (kRing - 1)];
+            const int qi = act ? (int)(it >> 16) : 0;
+            const int b = act ? (int)(it & 0xffffu) : 0;
+            const int owner = qi & 63, slot = qi >> 6;
+            float qx = 0.f, qy = 0.f, qz = 0.f;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {  // the query's coordinates from its owner lane
+                const float vx = __shfl(x[q], owner, 64), vy = __shfl(y[q], owner, 64), vz = __shfl(z[q], owner, 64);
+                if (slot == q) {
+                    qx = vx;
+                    qy = vy;
+                    qz = vz;
+                }
+            }
+            if (act) {
+                NNKey lb = ~0ull;
+                const v4f* tb = sh.tl + b * kLdsLeaf;
+#pragma unroll
+                for (int t = 0; t < kLdsLeaf; ++t) {
+                    const v4f c = tb[t];
+                    const NNKey kn = make_key(l2_simple(qx, qy, qz, c.x, c.y, c.z), __float_as_uint(c.w));
+                    lb = kn < lb ? kn : lb;
+                }
+                atomicMin(&bestl[qi], lb);
+            }
+            head += cnt;
+            evals += (unsigned long long)cnt * kLdsLeaf;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) best[q] = bestl[q * 64 + lane];  // tighter bounds for the tests
+        };
+        // Queue the lanes whose query `q` may reach block b.
+        auto push = [&](int b, const v4f lo, const v4f hi) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
+                const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
+                const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
+                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                const bool need = lbd * kLbShrink <= key_d2(best[q]);
+                const uint64_t mask = __ballot(need);
+                if (mask == 0) continue;
+                if (need) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                    ring[(tail + rank) & (kRing - 1)] = ((uint32_t)(q * 64 + lane) << 16) | (uint32_t)b;
+                }
+                tail += (uint32_t)__builtin_popcountll(mask);
+                if (tail - head >= 64) drain(64);
+            }
+        };
+        const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
+        const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (kLdsLeaf * kSuper);
+        int up = sb0, dn = sb0 - 1;
+        for (int k = 0; k < nsb; ++k) {
+            const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
+            const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+            if (!box_maybe(slo, shi, qlo, qhi, qmax) || !box_needed<Q>(slo, shi, x, y, z, best)) continue;
+            for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {
+                const v4f blo = tbx[2 * b], bhi = tbx[2 * b + 1];
+                if (!box_maybe(blo, bhi, qlo, qhi, qmax)) continue;
+                push(b, blo, bhi);
+            }
+        }
+        if (tail != head) drain(tail - head);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (orig[q] < 0) continue;
+            key[orig[q]] = best[q];
+            if (w.corr != nullptr && !fitness_pass) write_corr(w, a, p, orig[q], x[q], y[q], z[q], best[q], tgt);
+        }
+    }
+    if (lane == 0) atomicAdd(w.evals, evals);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -791,7 +977,7 @@ struct FoldShared {
 
 __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkArgs w) {
     __shared__ FoldShared sh;
-    const int p = blockIdx.x;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
     PairState& st = w.state[p];
     if (st.phase != kPhaseActive) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -944,7 +1130,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
     constexpr int I_CNT = MomLayout<kNumericsF64>::CNT;
     __shared__ SolveShared sh;
     __shared__ double red[kUpdWaves * NM];
-    const int p = blockIdx.x;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
     PairState& st = w.state[p];
     if (st.phase != kPhaseActive) return;
     const int tid = threadIdx.x;
@@ -986,7 +1172,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
 // ---------------------------------------------------------------------------------------------
 // fitness_prep_kernel: X := final * input (Registration::getFitnessScore / align's output).
 __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs w) {
-    const int p = blockIdx.x;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
     const PairState& st = w.state[p];
     if (st.phase == kPhaseInvalid) return;
     __shared__ float Tf[16];
@@ -1006,7 +1192,7 @@ __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs 
 // finish_kernel: fitness = mean of d² over d² <= max_range (double), results, aligned output.
 constexpr int kFinWG = 256;
 __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) {
-    const int p = blockIdx.x;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
     const PairState& st = w.state[p];
     const int n = a.src_n[p];
     const int64_t slot0 = (int64_t)p * w.x_stride;
@@ -1120,6 +1306,13 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     hipLaunchKernelGGL(index_kernel, dim3(npairs, 2), dim3(kIdxWG), 0, st, a, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int first,
+                         hipStream_t st) {
+    if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nn_lds_kernel, dim3(npairs), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     return hipGetLastError();
 }
 

@@ -178,6 +178,9 @@ typedef struct icp4r_plan_info {
     int32_t q;          /* queries per lane                                          */
     int32_t splits;     /* brute force: target splits per pair                       */
     int32_t leaf;       /* pruned: targets per block                                 */
+    int32_t lds;        /* pruned batch kernel with the target set in LDS (per-query
+                           work lists); used for >= 256 pairs with <= 8192 targets    */
+    int32_t reserved;
     int64_t nn_blocks;  /* workgroups of one NN launch                               */
 } icp4r_plan_info;
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);

@@ -68,10 +68,12 @@ def test_struct_layouts():
 def test_plan_geometry():
     import icp4r
 
-    big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, 2 queries per lane, 16-target blocks
-    assert big["pruned"] and big["q"] == 2 and big["leaf"] == 16 and big["splits"] == 1
-    single = icp4r.plan(1, 8192, 8192)  # C2: one query per lane to fill more waves
-    assert single["pruned"] and single["q"] == 1 and single["nn_blocks"] == 32
+    big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
+    assert big["pruned"] and big["lds"] and big["q"] == 2 and big["leaf"] == 16 and big["nn_blocks"] == 1024
+    assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
+    assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
+    single = icp4r.plan(1, 8192, 8192)  # C2: streamed kernel, one query per lane to fill more waves
+    assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32
     brute = icp4r.plan(1024, 8192, 8192, icp4r.NN_BRUTE)
     assert not brute["pruned"] and brute["q"] == 4 and brute["splits"] == 1
     bsingle = icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)

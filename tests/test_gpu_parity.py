@@ -176,12 +176,15 @@ def test_target_split_equals_unsplit(gpu_ctx):
         assert (res[k]["T"] == np.array(r.T, np.float32)).all()
 
 
+@pytest.mark.parametrize("lds", ["0", "1"])
 @pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map"])
-def test_nn_modes_identical(gpu_ctx, case):
-    """Pruned, brute-force and packed searches produce bit-identical registrations (T, fitness,
-    iterations, aligned cloud) — the pruned index changes only which targets are evaluated."""
+def test_nn_modes_identical(gpu_ctx, case, lds, monkeypatch):
+    """Pruned (streamed, or with the target set in LDS and per-query work lists), brute-force and
+    packed searches produce bit-identical registrations (T, fitness, iterations, aligned cloud) —
+    the pruned index changes only which targets are evaluated."""
     import icp4r
 
+    monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
     guess = None
     if case == "c2":
         pairs = [_pair(310, 8192)]
