@@ -659,6 +659,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     }
     __syncthreads();
     const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
+    const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
     const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
     const float4* X = w.X + (int64_t)p * w.x_stride;
     const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
@@ -749,9 +750,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) best[q] = bestl[q * 64 + lane];  // tighter bounds for the tests
         };
         // Queue the lanes whose query `q` may reach block b.
-        auto push = [&](int b, const v4f lo, const v4f hi) {
+        auto push = [&](int b, const v4f lo, const v4f hi, uint32_t qslots) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
+                if (!((qslots >> q) & 1)) continue;
                 const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
                 const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
                 const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
@@ -768,17 +770,37 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 if (tail - head >= 64) drain(64);
             }
         };
+        // coarse test of every superblock at once (lane = superblock; nsb <= 64 here)
+        uint64_t cmask;
+        {
+            const int sbl = min(lane, nsb - 1);
+            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+            cmask = __ballot(lane < nsb && box_maybe(sbv[2 * sbl], sbv[2 * sbl + 1], qlo, qhi, qmax));
+        }
         const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
         const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (kLdsLeaf * kSuper);
         int up = sb0, dn = sb0 - 1;
         for (int k = 0; k < nsb; ++k) {
             const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
+            if (!((cmask >> sb) & 1)) continue;
             const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
-            if (!box_maybe(slo, shi, qlo, qhi, qmax) || !box_needed<Q>(slo, shi, x, y, z, best)) continue;
-            for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {
-                const v4f blo = tbx[2 * b], bhi = tbx[2 * b + 1];
-                if (!box_maybe(blo, bhi, qlo, qhi, qmax)) continue;
-                push(b, blo, bhi);
+            uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const float gx = fmaxf(fmaxf(slo.x - x[q], x[q] - shi.x), 0.0f);
+                const float gy = fmaxf(fmaxf(slo.y - y[q], y[q] - shi.y), 0.0f);
+                const float gz = fmaxf(fmaxf(slo.z - z[q], z[q] - shi.z), 0.0f);
+                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                if (__ballot(lbd * kLbShrink <= key_d2(best[q])) != 0) qslots |= 1u << q;
+            }
+            if (qslots == 0) continue;
+            // coarse test of the superblock's blocks at once (lanes 0..7)
+            const int bl = sb * kSuper + (lane & (kSuper - 1));
+            uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
+            while (bmask) {
+                const int b = sb * kSuper + __builtin_ctz(bmask);
+                bmask &= bmask - 1;
+                push(b, tbx[2 * b], tbx[2 * b + 1], qslots);
             }
         }
         if (tail != head) drain(tail - head);
