@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 FLOP_PER_PAIR_EVAL = 8     # 3 sub + 3 mul + 2 add (FLANN L2_Simple); compare/select not counted
+FLOP_PER_BOX_TEST = 11     # 6 sub + 3 mul + 2 add (point-to-box lower bound); max/compare not counted
 
 
 def parse():
@@ -144,8 +145,9 @@ def main():
         elapsed = float(t.item())
     nn_ms, nn_launches = ctx.kernel_time_ms()
     batch_ms, _ = ctx.batch_time_ms()
-    evals = ctx.nn_evaluations()  # distance evaluations the NN kernels performed in the timed steps
+    evals, tests = ctx.nn_counters()  # work the NN kernels performed in the timed steps
     plan = icp4r.plan(P, n, n)
+    kernel = "nn_lds_kernel" if plan["lds"] else "nn_pruned_kernel" if plan["pruned"] else "nn_kernel"
 
     # result check (outside the timed region): statuses, iteration counts, and pairs vs the oracle
     res = np.frombuffer(results.cpu().numpy().tobytes(), dtype=icp4r.RESULT_DTYPE)
@@ -174,15 +176,17 @@ def main():
     total_pairs = world * P * args.steps
     value = total_pairs / elapsed
     evals_per_launch = evals / max(nn_launches, 1)
-    flops_per_launch = evals_per_launch * FLOP_PER_PAIR_EVAL
+    tests_per_launch = tests / max(nn_launches, 1)
+    flops_per_launch = evals_per_launch * FLOP_PER_PAIR_EVAL + tests_per_launch * FLOP_PER_BOX_TEST
     achieved_tflops = flops_per_launch / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    traffic = None
+    brute_equiv_tflops = P * n * n * FLOP_PER_PAIR_EVAL / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
+    traffic = None  # HBM bytes per launch from the committed PMC passes of THIS kernel and shape
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("pairs") == P and pmc.get("points") == n:
+            if pmc.get("pairs") == P and pmc.get("points") == n and pmc.get("kernel") == kernel:
                 traffic = pmc.get("hbm_bytes_per_nn_launch")
         except (OSError, ValueError):
             traffic = None
@@ -222,16 +226,20 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tflops / PEAK_FP32_TFLOPS,
                 "traffic": traffic,
-                "kernel": "nn_pruned_kernel (exact 1-NN)" if plan["pruned"] else "nn_kernel (exact 1-NN sweep)",
+                "kernel": kernel,
                 "flop_per_launch": flops_per_launch,
                 "evaluations_per_launch": evals_per_launch,
+                "box_tests_per_launch": tests_per_launch,
                 "evaluated_fraction_of_brute_force": evals_per_launch / (P * n * n),
+                "brute_force_equivalent_tflops": brute_equiv_tflops,
                 "avg_launch_ms": nn_ms,
                 "launches": nn_launches,
-                "note": "compute-bound on FP32 VALU: achieved = distance evaluations actually performed (device "
-                        "counter) x 8 FLOP (3 sub, 3 mul, 2 add; compare/select and box tests not counted) / "
-                        "avg launch time from HIP events on the launch stream; peak = dense FP32 "
-                        "(== f32 MFMA dense peak)",
+                "note": "FP32 VALU work of the exact pruned search, counted on the device: distance evaluations "
+                        "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add); "
+                        "compare/select/ballot/LDS not counted. achieved = that / avg launch time (HIP events on "
+                        "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). The search evaluates "
+                        "~1% of the n*m pairs, so brute_force_equivalent_tflops (n*m*8 / time) exceeds the peak; "
+                        "the kernel is issue/latency-bound (VALU + LDS at 4 waves/SIMD), see DESIGN.md",
             },
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -229,8 +229,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     w.x_stride = x_stride;
     w.splits = pl.splits;
     if (!ctx->evals.p) {
-        HIP_TRY(ctx->evals.ensure(sizeof(uint64_t)));
-        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, sizeof(uint64_t), st));
+        HIP_TRY(ctx->evals.ensure(2 * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, 2 * sizeof(uint64_t), st));
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
@@ -668,7 +668,7 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     if (ctx->evals.p) {
         HIP_TRY(hipSetDevice(ctx->device));
         HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemset(ctx->evals.p, 0, sizeof(uint64_t)));
+        HIP_TRY(hipMemset(ctx->evals.p, 0, 2 * sizeof(uint64_t)));
     }
     return ICP4R_OK;
 }
@@ -687,13 +687,14 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
     return ICP4R_OK;
 }
 
-int icp4r_nn_evaluations(icp4r_ctx* ctx, uint64_t* evaluations) {
+int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests) {
     if (!ctx || !evaluations) return fail(ICP4R_E_INVALID, "NULL argument");
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
-    uint64_t v = 0;
-    if (ctx->evals.p) HIP_TRY(hipMemcpy(&v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
-    *evaluations = v;
+    uint64_t v[2] = {0, 0};
+    if (ctx->evals.p) HIP_TRY(hipMemcpy(v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
+    *evaluations = v[0];
+    if (box_tests) *box_tests = v[1];
     return ICP4R_OK;
 }
 

@@ -427,8 +427,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             ts[pos] = make_float4(v.x, v.y, v.z, __uint_as_float((uint32_t)i));
             tinv[i] = (int32_t)pos;
         }
-        __threadfence();
-        __syncthreads();
+        __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
         // 5. tail duplicates, block boxes, superblock boxes
         const float4 last = ts[n - 1];
         for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = last;
@@ -448,8 +447,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             tb[2 * b] = l;
             tb[2 * b + 1] = h;
         }
-        __threadfence();
-        __syncthreads();
+        __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
         float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
         for (int s = tid; s < w.sb_stride; s += kIdxWG) {
             float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
@@ -596,19 +594,28 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
     const cv4f_ptr tb = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
     const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
     int up = sb0, dn = sb0 - 1, swept = 0;
+    unsigned long long tests = 0;  // box tests (lane-level: one query against one box)
     for (int k = 0; k < nsb; ++k) {
         const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
         const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
-        if (!box_maybe(slo, shi, qlo, qhi, qmax) || !box_needed<Q>(slo, shi, x, y, z, best)) continue;
+        ++tests;
+        if (!box_maybe(slo, shi, qlo, qhi, qmax)) continue;
+        tests += 64 * Q;
+        if (!box_needed<Q>(slo, shi, x, y, z, best)) continue;
         for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {  // blocks past nb have empty boxes
             const v4f blo = tb[2 * b], bhi = tb[2 * b + 1];
-            if (!box_maybe(blo, bhi, qlo, qhi, qmax) || !box_needed<Q>(blo, bhi, x, y, z, best)) continue;
+            ++tests;
+            if (!box_maybe(blo, bhi, qlo, qhi, qmax)) continue;
+            tests += 64 * Q;
+            if (!box_needed<Q>(blo, bhi, x, y, z, best)) continue;
             sweep_block<Q, B>(ts + (int64_t)b * B, x, y, z, best);
             ++swept;
         }
     }
-    if (lane == 0)
+    if (lane == 0) {
         atomicAdd(w.evals, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
+        atomicAdd(w.evals + 1, tests);
+    }
     if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence arrays
 #pragma unroll
         for (int q = 0; q < Q; ++q)
@@ -667,7 +674,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     const float4* tgt = a.tgt + uload(a.tgt_off + p);
     unsigned long long* bestl = sh.best[wave];
     uint32_t* ring = sh.items[wave];
-    unsigned long long evals = 0;
+    unsigned long long evals = 0, tests = 0;
 
     for (int base = wave * 64 * Q; base < n; base += kLdsWaves * 64 * Q) {
         float x[Q], y[Q], z[Q];
@@ -754,6 +761,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (!((qslots >> q) & 1)) continue;
+                tests += 64;
                 const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
                 const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
                 const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
@@ -776,6 +784,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             const int sbl = min(lane, nsb - 1);
             const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
             cmask = __ballot(lane < nsb && box_maybe(sbv[2 * sbl], sbv[2 * sbl + 1], qlo, qhi, qmax));
+            tests += nsb;
         }
         const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
         const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (kLdsLeaf * kSuper);
@@ -784,6 +793,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
             if (!((cmask >> sb) & 1)) continue;
             const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+            tests += 64 * Q + kSuper;
             uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
@@ -811,7 +821,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             if (w.corr != nullptr && !fitness_pass) write_corr(w, a, p, orig[q], x[q], y[q], z[q], best[q], tgt);
         }
     }
-    if (lane == 0) atomicAdd(w.evals, evals);
+    if (lane == 0) {
+        atomicAdd(w.evals, evals);
+        atomicAdd(w.evals + 1, tests);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
-    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_evaluations",
+    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters",
 ]
 
 
@@ -144,7 +144,7 @@ def load():
         "icp4r_batch_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_kernel_time_reset": (C.c_int, [vp]),
         "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
-        "icp4r_nn_evaluations": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -276,11 +276,15 @@ class Context:
     def reset_timers(self):
         _check(self._lib.icp4r_kernel_time_reset(self._h), "icp4r_kernel_time_reset")
 
+    def nn_counters(self) -> tuple[int, int]:
+        """(distance evaluations, box tests) of the NN kernels since the last reset_timers()."""
+        v, t = C.c_uint64(), C.c_uint64()
+        _check(self._lib.icp4r_nn_counters(self._h, C.byref(v), C.byref(t)), "icp4r_nn_counters")
+        return v.value, t.value
+
     def nn_evaluations(self) -> int:
         """Distance evaluations (query x target) of the NN kernels since the last reset_timers()."""
-        v = C.c_uint64()
-        _check(self._lib.icp4r_nn_evaluations(self._h, C.byref(v)), "icp4r_nn_evaluations")
-        return v.value
+        return self.nn_counters()[0]
 
 
 def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO) -> dict:

@@ -166,11 +166,11 @@ int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
 int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);
 int icp4r_kernel_time_reset(icp4r_ctx* ctx);
 
-/* Distance evaluations (query x target) the NN kernels performed since the last
- * icp4r_kernel_time_reset — the algorithmic work behind the roofline's `achieved` (the pruned
- * search evaluates a small fraction of n*m; brute force exactly n*m per pair and pass).
- * Synchronises the context's device. */
-int icp4r_nn_evaluations(icp4r_ctx* ctx, uint64_t* evaluations);
+/* Work the NN kernels performed since the last icp4r_kernel_time_reset — the algorithmic work
+ * behind the roofline's `achieved`: distance evaluations (query x target; brute force exactly n*m
+ * per pair and pass, the pruned search a small fraction) and bounding-box tests (query x box, the
+ * pruned search only; may be NULL).  Synchronises the context's device. */
+int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests);
 
 /* Launch geometry the batch path picks for a shape — exposed for tests and the benchmark report. */
 typedef struct icp4r_plan_info {

@@ -231,12 +231,12 @@ def test_pruned_evaluates_fewer_pairs(gpu_ctx):
     p = dict(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, compute_fitness=0)
     gpu_ctx.reset_timers()
     gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_BRUTE, **p))
-    brute = gpu_ctx.nn_evaluations()
-    assert brute == 5 * len(s) * len(t)
+    brute, brute_tests = gpu_ctx.nn_counters()
+    assert brute == 5 * len(s) * len(t) and brute_tests == 0
     gpu_ctx.reset_timers()
     gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_PRUNED, **p))
-    pruned = gpu_ctx.nn_evaluations()
-    assert 0 < pruned < 0.3 * brute
+    pruned, tests = gpu_ctx.nn_counters()
+    assert 0 < pruned < 0.3 * brute and tests > 0
 
 
 def test_repeatable_and_target_permutation_invariant(gpu_ctx):

@@ -38,7 +38,7 @@ def run(name, src, tgt, params, oparams, reps=5):
         walls.append(time.perf_counter() - t0)
     dev_ms, k = ctx.batch_time_ms()
     nn_ms, nk = ctx.kernel_time_ms()
-    evals = ctx.nn_evaluations() / max(nk, 1)
+    evals = ctx.nn_counters()[0] / max(nk, 1)
     t0 = time.perf_counter()
     o = oracle.align(src, tgt, **oparams)
     cpu_s = time.perf_counter() - t0

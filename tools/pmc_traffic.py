@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=1024)
     ap.add_argument("--points", type=int, default=8192)
     ap.add_argument("--tag", default="r01")
-    ap.add_argument("--kernel", default="nn_kernel")
+    ap.add_argument("--kernel", default="nn_lds_kernel", help="kernel name (substring match in the PMC CSV)")
     a = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     out = {"pairs": a.pairs, "points": a.points, "kernel": a.kernel, "tag": a.tag}
@@ -75,7 +75,9 @@ def main():
     if "fetch_bytes_corrected" in out and "write_bytes" in out:
         out["hbm_bytes_per_nn_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
         n, P = a.points, a.pairs
-        out["algorithmic_bytes_per_nn_launch"] = P * (n * 16 + n * 16 + n * 8)  # X read, target read, (d2, idx) write
+        # per query: X 16 B + permutation 4 B + previous key 8 B + key write 8 B + matched target 16 B +
+        # correspondence record write 32 B; per pair: the sorted target set 16 B/pt + boxes (staged once)
+        out["algorithmic_bytes_per_nn_launch"] = P * (n * (16 + 4 + 8 + 8 + 16 + 32) + n * 16 + (n // 16) * 36)
     if a.fetch or a.write:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)

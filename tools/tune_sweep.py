@@ -60,7 +60,7 @@ def main():
             torch.cuda.synchronize()
             nn_ms, k = ctx.kernel_time_ms()
             b_ms, _ = ctx.batch_time_ms()
-            ev = ctx.nn_evaluations() / max(k, 1)
+            ev = ctx.nn_counters()[0] / max(k, 1)
             if ref is None:
                 ref = res.clone()
             tf = ev * 8 / (nn_ms * 1e-3) / 1e12
