@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--pairs", type=int, default=1024)
     ap.add_argument("--points", type=int, default=8192)
-    ap.add_argument("--tag", default="r01")
+    ap.add_argument("--tag", default="round1", help="profiles/<tag>/ receives the kernel stats")
     ap.add_argument("--kernel", default="nn_lds_kernel", help="kernel name (substring match in the PMC CSV)")
     a = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
@@ -51,7 +51,8 @@ def main():
     if a.stats:
         st = find(a.stats, "*kernel_stats.csv")
         if st:
-            dst = os.path.join(ROOT, "profiles", f"kernel_stats_{a.tag}.csv")
+            dst = os.path.join(ROOT, "profiles", a.tag, "kernel_stats.csv")
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
             shutil.copy(st[0], dst)
             with open(st[0]) as f:
                 for row in csv.DictReader(f):
