@@ -17,14 +17,14 @@
 #include <vector>
 
 #include "icp4r/icp4r.h"
+#include "icp4r_host.hpp"
 #include "icp4r_internal.hpp"
 
 using namespace icp4r;
 
-namespace {
+namespace icp4r_host {
 
 thread_local std::string g_last_error;
-
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -36,53 +36,32 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                                 \
-    do {                                                                                              \
-        hipError_t _e = (expr);                                                                       \
-        if (_e != hipSuccess) return fail(ICP4R_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
-                                          __FILE__, __LINE__);                                        \
-    } while (0)
+int check_cloud(const float* c, int64_t n, int32_t stride, const char* what) {
+    if (n < 0) return fail(ICP4R_E_INVALID, "%s: negative point count", what);
+    if (n > 0 && !c) return fail(ICP4R_E_INVALID, "%s: NULL cloud with %lld points", what, (long long)n);
+    if (stride < 12 || stride % 4) return fail(ICP4R_E_INVALID, "%s: stride %d bytes (need >= 12, multiple of 4)", what, stride);
+    return ICP4R_OK;
+}
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) {
-            hipError_t e = hipFree(p);
-            if (e != hipSuccess) return e;
-            p = nullptr;
-            cap = 0;
-        }
-        size_t want = bytes < 256 ? 256 : bytes;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
-        return e;
+void pack_host(const float* c, int64_t n, int32_t stride_bytes, std::vector<float>& out) {
+    out.resize((size_t)(n > 0 ? n : 1) * 4);
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c);
+    for (int64_t i = 0; i < n; ++i) {
+        const float* p = reinterpret_cast<const float*>(b + (size_t)i * stride_bytes);
+        out[4 * (size_t)i + 0] = p[0];
+        out[4 * (size_t)i + 1] = p[1];
+        out[4 * (size_t)i + 2] = p[2];
+        out[4 * (size_t)i + 3] = stride_bytes >= 16 ? p[3] : 0.0f;
     }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
+}
 
-}  // namespace
+}  // namespace icp4r_host
 
-struct EventPair {
-    hipEvent_t start = nullptr, stop = nullptr;
-};
-
-struct icp4r_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    // staging for the host-buffer entry points
-    DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
-    // batch workspace
-    DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks;
-    std::vector<EventPair> nn_events, batch_events;
-    size_t nn_used = 0, batch_used = 0;
-    DevBuf evals;  // u64: distance evaluations of the NN kernels since the last reset
-};
+using icp4r_host::DevBuf;
+using icp4r_host::EventPair;
+using icp4r_host::check_cloud;
+using icp4r_host::fail;
+using icp4r_host::pack_host;
 
 namespace {
 
@@ -182,25 +161,6 @@ int make_kparams(const icp4r_params* p, KParams* kp) {
     kp->fit_max_range = p->fitness_max_range;
     kp->need_mse = (p->mse_threshold_absolute > 0 || p->euclidean_fitness_epsilon > 0) ? 1 : 0;
     return ICP4R_OK;
-}
-
-int check_cloud(const float* c, int32_t n, int32_t stride, const char* what) {
-    if (n < 0) return fail(ICP4R_E_INVALID, "%s: negative point count", what);
-    if (n > 0 && !c) return fail(ICP4R_E_INVALID, "%s: NULL cloud with %d points", what, n);
-    if (stride < 12 || stride % 4) return fail(ICP4R_E_INVALID, "%s: stride %d bytes (need >= 12, multiple of 4)", what, stride);
-    return ICP4R_OK;
-}
-
-void pack_host(const float* c, int32_t n, int32_t stride_bytes, std::vector<float>& out) {
-    out.resize((size_t)(n > 0 ? n : 1) * 4);
-    const unsigned char* b = reinterpret_cast<const unsigned char*>(c);
-    for (int32_t i = 0; i < n; ++i) {
-        const float* p = reinterpret_cast<const float*>(b + (size_t)i * stride_bytes);
-        out[4 * (size_t)i + 0] = p[0];
-        out[4 * (size_t)i + 1] = p[1];
-        out[4 * (size_t)i + 2] = p[2];
-        out[4 * (size_t)i + 3] = stride_bytes >= 16 ? p[3] : 0.0f;
-    }
 }
 
 int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
@@ -378,7 +338,7 @@ extern "C" {
 
 const char* icp4r_version(void) { return "icp4r 0.2.0 (gfx950, HIP)"; }
 int icp4r_abi_version(void) { return ICP4R_ABI_VERSION; }
-const char* icp4r_last_error(void) { return g_last_error.c_str(); }
+const char* icp4r_last_error(void) { return icp4r_host::g_last_error.c_str(); }
 
 void icp4r_params_default(icp4r_params* p) {
     if (!p) return;

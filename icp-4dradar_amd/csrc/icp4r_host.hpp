@@ -1,0 +1,71 @@
+// icp4r_host.hpp — host-side pieces shared by the C-ABI translation units (icp4r_capi.cpp,
+// icp4r_map.cpp): error reporting, device buffers and the context.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "icp4r/icp4r.h"
+
+namespace icp4r_host {
+
+// Records a printf-style message for icp4r_last_error() (thread-local) and returns `code`.
+int fail(int code, const char* fmt, ...);
+
+#define HIP_TRY(expr)                                                                                 \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            return ::icp4r_host::fail(ICP4R_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e),    \
+                                      __FILE__, __LINE__);                                            \
+    } while (0)
+
+// Grow-only device allocation.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct EventPair {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
+// Validates a host cloud argument (count, pointer, stride).
+int check_cloud(const float* c, int64_t n, int32_t stride, const char* what);
+
+// Repacks n host points of `stride_bytes` into float4 (x, y, z, 4th float or 0).
+void pack_host(const float* c, int64_t n, int32_t stride_bytes, std::vector<float>& out);
+
+}  // namespace icp4r_host
+
+struct icp4r_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // staging for the host-buffer entry points
+    icp4r_host::DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
+    // batch workspace
+    icp4r_host::DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks;
+    std::vector<icp4r_host::EventPair> nn_events, batch_events;
+    size_t nn_used = 0, batch_used = 0;
+    icp4r_host::DevBuf evals;  // u64[2]: NN distance evaluations and box tests since the last reset
+};

@@ -124,4 +124,19 @@ hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs,
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);
 
+// ---- scan-to-map store (icp4r_map.hip)
+struct SectorArgs {
+    float cx, cy, cz;  // query point (the vehicle position p_now)
+    float radius;      // RADAR_RADIUS
+    float heading;     // degrees (float, as Sector_Search receives it)
+};
+struct Mat3x4d {
+    double R[9];  // row-major
+    double t[3];
+};
+hipError_t launch_associate(const float4* in, int64_t n, const Mat3x4d& M, float4* out, hipStream_t st);
+int64_t sector_blocks(int64_t n);
+hipError_t launch_sector(const float4* map, int64_t n, const SectorArgs& a, int32_t* counts, int32_t* offsets,
+                         int32_t* total, float4* out, hipStream_t st);
+
 }  // namespace icp4r

@@ -45,6 +45,12 @@ EXPORTED_SYMBOLS = [
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
     "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters",
 ]
+# include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
+MAP_EXPORTED_SYMBOLS = [
+    "icp4r_map_create", "icp4r_map_destroy", "icp4r_map_build", "icp4r_map_add_points", "icp4r_map_add_scan",
+    "icp4r_map_size", "icp4r_map_sector_search", "icp4r_map_sector_search_device", "icp4r_map_points_device",
+    "icp4r_map_time_ms", "icp4r_map_time_reset",
+]
 
 
 def status_name(code: int) -> str:
@@ -145,6 +151,18 @@ def load():
         "icp4r_kernel_time_reset": (C.c_int, [vp]),
         "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
         "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        # icp4r_map.h
+        "icp4r_map_create": (C.c_int, [vp, C.POINTER(vp)]),
+        "icp4r_map_destroy": (C.c_int, [vp]),
+        "icp4r_map_build": (C.c_int, [vp, vp, i64, i32]),
+        "icp4r_map_add_points": (C.c_int, [vp, vp, i64, i32, i32]),
+        "icp4r_map_add_scan": (C.c_int, [vp, vp, i64, i32, vp, vp, vp]),
+        "icp4r_map_size": (C.c_int, [vp, C.POINTER(i64)]),
+        "icp4r_map_sector_search": (C.c_int, [vp, vp, C.c_float, C.c_float, vp, i64, C.POINTER(i64)]),
+        "icp4r_map_sector_search_device": (C.c_int, [vp, vp, C.c_float, C.c_float, vp, vp, vp]),
+        "icp4r_map_points_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(i64)]),
+        "icp4r_map_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
+        "icp4r_map_time_reset": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

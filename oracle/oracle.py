@@ -89,6 +89,16 @@ def lib():
                                      C.c_void_p, C.c_double, C.c_int32]
         L.oracle_fitness.restype = C.c_double
         L.oracle_kdtree_leaf_visits.restype = C.c_int64
+        L.oracle_calc_dist.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_calc_dist.restype = C.c_float
+        L.oracle_calc_heading.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_calc_heading.restype = C.c_float
+        L.oracle_sector_keep.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_float]
+        L.oracle_sector_keep.restype = C.c_int
+        L.oracle_sector_search.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_float, C.c_float,
+                                           C.c_void_p]
+        L.oracle_sector_search.restype = C.c_int64
+        L.oracle_associate_to_map.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -170,3 +180,31 @@ def fitness(src: np.ndarray, tgt: np.ndarray, T: np.ndarray, max_range: float = 
     t, m, ts = _cloud(tgt)
     Tc = np.ascontiguousarray(np.asarray(T, np.float32).T.reshape(16))
     return lib().oracle_fitness(s.ctypes.data, n, ss, t.ctypes.data, m, ts, Tc.ctypes.data, max_range, nn)
+
+
+# ---------------------------------------------------------------------------------------------------
+# Scan-to-map submap path (map_oracle.c): ikd-Tree map store + Sector_Search as radar_odometry uses it.
+
+def calc_heading(a, b) -> float:
+    a = np.ascontiguousarray(a, np.float32)[:3].copy()
+    b = np.ascontiguousarray(b, np.float32)[:3].copy()
+    return float(lib().oracle_calc_heading(a.ctypes.data, b.ctypes.data))
+
+
+def sector_search(map_pts: np.ndarray, center, radius: float, heading: float) -> np.ndarray:
+    """KD_TREE::Sector_Search over an append-only map: indices of the kept points, insertion order."""
+    m, n, stride = _cloud(map_pts)
+    c = np.ascontiguousarray(center, np.float32)[:3].copy()
+    out = np.empty(max(n, 1), np.int64)
+    k = lib().oracle_sector_search(m.ctypes.data, n, stride, c.ctypes.data, radius, heading, out.ctypes.data)
+    return out[:k].copy()
+
+
+def associate_to_map(pts: np.ndarray, R: np.ndarray, t: np.ndarray) -> np.ndarray:
+    """pointAssociateToMap: (n, 4) float32 x, y, z, intensity -> world frame (double math, float out)."""
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 4)
+    Rd = np.ascontiguousarray(R, np.float64).reshape(9)
+    td = np.ascontiguousarray(t, np.float64).reshape(3)
+    out = np.empty_like(p)
+    lib().oracle_associate_to_map(p.ctypes.data, len(p), Rd.ctypes.data, td.ctypes.data, out.ctypes.data)
+    return out

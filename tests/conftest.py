@@ -38,9 +38,16 @@ def oracle_mod():
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
-    """A context on cuda:0.  Fails (never skips) when the HIP library or the GPU is missing."""
+    """A context on cuda:0.  Fails (never skips) when the HIP library or the GPU is missing.
+
+    torch's HIP runtime is brought up first (as bench.py does): tests that hand torch device tensors
+    to the library need torch's runtime to be the process's first HIP initialisation."""
+    import torch
+
     import icp4r
 
+    torch.zeros(1, device="cuda:0")
+    torch.cuda.synchronize()
     ctx = icp4r.Context(0)
     yield ctx
     ctx.close()

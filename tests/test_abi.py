@@ -11,11 +11,15 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r.h")
+MAP_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_map.h")
 
 
-def header_functions():
-    txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int|void)\s+(icp4r_\w+)\s*\(", txt, re.M)))
+def header_functions(path=None):
+    paths = [path] if path else [HEADER, MAP_HEADER]
+    names = set()
+    for p in paths:
+        names |= set(re.findall(r"^\s*(?:const\s+char\s*\*|int|void)\s+(icp4r_\w+)\s*\(", open(p).read(), re.M))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -23,10 +27,11 @@ def test_library_exports_every_declared_symbol():
 
     L = icp4r.load()
     decl = header_functions()
-    assert len(decl) >= 15
+    assert len(decl) >= 26
     for name in decl:
-        assert hasattr(L, name), f"{name} declared in icp4r.h but not exported"
-    assert sorted(icp4r.EXPORTED_SYMBOLS) == decl
+        assert hasattr(L, name), f"{name} declared in include/icp4r/*.h but not exported"
+    assert sorted(icp4r.EXPORTED_SYMBOLS) == header_functions(HEADER)
+    assert sorted(icp4r.MAP_EXPORTED_SYMBOLS) == header_functions(MAP_HEADER)
 
 
 def test_nm_shows_c_linkage():
