@@ -194,3 +194,40 @@ def test_scan_to_map_registration_device_resident(gpu_ctx, oracle_mod):
     assert (r_dev["T"] == np.array(r_host.T, np.float32)).all() and r_dev["iterations"] == r_host.iterations
     o = oracle_mod.align(scan, host_sub, numerics=oracle_mod.NUM_F32, max_iterations=15)
     assert (r_host.matrix() == o["T"]).all()
+
+
+@pytest.mark.gpu
+def test_ikd_facade_callsite(oracle_mod):
+    """tests/cpp/map_callsite.cpp: radar_odometry's map calls through include/icp4r/ikd_compat.hpp
+    (namespace-scope KD_TREE, Build, set_downsample_param, Add_Points(.., false), Sector_Search) give
+    the oracle's submap, intensities included."""
+    import os
+    import subprocess
+
+    from helpers import GOLDEN_DIR
+
+    from icp4r import synth
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "_build", "map_callsite")
+    a, b = (os.path.join(GOLDEN_DIR, f) for f in ("c2_pair1_8k_tgt.bin", "c2_pair1_8k_src.bin"))
+    x, y, yaw = 5.0, -3.0, 30.0
+    r = subprocess.run([exe, a, b, str(x), str(y), str(yaw)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    head = lines[0].split()
+    got = np.array([[float(v) for v in ln.split()] for ln in lines[1:]], np.float32).reshape(-1, 4)
+    first = synth.records_to_xyzi(synth.read_bin(a))
+    nxt = synth.records_to_xyzi(synth.read_bin(b))
+    c, s_ = math.cos(math.radians(yaw)), math.sin(math.radians(yaw))
+    R = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1]])
+    world = oracle_mod.associate_to_map(nxt, R, np.array([x, y, 0.0]))
+    allp = np.concatenate([first, world])
+    assert int(head[1]) == len(allp)
+    ref = oracle_mod.sector_search(allp, [x, y, 0.0], 80.0, yaw)
+    gs, rs = {tuple(p) for p in got.tolist()}, {tuple(allp[i]) for i in ref.tolist()}
+    for p in gs ^ rs:
+        i = int(np.nonzero((allp == np.array(p, np.float32)).all(1))[0][0])
+        assert _edge_ok(oracle_mod, allp, [x, y, 0.0], yaw, i), p
+    if gs == rs:
+        assert (got == allp[ref]).all()  # insertion order, intensity carried through
