@@ -71,6 +71,7 @@ struct Plan {
     int splits;   // brute force: target splits
     bool pruned;  // Morton-block pruned exact search
     bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
+    bool cache;   // lds: cached-neighbour test + second-nearest search (ICP4R_NN_CACHE=0 disables)
     int leaf;     // pruned: targets per block
     int64_t blocks;
 };
@@ -93,6 +94,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
     pl.lds = false;
+    pl.cache = false;
     pl.splits = 1;
     pl.leaf = 0;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
@@ -112,6 +114,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
         if (pl.lds) {
             pl.q = 2;
             pl.blocks = npairs;
+            pl.cache = max_n <= kCacheMaxN && env_int("ICP4R_NN_CACHE", 1) != 0;
         }
         return pl;
     }
@@ -177,7 +180,7 @@ int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
 // Size the workspace for a plan and fill WorkArgs.
 int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, bool corr, hipStream_t st,
                WorkArgs& w) {
-    const int64_t x_stride = ((max_n > 0 ? max_n : 1) + 3) & ~3;
+    const int64_t x_stride = (((max_n > 0 ? max_n : 1) + 3) & ~3) + env_int("ICP4R_XPAD", 0);
     const int64_t slots = (int64_t)npairs * x_stride;
     HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
     HIP_TRY(ctx->nn_key.ensure((size_t)slots * sizeof(NNKey)));
@@ -189,12 +192,16 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     w.x_stride = x_stride;
     w.splits = pl.splits;
     if (!ctx->evals.p) {
-        HIP_TRY(ctx->evals.ensure(2 * sizeof(uint64_t)));
-        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, 2 * sizeof(uint64_t), st));
+        HIP_TRY(ctx->evals.ensure(4 * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, 4 * sizeof(uint64_t), st));
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
-        HIP_TRY(ctx->ticks.ensure(8 * sizeof(uint64_t)));
+        const size_t nt = 16 + 4 * (size_t)npairs;
+        if (ctx->ticks.cap < nt * sizeof(uint64_t)) {
+            HIP_TRY(ctx->ticks.ensure(nt * sizeof(uint64_t)));
+            HIP_TRY(hipMemsetAsync(ctx->ticks.p, 0, nt * sizeof(uint64_t), st));
+        }
         w.ticks = static_cast<uint64_t*>(ctx->ticks.p);
     }
     if (corr) {
@@ -217,6 +224,29 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.tbox = static_cast<float4*>(ctx->tbox.p);
         w.sbox = static_cast<float4*>(ctx->sbox.p);
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
+        if (pl.lds) {
+            HIP_TRY(ctx->plist.ensure((size_t)npairs * sizeof(int32_t)));
+            HIP_TRY(ctx->plist_n.ensure(2 * sizeof(int32_t)));
+            w.plist = static_cast<int32_t*>(ctx->plist.p);
+            w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
+            w.queue = w.plist_n + 1;
+        }
+        if (pl.cache) {
+            w.need_stride = (x_stride + 31) / 32;
+            HIP_TRY(ctx->nn_lb.ensure((size_t)slots * sizeof(float)));
+            HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
+            HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
+            HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
+            HIP_TRY(ctx->miss_cnt.ensure((size_t)npairs * sizeof(int32_t)));
+            w.nn_lb = static_cast<float*>(ctx->nn_lb.p);
+            w.sinv = static_cast<int32_t*>(ctx->sinv.p);
+            w.qlist = static_cast<int32_t*>(ctx->qlist.p);
+            w.need = static_cast<uint32_t*>(ctx->need.p);
+            w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
+            // the search clears what it consumed; a fresh registration starts from zero anyway
+            HIP_TRY(hipMemsetAsync(w.need, 0, (size_t)npairs * w.need_stride * sizeof(uint32_t), st));
+            HIP_TRY(hipMemsetAsync(w.miss_cnt, 0, (size_t)npairs * sizeof(int32_t), st));
+        }
     }
     return ICP4R_OK;
 }
@@ -229,7 +259,7 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
     HIP_TRY(hipEventRecord(ne->start, st));
     if (pl.lds) {
-        HIP_TRY(launch_nn_lds(a, w, npairs, fitness_pass, first, st));
+        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ctx->ncu, st));
     } else if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
@@ -373,6 +403,8 @@ int icp4r_create(icp4r_ctx** out, int device) {
     HIP_TRY(hipSetDevice(device));
     icp4r_ctx* c = new icp4r_ctx();
     c->device = device;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -388,7 +420,8 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks})
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lb, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->batch_events})
         for (auto& ev : *v) {
@@ -628,7 +661,7 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     if (ctx->evals.p) {
         HIP_TRY(hipSetDevice(ctx->device));
         HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemset(ctx->evals.p, 0, 2 * sizeof(uint64_t)));
+        HIP_TRY(hipMemset(ctx->evals.p, 0, 4 * sizeof(uint64_t)));
     }
     return ICP4R_OK;
 }
@@ -642,7 +675,7 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
     out->splits = pl.splits;
     out->leaf = pl.leaf;
     out->lds = pl.lds ? 1 : 0;
-    out->reserved = 0;
+    out->cache = pl.cache ? 1 : 0;
     out->nn_blocks = pl.blocks;
     return ICP4R_OK;
 }
@@ -658,10 +691,20 @@ int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests
     return ICP4R_OK;
 }
 
+int icp4r_nn_cache_hits(icp4r_ctx* ctx, uint64_t* hits) {
+    if (!ctx || !hits) return fail(ICP4R_E_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    uint64_t v[4] = {0, 0, 0, 0};
+    if (ctx->evals.p) HIP_TRY(hipMemcpy(v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
+    *hits = v[2];
+    return ICP4R_OK;
+}
+
 // Internal debug hook (not in icp4r.h): the last fold_update phase timestamps of pair 0 (100 MHz
 // ticks; needs ICP4R_PHASE_TICKS=1 in the environment when the registration ran).
 int icp4r__debug_ticks(icp4r_ctx* ctx, uint64_t* out, int32_t k) {
-    if (!ctx || !out || k <= 0 || k > 8) return fail(ICP4R_E_INVALID, "bad arguments");
+    if (!ctx || !out || k <= 0 || (size_t)k * sizeof(uint64_t) > ctx->ticks.cap) return fail(ICP4R_E_INVALID, "bad arguments");
     if (!ctx->ticks.p) return fail(ICP4R_E_INVALID, "phase ticks not enabled (ICP4R_PHASE_TICKS=1)");
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());

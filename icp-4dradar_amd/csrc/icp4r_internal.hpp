@@ -17,6 +17,7 @@ constexpr int kDefaultLeaf = 16;    // pruned: targets per block
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
 constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
+constexpr int kCacheMaxN = 16384; // cached-neighbour test (nn_lds_kernel<true>): max source points per pair
 
 constexpr int kNumericsPCL = ICP4R_NUMERICS_PCL;
 constexpr int kNumericsF64 = ICP4R_NUMERICS_F64;
@@ -96,16 +97,28 @@ struct WorkArgs {
     int32_t leaf;       // pruned: targets per block (16 or 32); 0 = brute force
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):
     float4* tsort;      // [npairs * t_stride] targets in Morton-cell order, .w = original index bits;
-                        // positions [m, t_stride) repeat the last target (harmless duplicates)
+                        // positions [m, t_stride): +inf coordinates (never a match)
     int32_t* tinv;      // [npairs * t_stride] original target index -> sorted position
     float4* tbox;       // [npairs * 2 * b_stride] per block: lo, hi (empty blocks: +inf, -inf)
     float4* sbox;       // [npairs * 2 * sb_stride] per superblock of kSuper blocks: lo, hi
     int32_t* sperm;     // [npairs * x_stride] source indices in Morton-cell order
     int64_t t_stride, b_stride, sb_stride;
     float4* corr;       // PCL numerics: [npairs * x_stride * 2] per source point {s.xyz, w}, {d.xyz, d²}
-    unsigned long long* evals;
+    // Cached-neighbour test (nn_lds_kernel<true>; nullptr = off):
+    float* nn_lb;       // [npairs * x_stride] L_i: lower bound on |X_i - t_k| for every target k other
+                        // than the current NN; set by a search, lowered by every kernel that moves X_i
+    int32_t* sinv;      // [npairs * x_stride] source index -> Morton position (inverse of sperm)
+    int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)
+    uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed
+    int64_t need_stride;
+    int32_t* miss_cnt;  // [npairs] misses of the current pass (cleared by the search)
+    // Batched search (nn_lds_kernel): the pass's pair work list, heaviest first, and its queue
+    int32_t* plist;     // [npairs]
+    int32_t* plist_n;   // [1]
+    int32_t* queue;     // [1] next work-list index (reset by nn_order_kernel)
+    unsigned long long* evals;  // [4]: distance evaluations, box tests, cached-neighbour hits, -
     uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
-                        // boundaries of pair 0 — start, pass A, pass B, solve, transform  // distance evaluations of valid queries (one atomic per wave / workgroup)
+                        // boundaries of pair 0 — start, pass A, pass B, solve, transform
 };
 
 hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
@@ -114,8 +127,8 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
                             int first, hipStream_t st);
-hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int first,
-                         hipStream_t st);
+hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
+                         int ncu, hipStream_t st);
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,

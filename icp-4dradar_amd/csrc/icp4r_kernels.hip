@@ -429,8 +429,10 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
         }
         __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
         // 5. tail duplicates, block boxes, superblock boxes
+        // padding: +inf coordinates (d² = +inf never beats a real target, and no padding entry
+        // can pose as a second-nearest duplicate of a real one); .w = the last target's index
         const float4 last = ts[n - 1];
-        for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = last;
+        for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = make_float4(INFINITY, INFINITY, INFINITY, last.w);
         const int B = w.leaf;
         const int nb = (n + B - 1) / B;
         float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
@@ -461,9 +463,12 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
         }
     } else {
         int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
+        int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
         for (int i = tid; i < n; i += kIdxWG) {
             const float4 v = pts[i];
-            sp[atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u)] = i;
+            const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
+            sp[pos] = i;
+            if (si) si[i] = (int32_t)pos;
         }
     }
 }
@@ -627,199 +632,462 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
 }
 
 // ---------------------------------------------------------------------------------------------
-// nn_lds_kernel: the batched exact 1-NN (many pairs, targets <= kLdsTargets).  One workgroup per
-// pair keeps the pair's whole Morton-sorted target set in LDS (128 KB; the block / superblock
-// boxes are wave-uniform and stream through the scalar cache).  Each wave owns 64*Q Morton-contiguous queries and, instead of sweeping every
-// block that ANY of its queries might need (nn_pruned_kernel), tests blocks per query and appends
-// the (query, block) pairs that pass to a per-wave ring of work items; every 64 items are
-// evaluated one per lane (16 targets from LDS each) and merged with an LDS atomicMin on the
-// (d², index) key.  The evaluations drop from the wave's union of needed blocks to each query's
-// own needs; the answer is the same exact minimum (PCL semantics, lowest index among ties).
+// The batched exact 1-NN (many pairs, targets <= kLdsTargets): three launches per NN pass.
+//
+//  nn_cache_test_kernel  (passes after the first, CACHE only) the cached-neighbour test of every
+//                        query, elementwise at full occupancy: hits get their key / correspondence
+//                        record; misses are flagged by Morton position in the pair's bitmap (w.need)
+//                        and counted per pair (w.miss_cnt).
+//  nn_order_kernel       one workgroup: the pairs that need a search, heaviest first (pair work list
+//                        w.plist, w.plist_n), and the search's work-queue counter reset.
+//  nn_lds_kernel<CACHE>  persistent (one workgroup per CU): takes pairs from the work list; per
+//                        pair it stages the Morton-sorted target set in LDS and searches the queries
+//                        that need it (all of them in the first pass / without CACHE).
+//
+// Search (per pair, one 1024-thread workgroup, the target set in LDS — 128 KB; block / superblock
+// boxes stream through the scalar cache).  Each wave owns a Morton-contiguous run of queries and,
+// instead of sweeping every block that ANY of its queries might need (nn_pruned_kernel), tests
+// blocks per query and appends the (query, block) pairs that pass to a per-wave ring of work items;
+// every 64 items are evaluated one per lane (16 targets from LDS each) and merged with an LDS
+// atomicMin on the (d², index) key.  The answer is the same exact minimum (PCL semantics, lowest
+// index among ties).
+//
+// CACHE (cached-neighbour test, exact): a search also returns L_i, a lower bound on the distance
+// from X_i to every target other than its nearest one j (the exact second-nearest distance: the
+// search prunes against the second-best key instead of the best, and an LDS atomicMin keeps the
+// smallest key that lost a comparison).  Every kernel that moves X_i by δ_i lowers L_i by δ_i
+// (triangle inequality, move_lb).  The next pass first evaluates d_j only: if
+// L_i² (1 − m) > d_j² (1 + m) every other target is strictly farther in float too, so (d_j², j)
+// IS the brute-force answer — no tie is possible — and the query needs no search.  ICP's increments
+// shrink geometrically, so after the first few iterations most queries pass.  The margin m = 1e-4
+// is ~500x the float rounding of the test (l2_simple: <= 5 ulp; the bounds are rounded down).
+//
+// Why persistent + a work list: a late pass leaves most pairs with no miss at all and a few (slowly
+// converging) pairs with thousands; one workgroup per pair paid a dispatch gap per pair and let
+// the heavy pairs that happened to share a CU set the launch time.
 constexpr int kLdsTargets = 8192;
 constexpr int kLdsLeaf = 16;
 constexpr int kLdsWG = 1024;
 constexpr int kLdsWaves = kLdsWG / 64;
 constexpr int kLdsQ = 2;
 constexpr int kRing = 128;  // work items per wave (<= 63 pending + 64 appended per query slot)
+constexpr float kCacheMargin = 1.0e-4f;
+constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
+static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
 struct LdsNN {
-    v4f tl[kLdsTargets];
-    unsigned long long best[kLdsWaves][64 * kLdsQ];
-    uint32_t items[kLdsWaves][kRing];
+    v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, Morton order
+    unsigned long long best[kLdsWaves][64 * kLdsQ];    // 16 KB: best (d², index) key per query
+    union {
+        uint32_t sec[kLdsWaves][64 * kLdsQ];           // 8 KB: second-smallest d² bits (CACHE search)
+        int32_t wsum[kLdsWaves];                       // compaction
+    } u;
+    uint16_t items[kLdsWaves][kRing];                  // 4 KB: (query slot << 9) | block
+    int32_t cur;                                       // the pair this workgroup works on
 };
 
+// L_i from the second-smallest d² a search saw: every other target has float d² >= sec, and the
+// true distance is >= sqrt(d²)(1 - 3u); rounded down by 1e-6 (>> the sqrt's own rounding).
+__device__ __forceinline__ float lb_from_sec(float sec_d2) { return sqrtf(sec_d2) * 0.999999f; }
+
+// L_i after X_i moved from o to v (float points): L - |v - o|, both roundings covered.
+__device__ __forceinline__ float move_lb(float L, float ox, float oy, float oz, float vx, float vy, float vz) {
+    const float dx = vx - ox, dy = vy - oy, dz = vz - oz;
+    const float d = sqrtf(dx * dx + dy * dy + dz * dz);
+    return fmaxf((L - d * 1.00001f) * 0.999999f, 0.0f);
+}
+
+__device__ __forceinline__ bool cache_hit(float L, float dj2) {
+    return L * L * (1.0f - kCacheMargin) > dj2 * (1.0f + kCacheMargin);
+}
+
+__device__ __forceinline__ void write_corr_t(const WorkArgs& w, const PairArgs& a, int p, int i, float sx, float sy,
+                                             float sz, float d2, const float4 t) {
+    float4* C = w.corr + ((int64_t)p * w.x_stride + i) * 2;
+    const float wt = a.kp.huber_delta < INFINITY ? (float)huber_w(d2, a.kp.huber_delta) : 1.0f;
+    C[0] = make_float4(sx, sy, sz, wt);
+    C[1] = make_float4(t.x, t.y, t.z, d2);
+}
+
+__device__ __forceinline__ bool pass_wants(int phase, int fitness_pass) {
+    return fitness_pass ? (phase != kPhaseInvalid) : (phase == kPhaseActive);
+}
+
+// ---- nn_cache_test_kernel: grid (chunks of kTestWG * kTestPer queries, npairs), XCD-aware.
+constexpr int kTestWG = 256;
+constexpr int kTestPer = 8;
+
+__global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, WorkArgs w, int fitness_pass) {
+    __shared__ uint32_t need[kNeedWords];
+    __shared__ int32_t wmiss[kTestWG / 64];
+    const int chunks = gridDim.x;
+    const int g = xcd_remap(blockIdx.x + chunks * blockIdx.y, chunks * gridDim.y);
+    const int p = g / chunks, chunk = g - p * chunks;
+    if (!pass_wants(uload(&w.state[p].phase), fitness_pass)) return;
+    const int n = uload(a.src_n + p);
+    const int i0 = chunk * kTestWG * kTestPer;
+    if (i0 >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwords = (n + 31) >> 5;
+    for (int k = tid; k < nwords; k += kTestWG) need[k] = 0;
+    __syncthreads();
+    const float4* X = w.X + (int64_t)p * w.x_stride;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const float* lb = w.nn_lb + (int64_t)p * w.x_stride;
+    const int32_t* sinv = w.sinv + (int64_t)p * w.x_stride;
+    const float4* tgt = a.tgt + uload(a.tgt_off + p);
+    const bool corr = w.corr != nullptr && !fitness_pass;
+    // every load issued before the first store (a load after a store waits behind it on vmcnt)
+    float4 v[kTestPer];
+    NNKey k[kTestPer];
+    float L[kTestPer];
+    int32_t sp[kTestPer];
+#pragma unroll
+    for (int e = 0; e < kTestPer; ++e) {
+        const int i = min(i0 + e * kTestWG + tid, n - 1);
+        v[e] = X[i];
+        k[e] = key[i];
+        L[e] = lb[i];
+        sp[e] = sinv[i];
+    }
+    float4 t[kTestPer];
+#pragma unroll
+    for (int e = 0; e < kTestPer; ++e) t[e] = tgt[key_idx(k[e])];
+    int hits = 0, misses = 0;
+#pragma unroll
+    for (int e = 0; e < kTestPer; ++e) {
+        const int i = i0 + e * kTestWG + tid;
+        const bool valid = i < n;
+        const float d2 = l2_simple(v[e].x, v[e].y, v[e].z, t[e].x, t[e].y, t[e].z);
+        const bool hit = valid & cache_hit(L[e], d2);  // '&': a conditional use would sink the lb load
+        asm volatile("" ::"v"(sp[e]));                  // ... and keep the sinv load up front as well
+        if (hit) {
+            key[i] = make_key(d2, (uint32_t)key_idx(k[e]));
+            if (corr) write_corr_t(w, a, p, i, v[e].x, v[e].y, v[e].z, d2, t[e]);
+            ++hits;
+        } else if (valid) {
+            atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
+            ++misses;
+        }
+    }
+    hits = wave_sum(hits);
+    misses = wave_sum(misses);
+    if (lane == 0) wmiss[wave] = misses;
+    if (lane == 0) {
+        atomicAdd(w.evals, (unsigned long long)hits);
+        atomicAdd(w.evals + 2, (unsigned long long)hits);
+    }
+    __syncthreads();
+    uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+    for (int q = tid; q < nwords; q += kTestWG)
+        if (need[q]) atomicOr(gneed + q, need[q]);
+    if (tid == 0) {
+        int tot = 0;
+        for (int q = 0; q < kTestWG / 64; ++q) tot += wmiss[q];
+        if (tot) atomicAdd(w.miss_cnt + p, tot);
+    }
+}
+
+// ---- nn_order_kernel: one workgroup.  Pairs to search, bucketed by floor(log2(work)) heaviest
+// first (longest-processing-time-first for the persistent search; the order inside a bucket is
+// arbitrary and cannot change any result).  all = 1: every pair the pass wants (first pass / no
+// CACHE), work = its source count.
+constexpr int kOrderWG = 1024;
+constexpr int kOrderBuckets = 32;
+
+__global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
+                                                            int all) {
+    __shared__ int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
+    const int tid = threadIdx.x;
+    if (tid < kOrderBuckets) bcnt[tid] = 0;
+    __syncthreads();
+    for (int p = tid; p < npairs; p += kOrderWG) {
+        const int c = !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
+        if (c > 0) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)c)], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int run = 0;
+        for (int b = kOrderBuckets - 1; b >= 0; --b) {
+            boff[b] = run;
+            run += bcnt[b];
+        }
+        *w.plist_n = run;
+        *w.queue = 0;
+    }
+    __syncthreads();
+    for (int p = tid; p < npairs; p += kOrderWG) {
+        const int c = !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
+        if (c > 0) w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)c)], 1)] = p;
+    }
+}
+
+// ---- nn_lds_kernel<CACHE>: persistent search over the pair work list.
+template <bool CACHE>
 __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
     constexpr int Q = kLdsQ;
     __shared__ LdsNN sh;
-    const int p = xcd_remap(blockIdx.x, gridDim.x);
-    const int phase = uload(&w.state[p].phase);
-    if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
-    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
-    if (n <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
-    {  // stage the pair's sorted targets into LDS
-        const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
-        const int nt = nsb * kSuper * kLdsLeaf;
-        for (int i = tid; i < nt; i += kLdsWG) sh.tl[i] = tsg[i];
-    }
-    __syncthreads();
-    const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
-    const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-    const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
-    const float4* X = w.X + (int64_t)p * w.x_stride;
-    const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
-    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
-    const float4* tgt = a.tgt + uload(a.tgt_off + p);
-    unsigned long long* bestl = sh.best[wave];
-    uint32_t* ring = sh.items[wave];
+    const bool corr = w.corr != nullptr && !fitness_pass;
+    const int npl = uload(w.plist_n);
     unsigned long long evals = 0, tests = 0;
+    for (;;) {
+        if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
+        __syncthreads();
+        const int idx = sh.cur;
+        if (idx >= npl) break;  // uniform: every wave read the same sh.cur
+        const int p = w.plist[idx];
+        const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+        const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
+        float4* X = w.X + (int64_t)p * w.x_stride;
+        const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
+        NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+        const float4* tgt = a.tgt + uload(a.tgt_off + p);
 
-    for (int base = wave * 64 * Q; base < n; base += kLdsWaves * 64 * Q) {
-        float x[Q], y[Q], z[Q];
-        NNKey best[Q];
-        int orig[Q];
+        // the queries to search: all (first pass / no CACHE) or the test kernel's misses, compacted
+        // from the pair's bitmap in Morton order (stable); the bitmap is cleared for the next pass
+        int nlist = n;
+        const int32_t* list = sperm;
+        if (CACHE && !first) {
+            int32_t* qlist = w.qlist + (int64_t)p * w.x_stride;
+            uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+            const int nwords = (n + 31) >> 5;
+            const uint32_t f = tid < nwords ? gneed[tid] : 0u;
+            const int c = __builtin_popcount(f);
+            int incl = c;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int s0 = base + lane + q * 64;
-            const int s = min(s0, n - 1);
-            const int o = sperm[s];
-            orig[q] = s0 < n ? o : -1;
-            const float4 v = X[o];
-            x[q] = v.x;
-            y[q] = v.y;
-            z[q] = v.z;
-            const uint32_t j = first ? __float_as_uint(sh.tl[((int64_t)s * m) / n].w) : (uint32_t)key_idx(key[o]);
-            const float4 t = tgt[j];
-            best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
-            bestl[q * 64 + lane] = best[q];
+            for (int off = 1; off < 64; off <<= 1) {
+                const int o = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += o;
+            }
+            if (lane == 63) sh.u.wsum[wave] = incl;
+            __syncthreads();
+            int base = 0, total = 0;
+            for (int v = 0; v < kLdsWaves; ++v) {
+                const int s = sh.u.wsum[v];
+                base += v < wave ? s : 0;
+                total += s;
+            }
+            if (f) {  // all 32 source indices of the word in one go (no load behind a store)
+                int4 sv[8];
+                const int4* s4 = reinterpret_cast<const int4*>(sperm + tid * 32);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sv[e] = s4[e];
+                int o = base + incl - c;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if ((f >> (4 * e)) & 1) qlist[o++] = sv[e].x;
+                    if ((f >> (4 * e + 1)) & 1) qlist[o++] = sv[e].y;
+                    if ((f >> (4 * e + 2)) & 1) qlist[o++] = sv[e].z;
+                    if ((f >> (4 * e + 3)) & 1) qlist[o++] = sv[e].w;
+                }
+                gneed[tid] = 0;
+            }
+            if (tid == 0) w.miss_cnt[p] = 0;
+            nlist = total;
+            list = qlist;
+            __syncthreads();  // qlist (global, this workgroup's) visible to the whole workgroup
         }
-        float qlo[3], qhi[3], qmax = 0.0f;
-        qlo[0] = qhi[0] = x[0];
-        qlo[1] = qhi[1] = y[0];
-        qlo[2] = qhi[2] = z[0];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            qlo[0] = fminf(qlo[0], x[q]); qhi[0] = fmaxf(qhi[0], x[q]);
-            qlo[1] = fminf(qlo[1], y[q]); qhi[1] = fmaxf(qhi[1], y[q]);
-            qlo[2] = fminf(qlo[2], z[q]); qhi[2] = fmaxf(qhi[2], z[q]);
-            qmax = fmaxf(qmax, key_d2(best[q]));
+
+        {  // stage the pair's sorted targets into LDS
+            const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
+            const int nt = nsb * kSuper * kLdsLeaf;
+            for (int i = tid; i < nt; i += kLdsWG) sh.tl[i] = tsg[i];
         }
+        __syncthreads();
+        const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
+        const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
+        const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
+        const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+        unsigned long long* bestl = sh.best[wave];
+        uint32_t* secl = sh.u.sec[wave];
+        uint16_t* ring = sh.items[wave];
+
+        // Queries per wave run: 64*Q from a long list; a short one (the misses of a late pass) is
+        // spread over all waves in Morton-contiguous runs — the traversal is latency-bound per wave,
+        // and a small run's tight query box lets the coarse tests prune most superblocks.
+        const int per = min(64 * Q, (nlist + kLdsWaves - 1) / kLdsWaves);
+        for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
+            const int cend = min(base + per, nlist);
+            float x[Q], y[Q], z[Q];
+            float bnd[Q];  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
+                           // -1 on idle lanes (never queue work, never widen the coarse bound)
+            int orig[Q];
+            int seed_pos0 = 0;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
+            for (int q = 0; q < Q; ++q) {
+                const int s0 = base + lane + q * 64;
+                const int s = s0 < cend ? s0 : base;  // idle lanes shadow the run's first query
+                const int o = list[s];
+                orig[q] = s0 < cend ? o : -1;
+                const float4 v = X[o];
+                x[q] = v.x;
+                y[q] = v.y;
+                z[q] = v.z;
+                // seed: the previous match (first pass: the target at the same relative Morton position)
+                const int pj = first ? (int)(((int64_t)s * m) / n) : tinv[key_idx(key[o])];
+                const v4f tj = sh.tl[pj];
+                const NNKey kj = make_key(l2_simple(x[q], y[q], z[q], tj.x, tj.y, tj.z), __float_as_uint(tj.w));
+                if (q == 0) seed_pos0 = pj;
+                if (CACHE) {
+                    // second seed: the Morton neighbour of the first (an upper bound of the second-nearest)
+                    NNKey k2 = ~0ull;
+                    if (m > 1) {
+                        const v4f tn = sh.tl[pj + 1 < m ? pj + 1 : pj - 1];
+                        k2 = make_key(l2_simple(x[q], y[q], z[q], tn.x, tn.y, tn.z), __float_as_uint(tn.w));
+                    }
+                    const NNKey lo = kj < k2 ? kj : k2, hi = kj < k2 ? k2 : kj;
+                    bestl[q * 64 + lane] = lo;
+                    secl[q * 64 + lane] = (uint32_t)(hi >> 32);
+                    bnd[q] = orig[q] >= 0 ? key_d2(hi) : -1.0f;
+                } else {
+                    bestl[q * 64 + lane] = kj;
+                    bnd[q] = orig[q] >= 0 ? key_d2(kj) : -1.0f;
+                }
+            }
+            float qlo[3], qhi[3], qmax = 0.0f;
+            qlo[0] = qhi[0] = x[0];
+            qlo[1] = qhi[1] = y[0];
+            qlo[2] = qhi[2] = z[0];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                qlo[0] = fminf(qlo[0], x[q]); qhi[0] = fmaxf(qhi[0], x[q]);
+                qlo[1] = fminf(qlo[1], y[q]); qhi[1] = fmaxf(qhi[1], y[q]);
+                qlo[2] = fminf(qlo[2], z[q]); qhi[2] = fmaxf(qhi[2], z[q]);
+                qmax = fmaxf(qmax, bnd[q]);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
+                    qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
+                }
+                qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+            }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
-                qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
+                qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
+                qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
             }
-            qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
-            qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
-        }
-        qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
+            qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
 
-        // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
-        uint32_t head = 0, tail = 0;
-        auto drain = [&](uint32_t cnt) {
-            const bool act = (uint32_t)lane < cnt;
-            const uint32_t it = ring[(head + lane) & (kRing - 1)];
-            const int qi = act ? (int)(it >> 16) : 0;
-            const int b = act ? (int)(it & 0xffffu) : 0;
-            const int owner = qi & 63, slot = qi >> 6;
-            float qx = 0.f, qy = 0.f, qz = 0.f;
+            // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
+            uint32_t head = 0, tail = 0;
+            auto drain = [&](uint32_t cnt) {
+                const bool act = (uint32_t)lane < cnt;
+                const uint32_t it = ring[(head + lane) & (kRing - 1)];
+                const int qi = act ? (int)(it >> 9) : 0;
+                const int b = act ? (int)(it & 0x1ffu) : 0;
+                const int owner = qi & 63, slot = qi >> 6;
+                float qx = 0.f, qy = 0.f, qz = 0.f;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) {  // the query's coordinates from its owner lane
-                const float vx = __shfl(x[q], owner, 64), vy = __shfl(y[q], owner, 64), vz = __shfl(z[q], owner, 64);
-                if (slot == q) {
-                    qx = vx;
-                    qy = vy;
-                    qz = vz;
+                for (int q = 0; q < Q; ++q) {  // the query's coordinates from its owner lane
+                    const float vx = __shfl(x[q], owner, 64), vy = __shfl(y[q], owner, 64), vz = __shfl(z[q], owner, 64);
+                    if (slot == q) {
+                        qx = vx;
+                        qy = vy;
+                        qz = vz;
+                    }
+                }
+                if (act) {
+                    NNKey k1 = ~0ull;
+                    uint32_t s2 = 0x7f800000u;  // second-smallest d² of the block (bits; +inf)
+                    const v4f* tb = sh.tl + b * kLdsLeaf;
+#pragma unroll
+                    for (int t = 0; t < kLdsLeaf; ++t) {
+                        const v4f c = tb[t];
+                        const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
+                        const NNKey kn = make_key(d2, __float_as_uint(c.w));
+                        if (CACHE) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
+                        k1 = kn < k1 ? kn : k1;
+                    }
+                    if (CACHE) {
+                        // every key but the final winner loses exactly one comparison: keep the smallest loser
+                        const NNKey old = atomicMin(&bestl[qi], k1);
+                        const uint32_t cand =
+                            k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
+                        atomicMin(&secl[qi], cand);
+                    } else {
+                        atomicMin(&bestl[qi], k1);
+                    }
+                }
+                head += cnt;
+                evals += (unsigned long long)cnt * kLdsLeaf;
+#pragma unroll
+                for (int q = 0; q < Q; ++q)  // tighter bounds for the tests
+                    bnd[q] = orig[q] < 0 ? -1.0f
+                             : CACHE     ? __uint_as_float(secl[q * 64 + lane])
+                                         : key_d2(bestl[q * 64 + lane]);
+            };
+            // Queue the lanes whose query `q` may reach block b.
+            auto push = [&](int b, const v4f lo, const v4f hi, uint32_t qslots) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    if (!((qslots >> q) & 1)) continue;
+                    tests += 64;
+                    const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
+                    const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
+                    const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
+                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                    const bool need = lbd * kLbShrink <= bnd[q];
+                    const uint64_t mask = __ballot(need);
+                    if (mask == 0) continue;
+                    if (need) {
+                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                        ring[(tail + rank) & (kRing - 1)] = (uint16_t)(((uint32_t)(q * 64 + lane) << 9) | (uint32_t)b);
+                    }
+                    tail += (uint32_t)__builtin_popcountll(mask);
+                    if (tail - head >= 64) drain(64);
+                }
+            };
+            // coarse test of every superblock at once (lane = superblock; nsb <= 64 here)
+            uint64_t cmask;
+            {
+                const int sbl = min(lane, nsb - 1);
+                const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+                cmask = __ballot(lane < nsb && box_maybe(sbv[2 * sbl], sbv[2 * sbl + 1], qlo, qhi, qmax));
+                tests += nsb;
+            }
+            const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos0) / (kLdsLeaf * kSuper);
+            int up = sb0, dn = sb0 - 1;
+            for (int k = 0; k < nsb; ++k) {
+                const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
+                if (!((cmask >> sb) & 1)) continue;
+                const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+                tests += 64 * Q + kSuper;
+                uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const float gx = fmaxf(fmaxf(slo.x - x[q], x[q] - shi.x), 0.0f);
+                    const float gy = fmaxf(fmaxf(slo.y - y[q], y[q] - shi.y), 0.0f);
+                    const float gz = fmaxf(fmaxf(slo.z - z[q], z[q] - shi.z), 0.0f);
+                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                    if (__ballot(lbd * kLbShrink <= bnd[q]) != 0) qslots |= 1u << q;
+                }
+                if (qslots == 0) continue;
+                // coarse test of the superblock's blocks at once (lanes 0..7)
+                const int bl = sb * kSuper + (lane & (kSuper - 1));
+                uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
+                while (bmask) {
+                    const int b = sb * kSuper + __builtin_ctz(bmask);
+                    bmask &= bmask - 1;
+                    push(b, tbx[2 * b], tbx[2 * b + 1], qslots);
                 }
             }
-            if (act) {
-                NNKey lb = ~0ull;
-                const v4f* tb = sh.tl + b * kLdsLeaf;
-#pragma unroll
-                for (int t = 0; t < kLdsLeaf; ++t) {
-                    const v4f c = tb[t];
-                    const NNKey kn = make_key(l2_simple(qx, qy, qz, c.x, c.y, c.z), __float_as_uint(c.w));
-                    lb = kn < lb ? kn : lb;
-                }
-                atomicMin(&bestl[qi], lb);
-            }
-            head += cnt;
-            evals += (unsigned long long)cnt * kLdsLeaf;
-#pragma unroll
-            for (int q = 0; q < Q; ++q) best[q] = bestl[q * 64 + lane];  // tighter bounds for the tests
-        };
-        // Queue the lanes whose query `q` may reach block b.
-        auto push = [&](int b, const v4f lo, const v4f hi, uint32_t qslots) {
+            if (tail != head) drain(tail - head);
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
-                if (!((qslots >> q) & 1)) continue;
-                tests += 64;
-                const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
-                const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
-                const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
-                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                const bool need = lbd * kLbShrink <= key_d2(best[q]);
-                const uint64_t mask = __ballot(need);
-                if (mask == 0) continue;
-                if (need) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                    ring[(tail + rank) & (kRing - 1)] = ((uint32_t)(q * 64 + lane) << 16) | (uint32_t)b;
-                }
-                tail += (uint32_t)__builtin_popcountll(mask);
-                if (tail - head >= 64) drain(64);
-            }
-        };
-        // coarse test of every superblock at once (lane = superblock; nsb <= 64 here)
-        uint64_t cmask;
-        {
-            const int sbl = min(lane, nsb - 1);
-            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-            cmask = __ballot(lane < nsb && box_maybe(sbv[2 * sbl], sbv[2 * sbl + 1], qlo, qhi, qmax));
-            tests += nsb;
-        }
-        const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
-        const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (kLdsLeaf * kSuper);
-        int up = sb0, dn = sb0 - 1;
-        for (int k = 0; k < nsb; ++k) {
-            const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
-            if (!((cmask >> sb) & 1)) continue;
-            const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
-            tests += 64 * Q + kSuper;
-            uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                const float gx = fmaxf(fmaxf(slo.x - x[q], x[q] - shi.x), 0.0f);
-                const float gy = fmaxf(fmaxf(slo.y - y[q], y[q] - shi.y), 0.0f);
-                const float gz = fmaxf(fmaxf(slo.z - z[q], z[q] - shi.z), 0.0f);
-                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                if (__ballot(lbd * kLbShrink <= key_d2(best[q])) != 0) qslots |= 1u << q;
-            }
-            if (qslots == 0) continue;
-            // coarse test of the superblock's blocks at once (lanes 0..7)
-            const int bl = sb * kSuper + (lane & (kSuper - 1));
-            uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
-            while (bmask) {
-                const int b = sb * kSuper + __builtin_ctz(bmask);
-                bmask &= bmask - 1;
-                push(b, tbx[2 * b], tbx[2 * b + 1], qslots);
+                if (orig[q] < 0) continue;
+                const NNKey kb = bestl[q * 64 + lane];
+                key[orig[q]] = kb;
+                if (CACHE) w.nn_lb[(int64_t)p * w.x_stride + orig[q]] = lb_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                if (corr) write_corr(w, a, p, orig[q], x[q], y[q], z[q], kb, tgt);
             }
         }
-        if (tail != head) drain(tail - head);
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (orig[q] < 0) continue;
-            key[orig[q]] = best[q];
-            if (w.corr != nullptr && !fitness_pass) write_corr(w, a, p, orig[q], x[q], y[q], z[q], best[q], tgt);
-        }
+        __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
     }
     if (lane == 0) {
         atomicAdd(w.evals, evals);
@@ -973,15 +1241,18 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
 }
 
 // transformCloud(*input_transformed, *input_transformed, transformation_) by the whole workgroup.
+// With the cached-neighbour test on (lb != nullptr) every moved point also lowers its bound L_i.
 template <int WG>
-__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds) {
+__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds, float* lb) {
     float Tl[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) Tl[k] = T_lds[k];
     for (int i = threadIdx.x; i < n; i += WG) {
-        float4 s = X[i];
-        xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
-        X[i] = s;
+        const float4 s = X[i];
+        float4 o = s;
+        xform_pt(Tl, s.x, s.y, s.z, o.x, o.y, o.z);
+        X[i] = o;
+        if (lb) lb[i] = move_lb(lb[i], s.x, s.y, s.z, o.x, o.y, o.z);
     }
 }
 
@@ -1149,7 +1420,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
     if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
-    transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
+    transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc, w.nn_lb ? w.nn_lb + (int64_t)p * xs : nullptr);
     __syncthreads();
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
 }
@@ -1201,7 +1472,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
     if (tid == 0) solve_pair<kNumericsF64>(sh, st, kp);
     __syncthreads();
     if (sh.flag == 1) return;
-    transform_pair<kUpdWG>(X, n, sh.T_inc);
+    transform_pair<kUpdWG>(X, n, sh.T_inc, w.nn_lb ? w.nn_lb + (int64_t)p * w.x_stride : nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1216,10 +1487,15 @@ __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs 
     const int n = a.src_n[p];
     const float4* src = a.src + a.src_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
+    float* lb = w.nn_lb ? w.nn_lb + (int64_t)p * w.x_stride : nullptr;
     for (int i = threadIdx.x; i < n; i += 256) {
         const float4 s = src[i];
         float4 o = s;
         xform_pt(Tf, s.x, s.y, s.z, o.x, o.y, o.z);
+        if (lb) {
+            const float4 old = X[i];
+            lb[i] = move_lb(lb[i], old.x, old.y, old.z, o.x, o.y, o.z);
+        }
         X[i] = o;
     }
 }
@@ -1344,10 +1620,24 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
     return hipGetLastError();
 }
 
-hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int first,
-                         hipStream_t st) {
-    if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nn_lds_kernel, dim3(npairs), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
+                         int ncu, hipStream_t st) {
+    if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
+    const bool cache = w.nn_lb != nullptr;
+    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt))
+        return hipErrorInvalidValue;
+    if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
+    if (cache && !first) {
+        const int chunks = (max_n + kTestWG * kTestPer - 1) / (kTestWG * kTestPer);
+        hipLaunchKernelGGL(nn_cache_test_kernel, dim3(chunks, npairs), dim3(kTestWG), 0, st, a, w, fitness_pass);
+    }
+    hipLaunchKernelGGL(nn_order_kernel, dim3(1), dim3(kOrderWG), 0, st, a, w, npairs, fitness_pass,
+                       (first || !cache) ? 1 : 0);
+    const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
+    if (cache)
+        hipLaunchKernelGGL(nn_lds_kernel<true>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    else
+        hipLaunchKernelGGL(nn_lds_kernel<false>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     return hipGetLastError();
 }
 

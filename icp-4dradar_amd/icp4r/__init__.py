@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
-    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters",
+    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits",
 ]
 # include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
 MAP_EXPORTED_SYMBOLS = [
@@ -111,7 +111,7 @@ class Batch(C.Structure):
 
 class PlanInfo(C.Structure):
     _fields_ = [("pruned", C.c_int32), ("q", C.c_int32), ("splits", C.c_int32), ("leaf", C.c_int32),
-                ("lds", C.c_int32), ("reserved", C.c_int32), ("nn_blocks", C.c_int64)]
+                ("lds", C.c_int32), ("cache", C.c_int32), ("nn_blocks", C.c_int64)]
 
 
 assert C.sizeof(Result) == 96
@@ -151,6 +151,7 @@ def load():
         "icp4r_kernel_time_reset": (C.c_int, [vp]),
         "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
         "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "icp4r_nn_cache_hits": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         # icp4r_map.h
         "icp4r_map_create": (C.c_int, [vp, C.POINTER(vp)]),
         "icp4r_map_destroy": (C.c_int, [vp]),
@@ -300,6 +301,12 @@ class Context:
         _check(self._lib.icp4r_nn_counters(self._h, C.byref(v), C.byref(t)), "icp4r_nn_counters")
         return v.value, t.value
 
+    def nn_cache_hits(self) -> int:
+        """Queries the cached-neighbour test resolved without a search since the last reset_timers()."""
+        v = C.c_uint64()
+        _check(self._lib.icp4r_nn_cache_hits(self._h, C.byref(v)), "icp4r_nn_cache_hits")
+        return v.value
+
     def nn_evaluations(self) -> int:
         """Distance evaluations (query x target) of the NN kernels since the last reset_timers()."""
         return self.nn_counters()[0]
@@ -308,7 +315,7 @@ class Context:
 def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO) -> dict:
     info = PlanInfo()
     _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, nn_mode, C.byref(info)), "icp4r_plan")
-    return {"pruned": bool(info.pruned), "lds": bool(info.lds), "q": info.q, "splits": info.splits,
+    return {"pruned": bool(info.pruned), "lds": bool(info.lds), "cache": bool(info.cache), "q": info.q, "splits": info.splits,
             "leaf": info.leaf, "nn_blocks": info.nn_blocks}
 
 

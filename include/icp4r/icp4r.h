@@ -172,6 +172,11 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx);
  * pruned search only; may be NULL).  Synchronises the context's device. */
 int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests);
 
+/* Queries whose nearest neighbour the cached-neighbour test proved unchanged without a search
+ * (icp4r_plan_info.cache) since the last icp4r_kernel_time_reset; each counts as one evaluation
+ * in icp4r_nn_counters.  Synchronises the context's device. */
+int icp4r_nn_cache_hits(icp4r_ctx* ctx, uint64_t* hits);
+
 /* Launch geometry the batch path picks for a shape — exposed for tests and the benchmark report. */
 typedef struct icp4r_plan_info {
     int32_t pruned;     /* 1: ICP4R_NN_PRUNED kernel, 0: brute force                 */
@@ -180,7 +185,9 @@ typedef struct icp4r_plan_info {
     int32_t leaf;       /* pruned: targets per block                                 */
     int32_t lds;        /* pruned batch kernel with the target set in LDS (per-query
                            work lists); used for >= 256 pairs with <= 8192 targets    */
-    int32_t reserved;
+    int32_t cache;      /* lds: cached-neighbour test (a query keeps its previous NN
+                           without a search when a second-nearest bound proves it;
+                           exact); off with ICP4R_NN_CACHE=0                          */
     int64_t nn_blocks;  /* workgroups of one NN launch                               */
 } icp4r_plan_info;
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);

@@ -75,6 +75,7 @@ def test_plan_geometry():
 
     big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
     assert big["pruned"] and big["lds"] and big["q"] == 2 and big["leaf"] == 16 and big["nn_blocks"] == 1024
+    assert big["cache"] and not icp4r.plan(1024, 16385, 8192)["cache"]  # cached-neighbour test: n <= 16384
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
     single = icp4r.plan(1, 8192, 8192)  # C2: streamed kernel, one query per lane to fill more waves

@@ -176,15 +176,16 @@ def test_target_split_equals_unsplit(gpu_ctx):
         assert (res[k]["T"] == np.array(r.T, np.float32)).all()
 
 
-@pytest.mark.parametrize("lds", ["0", "1"])
+@pytest.mark.parametrize("lds,cache", [("0", "1"), ("1", "0"), ("1", "1")])
 @pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map"])
-def test_nn_modes_identical(gpu_ctx, case, lds, monkeypatch):
-    """Pruned (streamed, or with the target set in LDS and per-query work lists), brute-force and
-    packed searches produce bit-identical registrations (T, fitness, iterations, aligned cloud) —
-    the pruned index changes only which targets are evaluated."""
+def test_nn_modes_identical(gpu_ctx, case, lds, cache, monkeypatch):
+    """Pruned (streamed, or with the target set in LDS and per-query work lists, with or without the
+    cached-neighbour test), brute-force and packed searches produce bit-identical registrations (T,
+    fitness, iterations, aligned cloud) — the pruned index changes only which targets are evaluated."""
     import icp4r
 
     monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
+    monkeypatch.setenv("ICP4R_NN_CACHE", cache)
     guess = None
     if case == "c2":
         pairs = [_pair(310, 8192)]
@@ -221,6 +222,40 @@ def test_nn_modes_identical(gpu_ctx, case, lds, monkeypatch):
         res = {mode: gpu_ctx.align_batch_host(*_batch(pairs), params=icp4r.default_params(nn_mode=mode, **p))
                for mode in (icp4r.NN_PRUNED, icp4r.NN_BRUTE)}
         assert res[icp4r.NN_PRUNED].tobytes() == res[icp4r.NN_BRUTE].tobytes()
+
+
+@pytest.mark.parametrize("numerics,huber", [(0, float("inf")), (1, float("inf")), (0, 0.5), (1, 0.5)])
+def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatch):
+    """The batched LDS search with the cached-neighbour test: bit-identical to the same search
+    without it (every numerics / weighting), to the oracle (PCL numerics), and it resolves most
+    queries of the late iterations without a search."""
+    import icp4r
+
+    npairs, n = 256, 8192
+    pairs = [_pair(700 + k, n) for k in range(npairs)]
+    args = _batch(pairs)
+    assert icp4r.plan(npairs, n, n)["lds"] and icp4r.plan(npairs, n, n)["cache"]
+    p = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
+                             numerics=numerics, huber_delta=huber)
+    monkeypatch.setenv("ICP4R_NN_CACHE", "0")
+    gpu_ctx.reset_timers()
+    plain = gpu_ctx.align_batch_host(*args, params=p)
+    ev_plain, _ = gpu_ctx.nn_counters()
+    monkeypatch.setenv("ICP4R_NN_CACHE", "1")
+    gpu_ctx.reset_timers()
+    cached = gpu_ctx.align_batch_host(*args, params=p)
+    ev_cached, _ = gpu_ctx.nn_counters()
+    hits = gpu_ctx.nn_cache_hits()
+    assert cached.tobytes() == plain.tobytes()
+    assert (cached["status"] == 0).all() and (cached["iterations"] == 20).all()
+    queries = npairs * n * 21  # 20 iterations + the fitness pass
+    assert hits > 0.5 * queries, (hits, queries)
+    assert ev_cached < ev_plain
+    if numerics == 0:
+        for k in (0, 131, 255):
+            o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20,
+                                 mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, huber_delta=huber)
+            assert (cached[k]["T"].reshape(4, 4).T == o["T"]).all() and cached[k]["fitness"] == o["fitness"]
 
 
 def test_pruned_evaluates_fewer_pairs(gpu_ctx):
