@@ -65,6 +65,21 @@ using icp4r_host::pack_host;
 
 namespace {
 
+constexpr size_t kCountBytes = (size_t)kCountSlots * kCountStride * sizeof(uint64_t);
+
+// Sum the per-slot work counters (evaluations, box tests, cache hits) since the last reset.
+int read_counters(icp4r_ctx* ctx, uint64_t (&out)[3]) {
+    out[0] = out[1] = out[2] = 0;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (!ctx->evals.p) return ICP4R_OK;
+    std::vector<uint64_t> v((size_t)kCountSlots * kCountStride);
+    HIP_TRY(hipMemcpy(v.data(), ctx->evals.p, kCountBytes, hipMemcpyDeviceToHost));
+    for (int s = 0; s < kCountSlots; ++s)
+        for (int k = 0; k < 3; ++k) out[k] += v[(size_t)s * kCountStride + k];
+    return ICP4R_OK;
+}
+
 struct Plan {
     int q;
     bool packed;  // brute force: v_pk_* FP32 sweep (two queries per register pair)
@@ -192,8 +207,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     w.x_stride = x_stride;
     w.splits = pl.splits;
     if (!ctx->evals.p) {
-        HIP_TRY(ctx->evals.ensure(4 * sizeof(uint64_t)));
-        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, 4 * sizeof(uint64_t), st));
+        HIP_TRY(ctx->evals.ensure(kCountBytes));
+        HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, kCountBytes, st));
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
@@ -234,6 +249,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         if (pl.cache) {
             w.need_stride = (x_stride + 31) / 32;
             HIP_TRY(ctx->nn_lb.ensure((size_t)slots * sizeof(float)));
+            HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
+            w.nn_t = static_cast<float4*>(ctx->nn_t.p);
             HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
@@ -420,7 +437,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lb, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lb, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->batch_events})
@@ -661,7 +678,7 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     if (ctx->evals.p) {
         HIP_TRY(hipSetDevice(ctx->device));
         HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemset(ctx->evals.p, 0, 4 * sizeof(uint64_t)));
+        HIP_TRY(hipMemset(ctx->evals.p, 0, kCountBytes));
     }
     return ICP4R_OK;
 }
@@ -682,10 +699,9 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
 
 int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests) {
     if (!ctx || !evaluations) return fail(ICP4R_E_INVALID, "NULL argument");
-    HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipDeviceSynchronize());
-    uint64_t v[2] = {0, 0};
-    if (ctx->evals.p) HIP_TRY(hipMemcpy(v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
+    uint64_t v[3];
+    int rc = read_counters(ctx, v);
+    if (rc) return rc;
     *evaluations = v[0];
     if (box_tests) *box_tests = v[1];
     return ICP4R_OK;
@@ -693,10 +709,9 @@ int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests
 
 int icp4r_nn_cache_hits(icp4r_ctx* ctx, uint64_t* hits) {
     if (!ctx || !hits) return fail(ICP4R_E_INVALID, "NULL argument");
-    HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipDeviceSynchronize());
-    uint64_t v[4] = {0, 0, 0, 0};
-    if (ctx->evals.p) HIP_TRY(hipMemcpy(v, ctx->evals.p, sizeof(v), hipMemcpyDeviceToHost));
+    uint64_t v[3];
+    int rc = read_counters(ctx, v);
+    if (rc) return rc;
     *hits = v[2];
     return ICP4R_OK;
 }

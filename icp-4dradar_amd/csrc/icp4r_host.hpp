@@ -64,8 +64,8 @@ struct icp4r_ctx {
     // staging for the host-buffer entry points
     icp4r_host::DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace
-    icp4r_host::DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks, nn_lb, sinv, qlist, need, miss_cnt,
-        plist, plist_n;
+    icp4r_host::DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks, nn_lb, nn_t, sinv, qlist, need,
+        miss_cnt, plist, plist_n;
     int ncu = 256;  // compute units of the device (persistent launches)
     std::vector<icp4r_host::EventPair> nn_events, batch_events;
     size_t nn_used = 0, batch_used = 0;

@@ -18,6 +18,10 @@ constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitn
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
 constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
 constexpr int kCacheMaxN = 16384; // cached-neighbour test (nn_lds_kernel<true>): max source points per pair
+// Work counters: one 128-B slot per wave (mod kCountSlots).  A single counter word hit by every wave
+// of a launch serialises the atomics at one L2 channel (~10 ns each: 30k waves = 0.3 ms per launch).
+constexpr int kCountSlots = 2048;
+constexpr int kCountStride = 16;
 
 constexpr int kNumericsPCL = ICP4R_NUMERICS_PCL;
 constexpr int kNumericsF64 = ICP4R_NUMERICS_F64;
@@ -107,6 +111,7 @@ struct WorkArgs {
     // Cached-neighbour test (nn_lds_kernel<true>; nullptr = off):
     float* nn_lb;       // [npairs * x_stride] L_i: lower bound on |X_i - t_k| for every target k other
                         // than the current NN; set by a search, lowered by every kernel that moves X_i
+    float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index (bits)
     int32_t* sinv;      // [npairs * x_stride] source index -> Morton position (inverse of sperm)
     int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)
     uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed
@@ -116,7 +121,8 @@ struct WorkArgs {
     int32_t* plist;     // [npairs]
     int32_t* plist_n;   // [1]
     int32_t* queue;     // [1] next work-list index (reset by nn_order_kernel)
-    unsigned long long* evals;  // [4]: distance evaluations, box tests, cached-neighbour hits, -
+    unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,
+                                // cached-neighbour hits (count_add; the host sums the slots)
     uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
                         // boundaries of pair 0 — start, pass A, pass B, solve, transform
 };

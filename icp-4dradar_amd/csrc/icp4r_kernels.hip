@@ -65,6 +65,14 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
     return xcd * per + min(xcd, rem) + slot;
 }
 
+// Work counters: add v to counter k of this wave's slot.  Call from one lane.
+__device__ __forceinline__ void count_add(unsigned long long* ctr, int k, unsigned long long v) {
+    if (v == 0) return;
+    const uint32_t blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const uint32_t slot = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kCountSlots;
+    atomicAdd(ctr + (size_t)slot * kCountStride + k, v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Exact brute-force 1-NN of Q register-resident queries per lane over targets [j0, j1) of a
 // wave-uniform target array; increasing index order and strict '<' => lowest index wins ties.
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int f
         nn_sweep<Q>(x, y, z, a.tgt + uload(a.tgt_off + p), j0, j1, best, bi);
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     if (threadIdx.x == 0)
-        atomicAdd(w.evals, (unsigned long long)(j1 - j0) * (unsigned long long)min(n - base, kNNWG * Q));
+        count_add(w.evals, 0, (unsigned long long)(j1 - j0) * (unsigned long long)min(n - base, kNNWG * Q));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int i = base + threadIdx.x + q * kNNWG;
@@ -618,8 +626,8 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
         }
     }
     if (lane == 0) {
-        atomicAdd(w.evals, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
-        atomicAdd(w.evals + 1, tests);
+        count_add(w.evals, 0, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
+        count_add(w.evals, 1, tests);
     }
     if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence arrays
 #pragma unroll
@@ -734,25 +742,22 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     const float4* X = w.X + (int64_t)p * w.x_stride;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const float* lb = w.nn_lb + (int64_t)p * w.x_stride;
+    const float4* nt = w.nn_t + (int64_t)p * w.x_stride;
     const int32_t* sinv = w.sinv + (int64_t)p * w.x_stride;
-    const float4* tgt = a.tgt + uload(a.tgt_off + p);
     const bool corr = w.corr != nullptr && !fitness_pass;
-    // every load issued before the first store (a load after a store waits behind it on vmcnt)
-    float4 v[kTestPer];
-    NNKey k[kTestPer];
+    // Every load is coalesced (the NN's coordinates come from nn_t, not a gather from the target
+    // cloud) and issued before the first store (a load after a store waits behind it on vmcnt).
+    float4 v[kTestPer], t[kTestPer];
     float L[kTestPer];
     int32_t sp[kTestPer];
 #pragma unroll
     for (int e = 0; e < kTestPer; ++e) {
         const int i = min(i0 + e * kTestWG + tid, n - 1);
         v[e] = X[i];
-        k[e] = key[i];
+        t[e] = nt[i];
         L[e] = lb[i];
         sp[e] = sinv[i];
     }
-    float4 t[kTestPer];
-#pragma unroll
-    for (int e = 0; e < kTestPer; ++e) t[e] = tgt[key_idx(k[e])];
     int hits = 0, misses = 0;
 #pragma unroll
     for (int e = 0; e < kTestPer; ++e) {
@@ -762,7 +767,7 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
         const bool hit = valid & cache_hit(L[e], d2);  // '&': a conditional use would sink the lb load
         asm volatile("" ::"v"(sp[e]));                  // ... and keep the sinv load up front as well
         if (hit) {
-            key[i] = make_key(d2, (uint32_t)key_idx(k[e]));
+            key[i] = make_key(d2, __float_as_uint(t[e].w));
             if (corr) write_corr_t(w, a, p, i, v[e].x, v[e].y, v[e].z, d2, t[e]);
             ++hits;
         } else if (valid) {
@@ -774,8 +779,8 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     misses = wave_sum(misses);
     if (lane == 0) wmiss[wave] = misses;
     if (lane == 0) {
-        atomicAdd(w.evals, (unsigned long long)hits);
-        atomicAdd(w.evals + 2, (unsigned long long)hits);
+        count_add(w.evals, 0, (unsigned long long)hits);
+        count_add(w.evals, 2, (unsigned long long)hits);
     }
     __syncthreads();
     uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
@@ -1082,16 +1087,21 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) {
                 if (orig[q] < 0) continue;
                 const NNKey kb = bestl[q * 64 + lane];
+                const float4 t = tgt[key_idx(kb)];
                 key[orig[q]] = kb;
-                if (CACHE) w.nn_lb[(int64_t)p * w.x_stride + orig[q]] = lb_from_sec(__uint_as_float(secl[q * 64 + lane]));
-                if (corr) write_corr(w, a, p, orig[q], x[q], y[q], z[q], kb, tgt);
+                if (CACHE) {
+                    const int64_t slot = (int64_t)p * w.x_stride + orig[q];
+                    w.nn_lb[slot] = lb_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                    w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(kb)));
+                }
+                if (corr) write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
             }
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
     }
     if (lane == 0) {
-        atomicAdd(w.evals, evals);
-        atomicAdd(w.evals + 1, tests);
+        count_add(w.evals, 0, evals);
+        count_add(w.evals, 1, tests);
     }
 }
 
@@ -1624,7 +1634,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
                          int ncu, hipStream_t st) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
     const bool cache = w.nn_lb != nullptr;
-    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt))
+    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
     if (cache && !first) {
