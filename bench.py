@@ -143,9 +143,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    nn_ms, nn_launches = ctx.kernel_time_ms()
+    nn_ms, nn_launches = ctx.kernel_time_ms()  # the dominant kernel: the batched search
+    test_ms, test_launches = ctx.stage_time_ms(icp4r.STAGE_NN_TEST)
+    upd_ms, upd_launches = ctx.stage_time_ms(icp4r.STAGE_UPDATE)
     batch_ms, _ = ctx.batch_time_ms()
-    evals, tests = ctx.nn_counters()  # work the NN kernels performed in the timed steps
+    st = ctx.nn_stats()  # work the NN kernels performed in the timed steps
+    evals, tests = st["evaluations"], st["box_tests"]
     plan = icp4r.plan(P, n, n)
     kernel = "nn_lds_kernel" if plan["lds"] else "nn_pruned_kernel" if plan["pruned"] else "nn_kernel"
 
@@ -175,7 +178,8 @@ def main():
 
     total_pairs = world * P * args.steps
     value = total_pairs / elapsed
-    evals_per_launch = evals / max(nn_launches, 1)
+    # the search kernel's own work: every evaluation except the test kernel's one per hit
+    evals_per_launch = (evals - st["cache_hits"]) / max(nn_launches, 1)
     tests_per_launch = tests / max(nn_launches, 1)
     flops_per_launch = evals_per_launch * FLOP_PER_PAIR_EVAL + tests_per_launch * FLOP_PER_BOX_TEST
     achieved_tflops = flops_per_launch / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
@@ -190,6 +194,18 @@ def main():
                 traffic = pmc.get("hbm_bytes_per_nn_launch")
         except (OSError, ValueError):
             traffic = None
+
+    # cached-neighbour test kernel (HBM-bound): algorithmic bytes = per tested query X (16) + nn_t
+    # (16) + L (4) + sinv (4) read; per hit its key (8) written, + its correspondence record (32)
+    # in the iteration passes
+    cache_test = None
+    if test_launches:
+        tb = (st["cache_tested"] * 40 + st["cache_hits"] * 8 + st["records_written_by_test"] * 32) / test_launches
+        cache_test = {"kernel": "nn_cache_test_kernel", "bound": "hbm", "avg_launch_ms": test_ms,
+                      "launches": test_launches, "bytes_per_launch": tb,
+                      "achieved": tb / (test_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                      "frac": tb / (test_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                      "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1)}
 
     if rank == 0:
         cpu = None
@@ -234,13 +250,16 @@ def main():
                 "brute_force_equivalent_tflops": brute_equiv_tflops,
                 "avg_launch_ms": nn_ms,
                 "launches": nn_launches,
-                "note": "FP32 VALU work of the exact pruned search, counted on the device: distance evaluations "
+                "note": "FP32 VALU work of the exact pruned search kernel (nn_lds_kernel: the queries the "
+                        "cached-neighbour test could not resolve), counted on the device: distance evaluations "
                         "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add); "
                         "compare/select/ballot/LDS not counted. achieved = that / avg launch time (HIP events on "
-                        "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). The search evaluates "
-                        "~1% of the n*m pairs, so brute_force_equivalent_tflops (n*m*8 / time) exceeds the peak; "
-                        "the kernel is issue/latency-bound (VALU + LDS at 4 waves/SIMD), see DESIGN.md",
+                        "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). brute_force_equivalent_"
+                        "tflops = n*m*8 per NN pass / search time. The search is latency-bound (4 waves/SIMD, "
+                        "LDS-limited), see DESIGN.md",
             },
+            "cache_test_kernel": cache_test,
+            "update_kernel": {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches},
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
             "batch_device_ms": batch_ms,

@@ -68,15 +68,16 @@ namespace {
 constexpr size_t kCountBytes = (size_t)kCountSlots * kCountStride * sizeof(uint64_t);
 
 // Sum the per-slot work counters (evaluations, box tests, cache hits) since the last reset.
-int read_counters(icp4r_ctx* ctx, uint64_t (&out)[3]) {
-    out[0] = out[1] = out[2] = 0;
+constexpr int kNumCounters = 5;
+int read_counters(icp4r_ctx* ctx, uint64_t (&out)[kNumCounters]) {
+    for (int k = 0; k < kNumCounters; ++k) out[k] = 0;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
     if (!ctx->evals.p) return ICP4R_OK;
     std::vector<uint64_t> v((size_t)kCountSlots * kCountStride);
     HIP_TRY(hipMemcpy(v.data(), ctx->evals.p, kCountBytes, hipMemcpyDeviceToHost));
     for (int s = 0; s < kCountSlots; ++s)
-        for (int k = 0; k < 3; ++k) out[k] += v[(size_t)s * kCountStride + k];
+        for (int k = 0; k < kNumCounters; ++k) out[k] += v[(size_t)s * kCountStride + k];
     return ICP4R_OK;
 }
 
@@ -268,16 +269,28 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     return ICP4R_OK;
 }
 
-// One NN pass over every active pair (timed with events: the roofline's kernel).
+// One NN pass over every active pair, timed with events: the roofline's kernel is the batched
+// search (nn_lds_kernel) or, for the other plans, the NN launch itself.
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
             int fitness_pass, int first, hipStream_t st) {
     EventPair* ne;
     int r;
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
-    HIP_TRY(hipEventRecord(ne->start, st));
     if (pl.lds) {
-        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ctx->ncu, st));
-    } else if (pl.pruned) {
+        NNLdsEvents ev;
+        ev.search_start = ne->start;
+        ev.search_stop = ne->stop;
+        if (pl.cache && !first) {
+            EventPair* te;
+            if ((r = next_event(ctx->test_events, ctx->test_used, &te))) return r;
+            ev.test_start = te->start;
+            ev.test_stop = te->stop;
+        }
+        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ctx->ncu, st, ev));
+        return ICP4R_OK;
+    }
+    HIP_TRY(hipEventRecord(ne->start, st));
+    if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));
@@ -306,7 +319,11 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     const int iters = max_iterations > 0 ? max_iterations : 1;
     for (int it = 0; it < iters; ++it) {
         if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
+        EventPair* ue;
+        if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
+        HIP_TRY(hipEventRecord(ue->start, st));
         HIP_TRY(launch_update(a, w, npairs, mn, pcl && !pl.pruned, st));
+        HIP_TRY(hipEventRecord(ue->stop, st));
     }
     if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
     if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, a, w, npairs, mn, 1, 0, st))) return rc;
@@ -440,7 +457,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lb, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n})
         b->release();
-    for (auto* v : {&ctx->nn_events, &ctx->batch_events})
+    for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events})
         for (auto& ev : *v) {
             (void)hipEventDestroy(ev.start);
             (void)hipEventDestroy(ev.stop);
@@ -671,9 +688,28 @@ int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls) {
     return rc;
 }
 
+int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* launches) {
+    if (!ctx || !avg_ms) return fail(ICP4R_E_INVALID, "NULL argument");
+    std::vector<EventPair>* v;
+    size_t used;
+    switch (stage) {
+        case ICP4R_STAGE_NN: v = &ctx->nn_events; used = ctx->nn_used; break;
+        case ICP4R_STAGE_NN_TEST: v = &ctx->test_events; used = ctx->test_used; break;
+        case ICP4R_STAGE_UPDATE: v = &ctx->upd_events; used = ctx->upd_used; break;
+        case ICP4R_STAGE_BATCH: v = &ctx->batch_events; used = ctx->batch_used; break;
+        default: return fail(ICP4R_E_INVALID, "unknown stage %d", stage);
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = events_avg(*v, used, avg_ms);
+    if (launches) *launches = (int32_t)used;
+    return rc;
+}
+
 int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
     ctx->nn_used = 0;
+    ctx->test_used = 0;
+    ctx->upd_used = 0;
     ctx->batch_used = 0;
     if (ctx->evals.p) {
         HIP_TRY(hipSetDevice(ctx->device));
@@ -699,7 +735,7 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
 
 int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests) {
     if (!ctx || !evaluations) return fail(ICP4R_E_INVALID, "NULL argument");
-    uint64_t v[3];
+    uint64_t v[kNumCounters];
     int rc = read_counters(ctx, v);
     if (rc) return rc;
     *evaluations = v[0];
@@ -709,10 +745,24 @@ int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests
 
 int icp4r_nn_cache_hits(icp4r_ctx* ctx, uint64_t* hits) {
     if (!ctx || !hits) return fail(ICP4R_E_INVALID, "NULL argument");
-    uint64_t v[3];
+    uint64_t v[kNumCounters];
     int rc = read_counters(ctx, v);
     if (rc) return rc;
     *hits = v[2];
+    return ICP4R_OK;
+}
+
+int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out) {
+    if (!ctx || !out) return fail(ICP4R_E_INVALID, "NULL argument");
+    uint64_t v[kNumCounters];
+    int rc = read_counters(ctx, v);
+    if (rc) return rc;
+    memset(out, 0, sizeof(*out));
+    out->evaluations = v[0];
+    out->box_tests = v[1];
+    out->cache_hits = v[2];
+    out->cache_tested = v[3];
+    out->records_written_by_test = v[4];
     return ICP4R_OK;
 }
 

@@ -67,7 +67,9 @@ struct icp4r_ctx {
     icp4r_host::DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks, nn_lb, nn_t, sinv, qlist, need,
         miss_cnt, plist, plist_n;
     int ncu = 256;  // compute units of the device (persistent launches)
-    std::vector<icp4r_host::EventPair> nn_events, batch_events;
-    size_t nn_used = 0, batch_used = 0;
+    // HIP events on the launch stream: the dominant NN kernel (the batched search, or the whole NN
+    // launch of the other plans), the cache-test kernel, the update kernel, whole registrations
+    std::vector<icp4r_host::EventPair> nn_events, test_events, upd_events, batch_events;
+    size_t nn_used = 0, test_used = 0, upd_used = 0, batch_used = 0;
     icp4r_host::DevBuf evals;  // u64[4]: NN distance evaluations, box tests, cached-neighbour hits since the last reset
 };

@@ -133,8 +133,12 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
                             int first, hipStream_t st);
+// events recorded around the batched NN's stages (any may be null)
+struct NNLdsEvents {
+    hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;
+};
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st);
+                         int ncu, hipStream_t st, const NNLdsEvents& ev);
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,

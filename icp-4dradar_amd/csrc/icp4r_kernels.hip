@@ -781,6 +781,8 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     if (lane == 0) {
         count_add(w.evals, 0, (unsigned long long)hits);
         count_add(w.evals, 2, (unsigned long long)hits);
+        count_add(w.evals, 3, (unsigned long long)(hits + misses));
+        if (corr) count_add(w.evals, 4, (unsigned long long)hits);
     }
     __syncthreads();
     uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
@@ -1631,23 +1633,28 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 }
 
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st) {
+                         int ncu, hipStream_t st, const NNLdsEvents& ev) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
     const bool cache = w.nn_lb != nullptr;
     if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
+    hipError_t e;
     if (cache && !first) {
         const int chunks = (max_n + kTestWG * kTestPer - 1) / (kTestWG * kTestPer);
+        if (ev.test_start && (e = hipEventRecord(ev.test_start, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(nn_cache_test_kernel, dim3(chunks, npairs), dim3(kTestWG), 0, st, a, w, fitness_pass);
+        if (ev.test_stop && (e = hipEventRecord(ev.test_stop, st)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(nn_order_kernel, dim3(1), dim3(kOrderWG), 0, st, a, w, npairs, fitness_pass,
                        (first || !cache) ? 1 : 0);
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
+    if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
     if (cache)
         hipLaunchKernelGGL(nn_lds_kernel<true>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     else
         hipLaunchKernelGGL(nn_lds_kernel<false>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ library_path = os.path.join(HERE, "_lib", "libicp4r.so")
 OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 NUMERICS_PCL, NUMERICS_F64 = 0, 1
 NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED, NN_PRUNED = 0, 1, 2, 3
+STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH = 0, 1, 2, 3
 DBL_MAX = sys.float_info.max
 
 _STATUS = {OK: "ICP4R_OK", E_INVALID: "ICP4R_E_INVALID", E_EMPTY: "ICP4R_E_EMPTY",
@@ -43,7 +44,8 @@ EXPORTED_SYMBOLS = [
     "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
-    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits",
+    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits", "icp4r_stage_time_ms",
+    "icp4r_nn_stats",
 ]
 # include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
 MAP_EXPORTED_SYMBOLS = [
@@ -152,6 +154,8 @@ def load():
         "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
         "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "icp4r_nn_cache_hits": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+        "icp4r_stage_time_ms": (C.c_int, [vp, i32, C.POINTER(C.c_double), C.POINTER(i32)]),
+        "icp4r_nn_stats": (C.c_int, [vp, C.POINTER(C.c_uint64 * 8)]),
         # icp4r_map.h
         "icp4r_map_create": (C.c_int, [vp, C.POINTER(vp)]),
         "icp4r_map_destroy": (C.c_int, [vp]),
@@ -292,6 +296,12 @@ class Context:
         _check(self._lib.icp4r_batch_time_ms(self._h, C.byref(ms), C.byref(k)), "icp4r_batch_time_ms")
         return ms.value, k.value
 
+    def stage_time_ms(self, stage: int) -> tuple[float, int]:
+        """(average ms, launches) of a stage (STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH)."""
+        ms, k = C.c_double(), C.c_int32()
+        _check(self._lib.icp4r_stage_time_ms(self._h, stage, C.byref(ms), C.byref(k)), "icp4r_stage_time_ms")
+        return ms.value, k.value
+
     def reset_timers(self):
         _check(self._lib.icp4r_kernel_time_reset(self._h), "icp4r_kernel_time_reset")
 
@@ -300,6 +310,13 @@ class Context:
         v, t = C.c_uint64(), C.c_uint64()
         _check(self._lib.icp4r_nn_counters(self._h, C.byref(v), C.byref(t)), "icp4r_nn_counters")
         return v.value, t.value
+
+    def nn_stats(self) -> dict:
+        """Every NN work counter since the last reset_timers() (icp4r_nn_stats_t)."""
+        v = (C.c_uint64 * 8)()
+        _check(self._lib.icp4r_nn_stats(self._h, C.byref(v)), "icp4r_nn_stats")
+        keys = ("evaluations", "box_tests", "cache_hits", "cache_tested", "records_written_by_test")
+        return {k: int(v[i]) for i, k in enumerate(keys)}
 
     def nn_cache_hits(self) -> int:
         """Queries the cached-neighbour test resolved without a search since the last reset_timers()."""

@@ -159,12 +159,26 @@ int icp4r_nearest(icp4r_ctx* ctx, const float* query, int32_t n, int32_t query_s
 int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream);
 
 /* Device-time accounting with HIP events on the launch stream (used by bench.py for the roofline):
- * icp4r_kernel_time_ms: average duration of the NN-sweep kernel launches (the dominant kernel)
+ * icp4r_kernel_time_ms: average duration of the NN kernel launches (the dominant kernel: the batched
+ *                       search nn_lds_kernel, or the whole NN launch of the other plans)
  *                       recorded since the last reset, and how many there were;
  * icp4r_batch_time_ms:  average duration of whole registration calls (all launches of a batch). */
 int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
 int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);
 int icp4r_kernel_time_reset(icp4r_ctx* ctx);
+
+/* Average device time of one stage of the registrations since the last reset (HIP events on the
+ * launch stream), and how many launches it averages.  ICP4R_STAGE_NN is what icp4r_kernel_time_ms
+ * reports: the batched search kernel (nn_lds_kernel) of the LDS plan, the whole NN launch of the
+ * others; ICP4R_STAGE_NN_TEST the cached-neighbour test kernel; ICP4R_STAGE_UPDATE the Umeyama /
+ * convergence update; ICP4R_STAGE_BATCH a whole registration call. */
+typedef enum icp4r_stage {
+    ICP4R_STAGE_NN = 0,
+    ICP4R_STAGE_NN_TEST = 1,
+    ICP4R_STAGE_UPDATE = 2,
+    ICP4R_STAGE_BATCH = 3
+} icp4r_stage;
+int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* launches);
 
 /* Work the NN kernels performed since the last icp4r_kernel_time_reset — the algorithmic work
  * behind the roofline's `achieved`: distance evaluations (query x target; brute force exactly n*m
@@ -176,6 +190,17 @@ int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests
  * (icp4r_plan_info.cache) since the last icp4r_kernel_time_reset; each counts as one evaluation
  * in icp4r_nn_counters.  Synchronises the context's device. */
 int icp4r_nn_cache_hits(icp4r_ctx* ctx, uint64_t* hits);
+
+/* All NN work counters since the last icp4r_kernel_time_reset (synchronises the device). */
+typedef struct icp4r_nn_stats_t {
+    uint64_t evaluations;             /* distance evaluations (a cache hit counts one)          */
+    uint64_t box_tests;               /* point-to-box lower-bound tests of the pruned searches  */
+    uint64_t cache_hits;              /* queries the cached-neighbour test resolved             */
+    uint64_t cache_tested;            /* queries the cached-neighbour test examined             */
+    uint64_t records_written_by_test; /* correspondence records the test kernel wrote (32 B)    */
+    uint64_t reserved[3];
+} icp4r_nn_stats_t;
+int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out);
 
 /* Launch geometry the batch path picks for a shape — exposed for tests and the benchmark report. */
 typedef struct icp4r_plan_info {

@@ -62,23 +62,20 @@ def main():
     if a.fetch:
         fs = counters(a.fetch, "FETCH_SIZE", a.kernel)
         if fs:
-            kib = statistics.median(fs)
-            out["fetch_size_kib_median"] = kib
+            kib = statistics.fmean(fs)  # launches differ per ICP pass: the mean matches the avg launch time
+            out["fetch_size_kib_mean"] = kib
             out["fetch_bytes_corrected"] = 2.0 * kib * 1024
             out["fetch_dispatches"] = len(fs)
     if a.write:
         ws = counters(a.write, "WRITE_SIZE", a.kernel)
         if ws:
-            kib = statistics.median(ws)
-            out["write_size_kib_median"] = kib
+            kib = statistics.fmean(ws)
+            out["write_size_kib_mean"] = kib
             out["write_bytes"] = kib * 1024
             out["write_dispatches"] = len(ws)
     if "fetch_bytes_corrected" in out and "write_bytes" in out:
         out["hbm_bytes_per_nn_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
-        n, P = a.points, a.pairs
-        # per query: X 16 B + permutation 4 B + previous key 8 B + key write 8 B + matched target 16 B +
-        # correspondence record write 32 B; per pair: the sorted target set 16 B/pt + boxes (staged once)
-        out["algorithmic_bytes_per_nn_launch"] = P * (n * (16 + 4 + 8 + 8 + 16 + 32) + n * 16 + (n // 16) * 36)
+
     if a.fetch or a.write:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)
