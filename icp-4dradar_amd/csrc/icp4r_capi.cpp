@@ -220,7 +220,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         }
         w.ticks = static_cast<uint64_t*>(ctx->ticks.p);
     }
-    if (corr) {
+    if (corr && !pl.cache) {  // with the cached-neighbour test the update reads X and nn_t instead
         HIP_TRY(ctx->corr.ensure((size_t)slots * 2 * sizeof(float4)));
         w.corr = static_cast<float4*>(ctx->corr.p);
     }
@@ -249,14 +249,15 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         }
         if (pl.cache) {
             w.need_stride = (x_stride + 31) / 32;
-            HIP_TRY(ctx->nn_lb.ensure((size_t)slots * sizeof(float)));
+            HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float2)));
             HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
             w.nn_t = static_cast<float4*>(ctx->nn_t.p);
             HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
             HIP_TRY(ctx->miss_cnt.ensure((size_t)npairs * sizeof(int32_t)));
-            w.nn_lb = static_cast<float*>(ctx->nn_lb.p);
+            w.nn_lu = static_cast<float2*>(ctx->nn_lu.p);
+            w.defer_xform = 1;
             w.sinv = static_cast<int32_t*>(ctx->sinv.p);
             w.qlist = static_cast<int32_t*>(ctx->qlist.p);
             w.need = static_cast<uint32_t*>(ctx->need.p);
@@ -454,7 +455,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lb, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events})

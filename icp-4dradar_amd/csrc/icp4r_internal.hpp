@@ -109,8 +109,10 @@ struct WorkArgs {
     int64_t t_stride, b_stride, sb_stride;
     float4* corr;       // PCL numerics: [npairs * x_stride * 2] per source point {s.xyz, w}, {d.xyz, d²}
     // Cached-neighbour test (nn_lds_kernel<true>; nullptr = off):
-    float* nn_lb;       // [npairs * x_stride] L_i: lower bound on |X_i - t_k| for every target k other
-                        // than the current NN; set by a search, lowered by every kernel that moves X_i
+    float2* nn_lu;      // [npairs * x_stride] (L_i, U_i): L a lower bound on |X_i - t_k| for every
+                        // target k other than the NN, U an upper bound of the second-nearest distance;
+                        // set by a search, widened by every kernel that moves X_i
+    int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index (bits)
     int32_t* sinv;      // [npairs * x_stride] source index -> Morton position (inverse of sperm)
     int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)

@@ -694,15 +694,21 @@ struct LdsNN {
     int32_t cur;                                       // the pair this workgroup works on
 };
 
-// L_i from the second-smallest d² a search saw: every other target has float d² >= sec, and the
-// true distance is >= sqrt(d²)(1 - 3u); rounded down by 1e-6 (>> the sqrt's own rounding).
-__device__ __forceinline__ float lb_from_sec(float sec_d2) { return sqrtf(sec_d2) * 0.999999f; }
+// Bounds on the second-nearest distance of X_i (float2 nn_lu[i]):
+//  L (.x): lower bound on |X_i - t_k| for every target k other than the NN — the cache test's;
+//  U (.y): upper bound on the second-nearest distance — the next search's initial pruning bound.
+// From the second-smallest d² a search saw (every other target has float d² >= sec; the true
+// distance is within sqrt(d²)(1 -/+ 3u)), rounded outwards by 1e-6 (>> the sqrt's own rounding).
+__device__ __forceinline__ float2 lu_from_sec(float sec_d2) {
+    const float r = sqrtf(sec_d2);
+    return make_float2(r * 0.999999f, r * 1.000001f);
+}
 
-// L_i after X_i moved from o to v (float points): L - |v - o|, both roundings covered.
-__device__ __forceinline__ float move_lb(float L, float ox, float oy, float oz, float vx, float vy, float vz) {
+// The bounds after X_i moved from o to v (float points): L - |v - o|, U + |v - o|, roundings covered.
+__device__ __forceinline__ float2 move_lu(float2 lu, float ox, float oy, float oz, float vx, float vy, float vz) {
     const float dx = vx - ox, dy = vy - oy, dz = vz - oz;
-    const float d = sqrtf(dx * dx + dy * dy + dz * dz);
-    return fmaxf((L - d * 1.00001f) * 0.999999f, 0.0f);
+    const float d = sqrtf(dx * dx + dy * dy + dz * dz) * 1.00001f;
+    return make_float2(fmaxf((lu.x - d) * 0.999999f, 0.0f), (lu.y + d) * 1.000001f);
 }
 
 __device__ __forceinline__ bool cache_hit(float L, float dj2) {
@@ -739,23 +745,28 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     const int nwords = (n + 31) >> 5;
     for (int k = tid; k < nwords; k += kTestWG) need[k] = 0;
     __syncthreads();
-    const float4* X = w.X + (int64_t)p * w.x_stride;
+    float4* X = w.X + (int64_t)p * w.x_stride;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
-    const float* lb = w.nn_lb + (int64_t)p * w.x_stride;
+    float2* lu = w.nn_lu + (int64_t)p * w.x_stride;
     const float4* nt = w.nn_t + (int64_t)p * w.x_stride;
     const int32_t* sinv = w.sinv + (int64_t)p * w.x_stride;
-    const bool corr = w.corr != nullptr && !fitness_pass;
+    // In the iteration passes the previous update's transformCloud(T_inc) is applied here (the
+    // update defers it: X_i is read and written once per iteration, and the bounds move with it).
+    const bool xform = !fitness_pass;
+    float T[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) T[q] = xform ? uload(&w.state[p].T_inc[q]) : 0.0f;
     // Every load is coalesced (the NN's coordinates come from nn_t, not a gather from the target
     // cloud) and issued before the first store (a load after a store waits behind it on vmcnt).
     float4 v[kTestPer], t[kTestPer];
-    float L[kTestPer];
+    float2 L[kTestPer];
     int32_t sp[kTestPer];
 #pragma unroll
     for (int e = 0; e < kTestPer; ++e) {
         const int i = min(i0 + e * kTestWG + tid, n - 1);
         v[e] = X[i];
         t[e] = nt[i];
-        L[e] = lb[i];
+        L[e] = lu[i];
         sp[e] = sinv[i];
     }
     int hits = 0, misses = 0;
@@ -763,12 +774,21 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     for (int e = 0; e < kTestPer; ++e) {
         const int i = i0 + e * kTestWG + tid;
         const bool valid = i < n;
+        if (xform) {
+            float4 o = v[e];
+            xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
+            L[e] = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            v[e] = o;
+            if (valid) {
+                X[i] = o;
+                lu[i] = L[e];
+            }
+        }
         const float d2 = l2_simple(v[e].x, v[e].y, v[e].z, t[e].x, t[e].y, t[e].z);
-        const bool hit = valid & cache_hit(L[e], d2);  // '&': a conditional use would sink the lb load
-        asm volatile("" ::"v"(sp[e]));                  // ... and keep the sinv load up front as well
+        const bool hit = valid & cache_hit(L[e].x, d2);  // '&': a conditional use would sink the load
+        asm volatile("" ::"v"(sp[e]));                    // ... and keep the sinv load up front as well
         if (hit) {
             key[i] = make_key(d2, __float_as_uint(t[e].w));
-            if (corr) write_corr_t(w, a, p, i, v[e].x, v[e].y, v[e].z, d2, t[e]);
             ++hits;
         } else if (valid) {
             atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
@@ -782,7 +802,6 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
         count_add(w.evals, 0, (unsigned long long)hits);
         count_add(w.evals, 2, (unsigned long long)hits);
         count_add(w.evals, 3, (unsigned long long)(hits + misses));
-        if (corr) count_add(w.evals, 4, (unsigned long long)hits);
     }
     __syncthreads();
     uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
@@ -945,9 +964,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         k2 = make_key(l2_simple(x[q], y[q], z[q], tn.x, tn.y, tn.z), __float_as_uint(tn.w));
                     }
                     const NNKey lo = kj < k2 ? kj : k2, hi = kj < k2 ? k2 : kj;
+                    // U of the previous search, moved since: an upper bound of the second-nearest
+                    // distance even if no evaluated target attains it (first pass: none)
+                    uint32_t sec0 = (uint32_t)(hi >> 32);
+                    if (!first) {
+                        const float u = w.nn_lu[(int64_t)p * w.x_stride + o].y;
+                        sec0 = min(sec0, __float_as_uint(u * u * 1.00001f));
+                    }
                     bestl[q * 64 + lane] = lo;
-                    secl[q * 64 + lane] = (uint32_t)(hi >> 32);
-                    bnd[q] = orig[q] >= 0 ? key_d2(hi) : -1.0f;
+                    secl[q * 64 + lane] = sec0;
+                    bnd[q] = orig[q] >= 0 ? __uint_as_float(sec0) : -1.0f;
                 } else {
                     bestl[q * 64 + lane] = kj;
                     bnd[q] = orig[q] >= 0 ? key_d2(kj) : -1.0f;
@@ -1091,12 +1117,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const NNKey kb = bestl[q * 64 + lane];
                 const float4 t = tgt[key_idx(kb)];
                 key[orig[q]] = kb;
-                if (CACHE) {
+                if (CACHE) {  // the update reads X, nn_t and the key: no correspondence record
                     const int64_t slot = (int64_t)p * w.x_stride + orig[q];
-                    w.nn_lb[slot] = lb_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                    w.nn_lu[slot] = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
                     w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(kb)));
+                } else if (corr) {
+                    write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
                 }
-                if (corr) write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
             }
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
@@ -1253,18 +1280,16 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
 }
 
 // transformCloud(*input_transformed, *input_transformed, transformation_) by the whole workgroup.
-// With the cached-neighbour test on (lb != nullptr) every moved point also lowers its bound L_i.
+// (With the cached-neighbour test the update defers this to the next pass's test kernel.)
 template <int WG>
-__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds, float* lb) {
+__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds) {
     float Tl[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) Tl[k] = T_lds[k];
     for (int i = threadIdx.x; i < n; i += WG) {
-        const float4 s = X[i];
-        float4 o = s;
-        xform_pt(Tl, s.x, s.y, s.z, o.x, o.y, o.z);
-        X[i] = o;
-        if (lb) lb[i] = move_lb(lb[i], s.x, s.y, s.z, o.x, o.y, o.z);
+        float4 s = X[i];
+        xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
+        X[i] = s;
     }
 }
 
@@ -1301,9 +1326,31 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = a.src_n[p];
     const int64_t xs = w.x_stride;
-    const float4* C = w.corr + (int64_t)p * xs * 2;
     const KParams& kp = a.kp;
     const bool weighted = kp.huber_delta < INFINITY;
+    // The correspondence of source point i: {s.xyz, w}, {d.xyz, d²} — the NN kernels' records, or,
+    // with the cached-neighbour test (no records), X_i (the searched point: the transform is
+    // deferred), its NN's coordinates nn_t[i] and d² = l2_simple(X_i, t) — the very expression the
+    // NN computed its key with, so the same bits.
+    const float4* C = w.corr ? w.corr + (int64_t)p * xs * 2 : nullptr;
+    const float4* Xp = w.X + (int64_t)p * xs;
+    const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
+    auto rec = [&](int i, float4& r0, float4& r1) {
+        if (C) {
+            r0 = C[2 * i];
+            r1 = C[2 * i + 1];
+        } else {
+            r0 = Xp[i];
+            r1 = NT[i];
+        }
+    };
+    auto rec_fix = [&](float4& r0, float4& r1) {
+        if (!C) {
+            const float d2 = l2_simple(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z);
+            r0.w = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
+            r1.w = d2;
+        }
+    };
     const bool mse = kp.need_mse != 0;  // wave 1 runs the MSE chain in pass A, else it fills
     const float ident = weighted ? 0.0f : -0.0f;
     const int nch = (n + kFoldChunkP - 1) / kFoldChunkP;
@@ -1323,13 +1370,13 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int i = base + min(tid - fill0 + e * nf, len - 1);
-            r[e][0] = C[2 * i];
-            r[e][1] = C[2 * i + 1];
+            rec(i, r[e][0], r[e][1]);
         }
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int o = tid - fill0 + e * nf;
             if (o >= len) break;
+            rec_fix(r[e][0], r[e][1]);
             const float d2 = r[e][1].w;
             const float sv[6] = {r[e][0].x, r[e][0].y, r[e][0].z, r[e][1].x, r[e][1].y, r[e][1].z};
             float v[6], wt = 0.0f, dd = 0.0f;
@@ -1392,13 +1439,13 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int i = base + min(tid - 64 + e * kFillB, len - 1);
-            r[e][0] = C[2 * i];
-            r[e][1] = C[2 * i + 1];
+            rec(i, r[e][0], r[e][1]);
         }
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int o = tid - 64 + e * kFillB;
             if (o >= len) break;
+            rec_fix(r[e][0], r[e][1]);
             float sv[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f}, wt = 0.f;
             if (!(r[e][1].w > kp.max_d2)) {
                 sv[0] = r[e][0].x - ms[0];
@@ -1432,7 +1479,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
     if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
-    transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc, w.nn_lb ? w.nn_lb + (int64_t)p * xs : nullptr);
+    if (!w.defer_xform) transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
     __syncthreads();
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
 }
@@ -1484,7 +1531,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
     if (tid == 0) solve_pair<kNumericsF64>(sh, st, kp);
     __syncthreads();
     if (sh.flag == 1) return;
-    transform_pair<kUpdWG>(X, n, sh.T_inc, w.nn_lb ? w.nn_lb + (int64_t)p * w.x_stride : nullptr);
+    if (!w.defer_xform) transform_pair<kUpdWG>(X, n, sh.T_inc);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1499,14 +1546,14 @@ __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs 
     const int n = a.src_n[p];
     const float4* src = a.src + a.src_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
-    float* lb = w.nn_lb ? w.nn_lb + (int64_t)p * w.x_stride : nullptr;
+    float2* lu = w.nn_lu ? w.nn_lu + (int64_t)p * w.x_stride : nullptr;
     for (int i = threadIdx.x; i < n; i += 256) {
         const float4 s = src[i];
         float4 o = s;
         xform_pt(Tf, s.x, s.y, s.z, o.x, o.y, o.z);
-        if (lb) {
+        if (lu) {  // X still holds the last NN pass's points (a deferred transform never ran)
             const float4 old = X[i];
-            lb[i] = move_lb(lb[i], old.x, old.y, old.z, o.x, o.y, o.z);
+            lu[i] = move_lu(lu[i], old.x, old.y, old.z, o.x, o.y, o.z);
         }
         X[i] = o;
     }
@@ -1635,8 +1682,9 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
                          int ncu, hipStream_t st, const NNLdsEvents& ev) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
-    const bool cache = w.nn_lb != nullptr;
-    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t))
+    const bool cache = w.nn_lu != nullptr;
+    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t ||
+                  !w.defer_xform))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
     hipError_t e;
