@@ -456,7 +456,8 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
-                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n})
+                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
+                      &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events})
         for (auto& ev : *v) {

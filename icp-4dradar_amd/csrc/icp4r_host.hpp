@@ -71,5 +71,7 @@ struct icp4r_ctx {
     // launch of the other plans), the cache-test kernel, the update kernel, whole registrations
     std::vector<icp4r_host::EventPair> nn_events, test_events, upd_events, batch_events;
     size_t nn_used = 0, test_used = 0, upd_used = 0, batch_used = 0;
-    icp4r_host::DevBuf evals;  // u64[4]: NN distance evaluations, box tests, cached-neighbour hits since the last reset
+    icp4r_host::DevBuf evals;  // per-wave counter slots (kCountSlots x kCountStride u64), summed by the host
+    // radar ego velocity (icp4r_ego.cpp): staging and workspace
+    icp4r_host::DevBuf ego_rec, ego_off, ego_cnt, ego_feat, ego_pd, ego_scores, ego_res, ego_mask, ego_xyzi;
 };

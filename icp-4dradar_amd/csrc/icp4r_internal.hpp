@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "icp4r/icp4r.h"
+#include "icp4r/icp4r_ego.h"
 #include "icp4r_math.hpp"
 
 namespace icp4r {
@@ -163,5 +164,24 @@ hipError_t launch_associate(const float4* in, int64_t n, const Mat3x4d& M, float
 int64_t sector_blocks(int64_t n);
 hipError_t launch_sector(const float4* map, int64_t n, const SectorArgs& a, int32_t* counts, int32_t* offsets,
                          int32_t* total, float4* out, hipStream_t st);
+
+// ---- radar ego velocity (icp4r_ego.hip)
+struct EgoArgs {
+    const float* rec;      // device records, 5 floats each
+    const int64_t* off;    // [nscans] first record of scan s
+    const int32_t* cnt;    // [nscans]
+    int64_t stride;        // workspace points per scan (>= max cnt)
+    float4* feat;          // [nscans * stride] distance, arfa, beta, v_r
+    double4* pd;           // [nscans * stride] cos(DEG2RAD(beta)) v_r, cos / sin / DEG2RAD of arfa
+    int32_t* scores;       // [nscans * max_h] inlier counts
+    int32_t max_h;         // hypotheses of the largest scan
+    int32_t iterations;    // icp4r_ego_params.iterations (<= 0: (int)(0.2 n) per scan)
+    double sigma, dyn;
+    uint64_t seed;
+    uint8_t* mask;         // optional: static flag per record
+    icp4r_ego_result* results;
+};
+hipError_t launch_ego(const EgoArgs& e, int nscans, int max_n, float4* xyzi, hipStream_t st);
+hipError_t launch_ego_features(const EgoArgs& e, int nscans, int max_n, float4* xyzi, hipStream_t st);
 
 }  // namespace icp4r

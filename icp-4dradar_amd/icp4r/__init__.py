@@ -47,6 +47,10 @@ EXPORTED_SYMBOLS = [
     "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits", "icp4r_stage_time_ms",
     "icp4r_nn_stats",
 ]
+# include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
+EGO_EXPORTED_SYMBOLS = [
+    "icp4r_ego_params_default", "icp4r_radar_features", "icp4r_ego_velocity", "icp4r_ego_velocity_batch_device",
+]
 # include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
 MAP_EXPORTED_SYMBOLS = [
     "icp4r_map_create", "icp4r_map_destroy", "icp4r_map_build", "icp4r_map_add_points", "icp4r_map_add_scan",

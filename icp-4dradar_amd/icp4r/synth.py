@@ -51,9 +51,9 @@ def _rot_zyx(yaw: float, pitch: float, roll: float) -> np.ndarray:
     return Rz @ Ry @ Rx
 
 
-def _sensor_points(rng: np.random.Generator, n: int, structured: bool) -> np.ndarray:
+def _sensor_points(rng: np.random.Generator, n: int, structured: bool, el_deg: float = 15.0) -> np.ndarray:
     az = np.deg2rad(rng.uniform(-60.0, 60.0, n))
-    el = np.deg2rad(rng.uniform(-15.0, 15.0, n))
+    el = np.deg2rad(rng.uniform(-el_deg, el_deg, n))
     r = rng.uniform(2.0, 80.0, n)
     if structured:
         kind = rng.random(n)
@@ -133,6 +133,48 @@ def make_map_pair(index: int = 0, n_src: int = 8192, scans: int = 10, pts_per_sc
         return rec
 
     return ScanPair(src=records(src_xyz), tgt=records(map_xyz), T_gt=T)
+
+
+def make_sequence(index: int = 0, frames: int = 5, n: int = 2048, speed: float = 5.0, dt: float = 0.1,
+                  yaw_rate_deg: float = 2.0, el_deg: float = 3.0, dynamic: float = 0.1,
+                  doppler_noise: float = 0.02) -> tuple[list[np.ndarray], np.ndarray]:
+    """A radar sequence with Doppler (seed ``9000 + index``): the sensor moves along its own x axis at
+    ``speed`` m/s, turning at ``yaw_rate_deg``/s, through a static structured scene (elevations within
+    ±``el_deg``, where the node's planar sine model fits).  Static points get the radial velocity
+    ``v_r = -û·v_sensor`` (+ N(0, doppler_noise)); a ``dynamic`` fraction moves on its own
+    (``v_r += U(1.5, 5)`` m/s, so the node's ``delta > 0.2`` test flags it).  Returns the per-frame
+    (N, 5) records and the true sensor velocity in the sensor frame — the least squares over the
+    static points recovers ``-v_sensor`` (the node's Vxyz convention, K·V = v_r)."""
+    rng = np.random.default_rng(9000 + index)
+    world = _sensor_points(rng, 3 * n, structured=True, el_deg=el_deg)
+    v_sensor = np.array([speed, 0.0, 0.0])
+    t = np.zeros(3)
+    yaw = 0.0
+    out = []
+    for _ in range(frames):
+        R = _rot_zyx(yaw, 0.0, 0.0)
+        sel = rng.choice(len(world), size=n, replace=False)
+        p = (world[sel] - t) @ R + rng.normal(0.0, 0.02, (n, 3))  # R^T (p - t), row form
+        u = p / np.linalg.norm(p, axis=1, keepdims=True)
+        vr = -(u @ v_sensor) + rng.normal(0.0, doppler_noise, n)
+        dyn = rng.random(n) < dynamic
+        vr[dyn] += rng.uniform(1.5, 5.0, int(dyn.sum()))
+        rec = np.empty((n, RECORD_FLOATS), np.float32)
+        rec[:, :3] = p
+        rec[:, 3] = rng.uniform(0.0, 30.0, n)
+        rec[:, 4] = vr
+        out.append(rec)
+        t = t + R @ v_sensor * dt
+        yaw += np.deg2rad(yaw_rate_deg) * dt
+    return out, v_sensor
+
+
+def write_sequence(folder: str | os.PathLike, frames: list[np.ndarray]) -> None:
+    """The node's input layout (:303-304): ``<folder>/data/radar_pointcloud_<k>.bin``."""
+    d = os.path.join(folder, "data")
+    os.makedirs(d, exist_ok=True)
+    for k, rec in enumerate(frames):
+        write_bin(os.path.join(d, f"radar_pointcloud_{k}.bin"), rec)
 
 
 def write_bin(path: str | os.PathLike, records: np.ndarray) -> None:

@@ -99,6 +99,17 @@ def lib():
                                            C.c_void_p]
         L.oracle_sector_search.restype = C.c_int64
         L.oracle_associate_to_map.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ego_features.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+        L.ego_features.restype = None
+        L.ego_hyp_index.argtypes = [C.c_uint64, C.c_int64, C.c_int32]
+        L.ego_hyp_index.restype = C.c_int32
+        L.ego_fit_sine_ransac.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_double, C.c_uint64,
+                                          C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_void_p,
+                                          C.POINTER(C.c_int32)]
+        L.ego_fit_sine_ransac.restype = C.c_double
+        L.ego_split_lsq.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double, C.c_void_p,
+                                    C.c_void_p]
+        L.ego_split_lsq.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -208,3 +219,40 @@ def associate_to_map(pts: np.ndarray, R: np.ndarray, t: np.ndarray) -> np.ndarra
     out = np.empty_like(p)
     lib().oracle_associate_to_map(p.ctypes.data, len(p), Rd.ctypes.data, td.ctypes.data, out.ctypes.data)
     return out
+
+
+# ---- radar ego velocity (ego_oracle.c)
+EGO_SEED = 0x1CB4D12A5EED  # icp4r_ego_params_default
+
+
+def ego_features(records: np.ndarray) -> np.ndarray:
+    """The node's parse (:373-384): (N, 4) float32 distance, arfa, beta [deg], v_r."""
+    rec = np.ascontiguousarray(records, dtype=np.float32)
+    feat = np.zeros((len(rec), 4), np.float32)
+    if len(rec):
+        lib().ego_features(rec.ctypes.data, len(rec), feat.ctypes.data)
+    return feat
+
+
+def ego_ransac(feat: np.ndarray, iterations: int | None = None, sigma: float = 0.5, seed: int = EGO_SEED):
+    """fitSineRansac (:85-128) with the reproducible hypothesis stream: (A, b, best score, best index,
+    per-hypothesis scores)."""
+    feat = np.ascontiguousarray(feat, dtype=np.float32)
+    n = len(feat)
+    it = int(n * 0.2) if iterations is None or iterations <= 0 else int(iterations)
+    A, b, bh = C.c_double(0.0), C.c_double(0.0), C.c_int32(-1)
+    scores = np.zeros(max(it, 1), np.float64)
+    best = lib().ego_fit_sine_ransac(feat.ctypes.data if n else None, n, it, sigma, seed, C.byref(A), C.byref(b),
+                                     scores.ctypes.data, C.byref(bh))
+    return A.value, b.value, best, bh.value, scores[:it]
+
+
+def ego_split_lsq(feat: np.ndarray, A: float, b: float, dyn_threshold: float = 0.2):
+    """Split + Vxyz (:391-431): (V (3,), static mask (N,) uint8, number of static points)."""
+    feat = np.ascontiguousarray(feat, dtype=np.float32)
+    n = len(feat)
+    mask = np.zeros(n, np.uint8)
+    V = np.zeros(3, np.float64)
+    ns = lib().ego_split_lsq(feat.ctypes.data if n else None, n, A, b, dyn_threshold, mask.ctypes.data if n else None,
+                             V.ctypes.data)
+    return V, mask, ns
