@@ -1,0 +1,291 @@
+// icp4radar_replay.cpp — the icp4radar node's frame loop without ROS.
+//
+// Replays /root/reference/src/iterative_closest_point.cpp:130-820 (USE_BIN_FILES, ICP result mode)
+// over a dataset folder and writes the node's output files:
+//
+//   <dataset>/data/radar_pointcloud_<k>.bin   input, 5-float records (:303-321, read_radar_data :64-82)
+//   <dataset>/radar/pcl_info.txt              points per frame (:182-185, :325)
+//   <dataset>/radar/velocity.txt              Vxyz per frame, precision 15 (:150-168, :757-765)
+//   <dataset>/radar/icp.txt                   R row-major + t per frame, precision 15 (:170-174, :767-791)
+//   <dataset>/radar/icp_map.txt               empty (USE_LOCAL_MAP is off, :32, :793-812)
+//   <csv>                                     output_result.csv (:188-191, :701-706)
+//
+// Per frame k (curr = scan k, last = scan k-1, or scan 0 for k = 0 — :306-315): parse, radar ego
+// velocity of the current scan (icp4r_ego_velocity: fitSineRansac + split + LSQ, :387-431), ICP of
+// curr against last with PCL defaults through the pcl::IterativeClosestPoint facade (:505-521), pose
+// composition currOdom = currOdom * T, t += Rtrans * dt, Rtrans = Rtrans * dR (:541-556).  ROS topics,
+// the 20-frame submap publisher (:577-633) and stdout are not reproduced; the node's RANSAC of the
+// previous scan (:465-493) feeds nothing that is written and is skipped.
+//
+//   icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N]
+//
+// --batch: every frame's ICP is independent of the poses (identity guess), so all frames are
+// registered in ONE device batch (icp4r_align_batch_host) and composed afterwards — identical output
+// to the per-frame loop (the batch path is bit-identical to single calls), one launch sequence.
+#include <sys/stat.h>
+
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "icp4r/icp4r.h"
+#include "icp4r/icp4r_ego.h"
+#include "icp4r/pcl_compat.hpp"
+
+namespace {
+
+// read_radar_data (:64-82): the whole file as float32; a missing file is an empty scan.
+std::vector<float> read_radar_data(const std::string& path) {
+    std::ifstream f(path, std::ifstream::in | std::ifstream::binary);
+    if (!f) return {};
+    f.seekg(0, std::ios::end);
+    const size_t num_elements = (size_t)f.tellg() / sizeof(float);
+    f.seekg(0, std::ios::beg);
+    std::vector<float> buf(num_elements);
+    if (num_elements) f.read(reinterpret_cast<char*>(buf.data()), (std::streamsize)(num_elements * sizeof(float)));
+    return buf;
+}
+
+bool exists(const std::string& p) {
+    struct stat st;
+    return stat(p.c_str(), &st) == 0;
+}
+
+std::string scan_path(const std::string& folder, size_t k) {
+    std::stringstream s;
+    s << folder << "data/" << "radar_pointcloud_" << k << ".bin";
+    return s.str();
+}
+
+// Eigen-like 3x3 / 4x4 double helpers (row-major storage here; the arithmetic is Eigen's
+// coefficient order for fixed-size products: sum over k in order).
+struct M3 {
+    double a[9];
+};
+struct M4 {
+    double a[16];
+};
+M4 mul4(const M4& A, const M4& B) {
+    M4 C;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = A.a[4 * i] * B.a[j];
+            for (int k = 1; k < 4; ++k) s += A.a[4 * i + k] * B.a[4 * k + j];
+            C.a[4 * i + j] = s;
+        }
+    return C;
+}
+M3 mul3(const M3& A, const M3& B) {
+    M3 C;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = A.a[3 * i] * B.a[j];
+            for (int k = 1; k < 3; ++k) s += A.a[3 * i + k] * B.a[3 * k + j];
+            C.a[3 * i + j] = s;
+        }
+    return C;
+}
+
+struct FrameOut {
+    bool registered = false;
+    double T[16];  // icp_result, row-major (double of the float Matrix4f)
+    double score = 0;
+    double A = 0, b = 0;
+    double V[3] = {0, 0, 0};
+};
+
+int usage() {
+    std::fprintf(stderr, "usage: icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N]\n");
+    return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) return usage();
+    std::string dataset_folder = argv[1];
+    if (dataset_folder.empty() || dataset_folder.back() != '/') dataset_folder += "/";
+    std::string csv = dataset_folder + "output_result.csv";
+    bool batch = false;
+    icp4r_ego_params ep;
+    icp4r_ego_params_default(&ep);
+    int max_iterations = -1;  // PCL default (10) unless given
+    for (int i = 2; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "--csv") && i + 1 < argc) csv = argv[++i];
+        else if (!std::strcmp(argv[i], "--batch")) batch = true;
+        else if (!std::strcmp(argv[i], "--seed") && i + 1 < argc) ep.seed = std::strtoull(argv[++i], nullptr, 0);
+        else if (!std::strcmp(argv[i], "--max-iterations") && i + 1 < argc) max_iterations = std::atoi(argv[++i]);
+        else return usage();
+    }
+    const std::string out_dir = dataset_folder + "radar";
+    if (!exists(out_dir) && mkdir(out_dir.c_str(), 0755) != 0) {  // the node shells out to `sudo mkdir` (:151-156)
+        std::perror("mkdir");
+        return 1;
+    }
+    icp4r_ctx* ctx = icp4r::thread_context();
+
+    // ---- the frame loop (:263-721): scans k = 0, 1, ... while radar_pointcloud_<k+1>.bin exists
+    std::vector<std::vector<float>> scans;
+    for (size_t order = 0;; ++order) {
+        scans.push_back(read_radar_data(scan_path(dataset_folder, order)));
+        if (!exists(scan_path(dataset_folder, order + 1))) break;
+    }
+    const size_t nframes = scans.size();
+    std::vector<FrameOut> out(nframes);
+    std::ofstream pcl_info(out_dir + "/pcl_info.txt", std::ios::trunc);
+    pcl_info.setf(std::ios::dec, std::ios::floatfield);
+    using Cloud = pcl::PointCloud<pcl::PointXYZI>;
+    auto to_cloud = [](const std::vector<float>& rec) {
+        auto c = std::make_shared<Cloud>();
+        const size_t n = rec.size() / 5;  // (int)(size() / 5.0) records
+        c->points.reserve(n);
+        for (size_t i = 0; i < n; ++i) c->push_back(pcl::PointXYZI(rec[5 * i], rec[5 * i + 1], rec[5 * i + 2], rec[5 * i + 3]));
+        return c;
+    };
+    icp4r_params ip;
+    icp4r_params_default(&ip);
+    if (max_iterations >= 0) ip.max_iterations = max_iterations;
+
+    for (size_t k = 0; k < nframes; ++k) {
+        const std::vector<float>& curr = scans[k];
+        pcl_info << curr.size() / 5.0 << std::endl;
+        // radar ego velocity of the current scan (:352-431); frame k draws from seed + (k << 32)
+        icp4r_ego_params pk = ep;
+        pk.seed = ep.seed + ((uint64_t)k << 32);
+        icp4r_ego_result er;
+        const int n = (int)(curr.size() / 5);
+        int rc = icp4r_ego_velocity(ctx, curr.data(), n, &pk, &er, nullptr, nullptr);
+        if (rc != ICP4R_OK && rc != ICP4R_E_EMPTY) {
+            std::fprintf(stderr, "icp4r_ego_velocity: %s\n", icp4r_last_error());
+            return 1;
+        }
+        out[k].A = er.A;
+        out[k].b = er.b;
+        for (int c = 0; c < 3; ++c) out[k].V[c] = er.v[c];
+    }
+
+    if (batch) {
+        // every registration in one device batch: pair k = (scan k, scan max(k-1, 0))
+        std::vector<float> src, tgt;
+        std::vector<int64_t> so, to;
+        std::vector<int32_t> sn, tn;
+        std::vector<size_t> frame_of;
+        for (size_t k = 0; k < nframes; ++k) {
+            const std::vector<float>& c = scans[k];
+            const std::vector<float>& l = scans[k ? k - 1 : 0];
+            const int32_t n = (int32_t)(c.size() / 5), m = (int32_t)(l.size() / 5);
+            if (!n || !m) continue;  // `if (cloud_tar_in->size() && cloud_src_in->size())` (:505)
+            so.push_back((int64_t)src.size() / 4);
+            to.push_back((int64_t)tgt.size() / 4);
+            sn.push_back(n);
+            tn.push_back(m);
+            for (int32_t i = 0; i < n; ++i) src.insert(src.end(), &c[5 * (size_t)i], &c[5 * (size_t)i] + 4);
+            for (int32_t i = 0; i < m; ++i) tgt.insert(tgt.end(), &l[5 * (size_t)i], &l[5 * (size_t)i] + 4);
+            frame_of.push_back(k);
+        }
+        std::vector<icp4r_result> res(frame_of.size());
+        if (!frame_of.empty()) {
+            int rc = icp4r_align_batch_host(ctx, src.data(), so.data(), sn.data(), tgt.data(), to.data(), tn.data(),
+                                            (int32_t)frame_of.size(), nullptr, &ip, res.data());
+            if (rc != ICP4R_OK) {
+                std::fprintf(stderr, "icp4r_align_batch_host: %s\n", icp4r_last_error());
+                return 1;
+            }
+        }
+        for (size_t q = 0; q < frame_of.size(); ++q) {
+            FrameOut& f = out[frame_of[q]];
+            f.registered = true;
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) f.T[4 * r + c] = (double)res[q].T[4 * c + r];  // column-major float
+            f.score = res[q].fitness;
+        }
+    } else {
+        for (size_t k = 0; k < nframes; ++k) {
+            auto cloud_src_in = to_cloud(scans[k]);
+            auto cloud_tar_in = to_cloud(scans[k ? k - 1 : 0]);
+            if (!(cloud_tar_in->size() && cloud_src_in->size())) continue;  // :505
+            Cloud Final;
+            pcl::IterativeClosestPoint<pcl::PointXYZI, pcl::PointXYZI> icp;  // :510-521
+            icp.setInputSource(cloud_src_in);
+            icp.setInputTarget(cloud_tar_in);
+            if (max_iterations >= 0) icp.setMaximumIterations(max_iterations);
+            icp.align(Final);
+            const double score = icp.getFitnessScore();
+            const Eigen::Matrix4d icp_result = icp.getFinalTransformation().cast<double>();
+            FrameOut& f = out[k];
+            f.registered = true;
+            for (int r = 0; r < 4; ++r)
+                for (int c = 0; c < 4; ++c) f.T[4 * r + c] = icp_result(r, c);
+            f.score = score;
+        }
+    }
+
+    // ---- pose composition and the per-frame CSV (:541-558, :701-708)
+    FILE* fp = std::fopen(csv.c_str(), "w+");
+    if (!fp) {
+        std::perror("output_result.csv");
+        return 1;
+    }
+    std::fprintf(fp, "#time(s),Rtrans00,Rtrans01,Rtrans02,Rtrans03,Rtrans10,Rtrans11,Rtrans12,Rtrans13,Rtrans20,"
+                     "Rtrans21,Rtrans22,Rtrans23,Rtrans00,Rtrans00,Rtrans00,Rtrans00,score,A,b\n");
+    M4 currOdom = {{1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}};
+    M3 Rtrans = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    double t[3] = {0, 0, 0};
+    double output_time = 0;
+    std::vector<M3> Icp_Rtrans_result;
+    std::vector<std::array<double, 3>> Icp_Ttrans_result;
+    for (size_t k = 0; k < nframes; ++k) {
+        const FrameOut& f = out[k];
+        if (!f.registered) continue;
+        M4 T;
+        std::memcpy(T.a, f.T, sizeof(T.a));
+        M3 dR = {{T.a[0], T.a[1], T.a[2], T.a[4], T.a[5], T.a[6], T.a[8], T.a[9], T.a[10]}};
+        const double dt[3] = {T.a[3], T.a[7], T.a[11]};
+        Icp_Rtrans_result.push_back(dR);
+        Icp_Ttrans_result.push_back({dt[0], dt[1], dt[2]});
+        currOdom = mul4(currOdom, T);
+        for (int r = 0; r < 3; ++r) {  // t = t + Rtrans * odom_Ptrans
+            double s = Rtrans.a[3 * r] * dt[0];
+            s += Rtrans.a[3 * r + 1] * dt[1];
+            s += Rtrans.a[3 * r + 2] * dt[2];
+            t[r] = t[r] + s;
+        }
+        Rtrans = mul3(Rtrans, dR);
+        std::fprintf(fp, "%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f\n", output_time, T.a[0], T.a[1],
+                     T.a[2], T.a[3], T.a[4], T.a[5], T.a[6], T.a[7], T.a[8], T.a[9], T.a[10], T.a[11], T.a[12],
+                     T.a[13], T.a[14], T.a[15], f.score, f.A, f.b);
+        output_time += 1.0;
+    }
+    std::fclose(fp);
+
+    // ---- the files written after the loop (:757-816)
+    std::ofstream velocity_odom(out_dir + "/velocity.txt", std::ios::trunc);
+    velocity_odom.setf(std::ios::dec, std::ios::floatfield);
+    velocity_odom.precision(15);
+    for (size_t k = 0; k < nframes; ++k)
+        velocity_odom << out[k].V[0] << ' ' << out[k].V[1] << ' ' << out[k].V[2] << std::endl;
+    std::ofstream icp_odom(out_dir + "/icp.txt", std::ios::trunc);
+    icp_odom.setf(std::ios::dec, std::ios::floatfield);
+    icp_odom.precision(15);
+    for (size_t i = 0; i < Icp_Rtrans_result.size(); ++i) {
+        const M3& R = Icp_Rtrans_result[i];
+        const auto& T = Icp_Ttrans_result[i];
+        icp_odom << R.a[0] << ' ' << R.a[1] << ' ' << R.a[2] << ' ' << T[0] << ' ' << R.a[3] << ' ' << R.a[4] << ' '
+                 << R.a[5] << ' ' << T[1] << ' ' << R.a[6] << ' ' << R.a[7] << ' ' << R.a[8] << ' ' << T[2]
+                 << std::endl;
+    }
+    std::ofstream icp_map(out_dir + "/icp_map.txt", std::ios::trunc);  // USE_LOCAL_MAP off: stays empty
+    std::printf("replayed %zu frames (%zu registered)%s; final position %.6f %.6f %.6f\n", nframes,
+                Icp_Rtrans_result.size(), batch ? " in one device batch" : "", t[0], t[1], t[2]);
+    return 0;
+}
