@@ -15,10 +15,10 @@
 //                        from 0), the winner's model recomputed, split, KᵀK / KᵀVr in double with a
 //                        fixed-order reduction, Eigen's cofactor 3x3 inverse
 //
-// The inlier test evaluates cos(a_j + b_h) as cos a_j cos b_h - sin a_j sin b_h (a_j, b_h per point /
-// per hypothesis): the two differ by a few ulp of double, so a score can differ from the direct form
-// only for a point whose |delta| lies within ~1e-14 of sigma — never observed (tests/test_ego.py
-// compares every hypothesis score with the oracle's direct evaluation).
+// The inlier test evaluates A cos(a_j + b_h) as (A cos b_h) cos a_j - (A sin b_h) sin a_j with two
+// FMAs (a_j per point, b_h per hypothesis): it differs from the direct form by a few ulp of double, so
+// a score can differ only for a point whose |delta| lies within ~1e-14 of sigma — never observed
+// (tests/test_ego.py compares every hypothesis score with the oracle's direct evaluation).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -81,10 +81,14 @@ __device__ __forceinline__ int ego_hyps(const EgoArgs& e, int n) {
     return e.iterations > 0 ? e.iterations : (int)(n * 0.2);
 }
 
-constexpr int kEgoHyp = 256;  // hypotheses per workgroup (one per lane)
+constexpr int kEgoWG = 256;   // threads per RANSAC workgroup
+constexpr int kEgoPer = 4;    // hypotheses per thread (each LDS point read feeds 4 tests)
+constexpr int kEgoHyp = kEgoWG * kEgoPer;  // hypotheses per workgroup
 constexpr int kEgoPts = 512;  // points per workgroup tile
 
-__global__ __launch_bounds__(kEgoHyp) void ego_ransac_kernel(EgoArgs e) {
+// Inlier test of point j against hypothesis h: |cbv_j - A cos(a_j + b)| < sigma with
+// A cos(a_j + b) = (A cos b) cos a_j - (A sin b) sin a_j: two fused multiply-adds per test.
+__global__ __launch_bounds__(kEgoWG) void ego_ransac_kernel(EgoArgs e) {
     __shared__ double sc[kEgoPts], sca[kEgoPts], ssa[kEgoPts];
     const int s = blockIdx.z;
     const int n = e.cnt[s];
@@ -94,28 +98,41 @@ __global__ __launch_bounds__(kEgoHyp) void ego_ransac_kernel(EgoArgs e) {
     if (n <= 0 || h0 >= H || j0 >= n) return;
     const int64_t base = (int64_t)s * e.stride;
     const int len = min(kEgoPts, n - j0);
-    for (int k = threadIdx.x; k < len; k += kEgoHyp) {
+    for (int k = threadIdx.x; k < len; k += kEgoWG) {
         const double4 v = e.pd[base + j0 + k];
         sc[k] = v.x;
         sca[k] = v.y;
         ssa[k] = v.z;
     }
-    const int h = h0 + threadIdx.x;
-    double A = 0.0, b = 0.0, cb = 0.0, sb = 0.0;
-    if (h < H) {
-        ego_model(e.feat + base, n, e.seed + ((uint64_t)s << 32), h, A, b);
-        cb = cos(b);
-        sb = sin(b);
+    double acb[kEgoPer], asb[kEgoPer];
+#pragma unroll
+    for (int q = 0; q < kEgoPer; ++q) {
+        const int h = h0 + threadIdx.x + q * kEgoWG;
+        acb[q] = 0.0;
+        asb[q] = 0.0;
+        if (h < H) {
+            double A, b;
+            ego_model(e.feat + base, n, e.seed + ((uint64_t)s << 32), h, A, b);
+            acb[q] = A * cos(b);
+            asb[q] = A * sin(b);
+        }
     }
     __syncthreads();
-    if (h >= H) return;
-    int score = 0;
+    int score[kEgoPer] = {};
+    const double sigma = e.sigma;
     for (int k = 0; k < len; ++k) {
-        const double c = sca[k] * cb - ssa[k] * sb;  // cos(a_k + b)
-        const double delta = sc[k] - A * c;
-        score += fabs(delta) < e.sigma ? 1 : 0;
+        const double c = sc[k], ca = sca[k], sa = ssa[k];
+#pragma unroll
+        for (int q = 0; q < kEgoPer; ++q) {
+            const double delta = __builtin_fma(asb[q], sa, __builtin_fma(-acb[q], ca, c));
+            score[q] += fabs(delta) < sigma ? 1 : 0;  // NaN models (a degenerate pair) never count
+        }
     }
-    if (score) atomicAdd(e.scores + (int64_t)s * e.max_h + h, score);
+#pragma unroll
+    for (int q = 0; q < kEgoPer; ++q) {
+        const int h = h0 + threadIdx.x + q * kEgoWG;
+        if (h < H && score[q]) atomicAdd(e.scores + (int64_t)s * e.max_h + h, score[q]);
+    }
 }
 
 constexpr int kEgoSelWG = 256;
@@ -236,7 +253,7 @@ hipError_t launch_ego(const EgoArgs& e, int nscans, int max_n, float4* xyzi, hip
         hipError_t err = hipMemsetAsync(e.scores, 0, (size_t)nscans * e.max_h * sizeof(int32_t), st);
         if (err != hipSuccess) return err;
         hipLaunchKernelGGL(ego_ransac_kernel, dim3((e.max_h + kEgoHyp - 1) / kEgoHyp, (max_n + kEgoPts - 1) / kEgoPts, nscans),
-                           dim3(kEgoHyp), 0, st, e);
+                           dim3(kEgoWG), 0, st, e);
     }
     hipLaunchKernelGGL(ego_select_kernel, dim3(nscans), dim3(kEgoSelWG), 0, st, e);
     return hipGetLastError();
