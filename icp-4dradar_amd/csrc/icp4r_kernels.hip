@@ -694,6 +694,10 @@ struct LdsNN {
     int32_t cur;                                       // the pair this workgroup works on
 };
 
+// LDS slot of sorted target position p: the slot inside its 16-target block XOR the block's low
+// bits — an involution per block (bank spreading for the drain, see nn_lds_kernel)
+__device__ __forceinline__ int lds_swz(int p) { return p ^ ((p >> 4) & (kLdsLeaf - 1)); }
+
 // Bounds on the second-nearest distance of X_i (float2 nn_lu[i]):
 //  L (.x): lower bound on |X_i - t_k| for every target k other than the NN — the cache test's;
 //  U (.y): upper bound on the second-nearest distance — the next search's initial pruning bound.
@@ -863,6 +867,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         __syncthreads();
         const int idx = sh.cur;
         if (idx >= npl) break;  // uniform: every wave read the same sh.cur
+        // debug (ICP4R_PHASE_TICKS=1): per-pair compaction / staging / search wall time, summed over
+        // the pairs of the launch into ticks[8..10], pairs in ticks[11]
+        const bool tk = w.ticks != nullptr && tid == 0;
+        uint64_t tk0 = tk ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = tk0, tk2 = tk0;
         const int p = w.plist[idx];
         const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
         const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
@@ -914,14 +922,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             nlist = total;
             list = qlist;
             __syncthreads();  // qlist (global, this workgroup's) visible to the whole workgroup
+            if (tk) tk1 = __builtin_amdgcn_s_memrealtime();
         }
 
         {  // stage the pair's sorted targets into LDS
             const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
             const int nt = nsb * kSuper * kLdsLeaf;
-            for (int i = tid; i < nt; i += kLdsWG) sh.tl[i] = tsg[i];
+            for (int i = tid; i < nt; i += kLdsWG) sh.tl[lds_swz(i)] = tsg[i];
         }
         __syncthreads();
+        if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
         const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
@@ -930,10 +940,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         uint32_t* secl = sh.u.sec[wave];
         uint16_t* ring = sh.items[wave];
 
-        // Queries per wave run: 64*Q from a long list; a short one (the misses of a late pass) is
-        // spread over all waves in Morton-contiguous runs — the traversal is latency-bound per wave,
-        // and a small run's tight query box lets the coarse tests prune most superblocks.
-        const int per = min(64 * Q, (nlist + kLdsWaves - 1) / kLdsWaves);
+        // Queries per wave run: the list is cut into R rounds of kLdsWaves equal Morton-contiguous
+        // runs of at most 64*Q (R = ceil(nlist / (kLdsWaves * 64 Q))), so every wave gets the same
+        // share — a short list (the misses of a late pass) spreads over all waves, and the traversal,
+        // latency-bound per wave, runs on small runs whose tight query box prunes most superblocks.
+        const int rounds = (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q);
+        const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
         for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
             const int cend = min(base + per, nlist);
             float x[Q], y[Q], z[Q];
@@ -951,19 +963,22 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 x[q] = v.x;
                 y[q] = v.y;
                 z[q] = v.z;
-                // seed: the previous match (first pass: the target at the same relative Morton position)
+                // seed: the previous match (first pass: the target at the same relative Morton
+                // position) and the rest of its 16-target block, evaluated up front from LDS — tight
+                // initial bounds, so the coarse tests below already prune with them
                 const int pj = first ? (int)(((int64_t)s * m) / n) : tinv[key_idx(key[o])];
-                const v4f tj = sh.tl[pj];
-                const NNKey kj = make_key(l2_simple(x[q], y[q], z[q], tj.x, tj.y, tj.z), __float_as_uint(tj.w));
                 if (q == 0) seed_pos0 = pj;
+                const int bj = pj / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
+                const v4f* tb = sh.tl + bj * kLdsLeaf;
+                NNKey lo = ~0ull, hi = ~0ull;  // the two smallest distinct keys seen
+#pragma unroll
+                for (int t = 0; t < kLdsLeaf; ++t) {
+                    const v4f c = tb[t ^ sw];
+                    const NNKey kn = make_key(l2_simple(x[q], y[q], z[q], c.x, c.y, c.z), __float_as_uint(c.w));
+                    hi = kn < lo ? lo : (kn != lo && kn < hi ? kn : hi);
+                    lo = kn < lo ? kn : lo;
+                }
                 if (CACHE) {
-                    // second seed: the Morton neighbour of the first (an upper bound of the second-nearest)
-                    NNKey k2 = ~0ull;
-                    if (m > 1) {
-                        const v4f tn = sh.tl[pj + 1 < m ? pj + 1 : pj - 1];
-                        k2 = make_key(l2_simple(x[q], y[q], z[q], tn.x, tn.y, tn.z), __float_as_uint(tn.w));
-                    }
-                    const NNKey lo = kj < k2 ? kj : k2, hi = kj < k2 ? k2 : kj;
                     // U of the previous search, moved since: an upper bound of the second-nearest
                     // distance even if no evaluated target attains it (first pass: none)
                     uint32_t sec0 = (uint32_t)(hi >> 32);
@@ -975,9 +990,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     secl[q * 64 + lane] = sec0;
                     bnd[q] = orig[q] >= 0 ? __uint_as_float(sec0) : -1.0f;
                 } else {
-                    bestl[q * 64 + lane] = kj;
-                    bnd[q] = orig[q] >= 0 ? key_d2(kj) : -1.0f;
+                    bestl[q * 64 + lane] = lo;
+                    bnd[q] = orig[q] >= 0 ? key_d2(lo) : -1.0f;
                 }
+                evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
             }
             float qlo[3], qhi[3], qmax = 0.0f;
             qlo[0] = qhi[0] = x[0];
@@ -1027,10 +1043,14 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 if (act) {
                     NNKey k1 = ~0ull;
                     uint32_t s2 = 0x7f800000u;  // second-smallest d² of the block (bits; +inf)
+                    // block b's targets sit XOR-swizzled (lds_swz): at step t lane L reads slot
+                    // t ^ (b_L & 15), so lanes on different blocks spread over the 64 banks instead of
+                    // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
                     const v4f* tb = sh.tl + b * kLdsLeaf;
+                    const int sw = b & (kLdsLeaf - 1);
 #pragma unroll
                     for (int t = 0; t < kLdsLeaf; ++t) {
-                        const v4f c = tb[t];
+                        const v4f c = tb[t ^ sw];
                         const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
                         const NNKey kn = make_key(d2, __float_as_uint(c.w));
                         if (CACHE) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
@@ -1127,6 +1147,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             }
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
+        if (tk) {
+            unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
+            atomicAdd(tt + 8, (unsigned long long)(tk1 - tk0));
+            atomicAdd(tt + 9, (unsigned long long)(tk2 - tk1));
+            atomicAdd(tt + 10, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tk2));
+            atomicAdd(tt + 11, 1ull);
+        }
     }
     if (lane == 0) {
         count_add(w.evals, 0, evals);
