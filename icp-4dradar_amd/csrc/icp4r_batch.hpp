@@ -1,0 +1,38 @@
+// icp4r_batch.hpp — the batch registration pipeline's host helpers (icp4r_capi.cpp), shared with
+// the other entry points that run the same device machinery (icp4r_gicp.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "icp4r_host.hpp"
+#include "icp4r_internal.hpp"
+
+namespace icp4r_pipe {
+
+struct Plan {
+    int q;
+    bool packed;  // brute force: v_pk_* FP32 sweep (two queries per register pair)
+    int splits;   // brute force: target splits
+    bool pruned;  // Morton-block pruned exact search
+    bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
+    bool cache;   // lds: cached-neighbour test + second-nearest search (ICP4R_NN_CACHE=0 disables)
+    int leaf;     // pruned: targets per block
+    int64_t blocks;
+};
+
+int env_int(const char* name, int dflt);
+// Geometry of the NN pass for a batch shape.
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO);
+// icp4r_params -> the kernels' KParams (validates).
+int make_kparams(const icp4r_params* p, icp4r::KParams* kp);
+// Size the context's workspace for a plan and fill WorkArgs.
+int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, bool corr, hipStream_t st,
+               icp4r::WorkArgs& w);
+// One NN pass over every pair the pass wants (timed with the context's NN events).
+int nn_pass(icp4r_ctx* ctx, const Plan& pl, const icp4r::PairArgs& a, const icp4r::WorkArgs& w, int npairs, int max_n,
+            int fitness_pass, int first, hipStream_t st);
+int next_event(std::vector<icp4r_host::EventPair>& v, size_t& used, icp4r_host::EventPair** out);
+
+}  // namespace icp4r_pipe

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "icp4r/icp4r.h"
+#include "icp4r_batch.hpp"
 #include "icp4r_host.hpp"
 #include "icp4r_internal.hpp"
 
@@ -63,7 +64,8 @@ using icp4r_host::check_cloud;
 using icp4r_host::fail;
 using icp4r_host::pack_host;
 
-namespace {
+// Batch-pipeline helpers shared with the other entry points (icp4r_gicp.cpp): icp4r_batch.hpp.
+namespace icp4r_pipe {
 
 constexpr size_t kCountBytes = (size_t)kCountSlots * kCountStride * sizeof(uint64_t);
 
@@ -81,17 +83,6 @@ int read_counters(icp4r_ctx* ctx, uint64_t (&out)[kNumCounters]) {
     return ICP4R_OK;
 }
 
-struct Plan {
-    int q;
-    bool packed;  // brute force: v_pk_* FP32 sweep (two queries per register pair)
-    int splits;   // brute force: target splits
-    bool pruned;  // Morton-block pruned exact search
-    bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
-    bool cache;   // lds: cached-neighbour test + second-nearest search (ICP4R_NN_CACHE=0 disables)
-    int leaf;     // pruned: targets per block
-    int64_t blocks;
-};
-
 int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -105,7 +96,7 @@ int env_int(const char* name, int dflt) {
 //    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
 //    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/tune_sweep.py, profiles/tune_r01.jsonl).
 // Tuning overrides (tools/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO) {
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
@@ -397,7 +388,9 @@ int events_avg(std::vector<EventPair>& v, size_t used, double* avg_ms) {
     return ICP4R_OK;
 }
 
-}  // namespace
+}  // namespace icp4r_pipe
+
+using namespace icp4r_pipe;
 
 extern "C" {
 
@@ -457,9 +450,10 @@ int icp4r_destroy(icp4r_ctx* ctx) {
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
-                      &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi})
+                      &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
+                      &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})
         b->release();
-    for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events})
+    for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events, &ctx->gicp_events})
         for (auto& ev : *v) {
             (void)hipEventDestroy(ev.start);
             (void)hipEventDestroy(ev.stop);
@@ -699,6 +693,7 @@ int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* 
         case ICP4R_STAGE_NN_TEST: v = &ctx->test_events; used = ctx->test_used; break;
         case ICP4R_STAGE_UPDATE: v = &ctx->upd_events; used = ctx->upd_used; break;
         case ICP4R_STAGE_BATCH: v = &ctx->batch_events; used = ctx->batch_used; break;
+        case ICP4R_STAGE_GICP_COV: v = &ctx->gicp_events; used = ctx->gicp_used; break;
         default: return fail(ICP4R_E_INVALID, "unknown stage %d", stage);
     }
     HIP_TRY(hipSetDevice(ctx->device));
@@ -713,6 +708,7 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     ctx->test_used = 0;
     ctx->upd_used = 0;
     ctx->batch_used = 0;
+    ctx->gicp_used = 0;
     if (ctx->evals.p) {
         HIP_TRY(hipSetDevice(ctx->device));
         HIP_TRY(hipDeviceSynchronize());

@@ -1,0 +1,282 @@
+// icp4r_gicp.cpp — C ABI of the generalized ICP (include/icp4r/icp4r_gicp.h).
+//
+// FastGICPSingleThread::align (reference: src/radar_odometry.cpp:398-411) as one stream-ordered
+// launch sequence per batch, on the ICP core's device machinery:
+//
+//   init_kernel + gicp_init        validate, X := guess * src, x0 := guess, lambda := -1
+//   index_kernel                   (pruned plans) Morton sort / block boxes of the targets, once
+//   gicp_cov x 2                   source and target covariances (calculate_covariances)
+//   repeat                         NN pass (exact 1-NN of X in the target) + gicp_iter_kernel
+//                                  (Mahalanobis, H / g, LM trials, x0 update, X := float(x0) src);
+//                                  every 4 iterations the host reads how many pairs still iterate
+//   fitness_prep + NN + finish     getFitnessScore and the results, as the ICP path
+//
+// No CPU fallback: every entry fails with ICP4R_E_HIP if the device path cannot run.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "icp4r/icp4r_gicp.h"
+#include "icp4r_batch.hpp"
+#include "icp4r_host.hpp"
+#include "icp4r_internal.hpp"
+
+using namespace icp4r;
+using icp4r_host::DevBuf;
+using icp4r_host::EventPair;
+using icp4r_host::fail;
+
+namespace {
+
+constexpr int kActiveCheck = 4;  // iterations between the host's reads of the active-pair count
+
+int check_params(const icp4r_gicp_params* p) {
+    if (p->k_correspondences < 1 || p->k_correspondences > 32)
+        return fail(ICP4R_E_INVALID, "k_correspondences %d outside [1, 32]", p->k_correspondences);
+    if (p->max_iterations < 0) return fail(ICP4R_E_INVALID, "max_iterations < 0");
+    if (p->lm_max_iterations < 0) return fail(ICP4R_E_INVALID, "lm_max_iterations < 0");
+    if (p->regularization < ICP4R_GICP_REG_NONE || p->regularization > ICP4R_GICP_REG_FROBENIUS)
+        return fail(ICP4R_E_INVALID, "unknown regularization %d", p->regularization);
+    if (!(p->rotation_epsilon > 0) || !(p->transformation_epsilon > 0))
+        return fail(ICP4R_E_INVALID, "convergence epsilons must be > 0");
+    if (!(p->max_correspondence_distance > 0)) return fail(ICP4R_E_INVALID, "max_correspondence_distance must be > 0");
+    return ICP4R_OK;
+}
+
+// The registration of a device-resident batch (pointers in `a`), results into a.results.
+int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m, const icp4r_gicp_params& gp,
+             hipStream_t st) {
+    using namespace icp4r_pipe;
+    if (npairs <= 0) return ICP4R_OK;
+    const int mn = max_n > 0 ? max_n : 1;
+    const int mm = max_m > 0 ? max_m : 1;
+    Plan pl = make_plan(npairs, mn, max_m, ICP4R_NN_AUTO);
+    pl.cache = false;  // gicp_iter_kernel moves X without maintaining the cached-neighbour bounds
+    WorkArgs w;
+    int rc;
+    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, false, st, w))) return rc;
+    const int64_t xs = w.x_stride;
+    const int64_t ts = mm;
+    HIP_TRY(ctx->gicp_gs.ensure((size_t)npairs * sizeof(GicpState)));
+    HIP_TRY(ctx->gicp_cov_src.ensure((size_t)npairs * xs * 6 * sizeof(double)));
+    HIP_TRY(ctx->gicp_cov_tgt.ensure((size_t)npairs * ts * 6 * sizeof(double)));
+    HIP_TRY(ctx->gicp_mah.ensure((size_t)npairs * xs * 6 * sizeof(double)));
+    HIP_TRY(ctx->gicp_active.ensure(sizeof(int32_t)));
+    GicpArgs g;
+    g.gs = static_cast<GicpState*>(ctx->gicp_gs.p);
+    g.cov_src = static_cast<const double*>(ctx->gicp_cov_src.p);
+    g.cov_tgt = static_cast<const double*>(ctx->gicp_cov_tgt.p);
+    g.mah = static_cast<double*>(ctx->gicp_mah.p);
+    g.t_stride = ts;
+    const float thr = (float)fmin(gp.max_correspondence_distance, (double)FLT_MAX);
+    g.max_d2 = (double)(thr * thr);  // corr_dist_threshold_ * corr_dist_threshold_ (float)
+    g.rot_eps = gp.rotation_epsilon;
+    g.trans_eps = gp.transformation_epsilon;
+    g.lm_init = gp.lm_init_lambda_factor;
+    g.lm_max_iterations = gp.lm_max_iterations;
+    g.max_iterations = gp.max_iterations;
+
+    EventPair* be;
+    if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
+    HIP_TRY(hipEventRecord(be->start, st));
+    HIP_TRY(launch_init(a, w, npairs, st));
+    HIP_TRY(launch_gicp_init(a.guess, g.gs, npairs, st));
+    if (pl.pruned) HIP_TRY(launch_index(a, w, npairs, st));
+    EventPair* ce;
+    if ((rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
+    HIP_TRY(hipEventRecord(ce->start, st));
+    HIP_TRY(launch_gicp_cov(a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization,
+                            static_cast<double*>(ctx->gicp_cov_src.p), st));
+    HIP_TRY(launch_gicp_cov(a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization,
+                            static_cast<double*>(ctx->gicp_cov_tgt.p), st));
+    HIP_TRY(hipEventRecord(ce->stop, st));
+    int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
+    for (int it = 0; it < gp.max_iterations; ++it) {
+        if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
+        EventPair* ue;
+        if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
+        HIP_TRY(hipEventRecord(ue->start, st));
+        HIP_TRY(launch_gicp_iter(a, w, g, npairs, it, st));
+        HIP_TRY(hipEventRecord(ue->stop, st));
+        if ((it + 1) % kActiveCheck == 0 && it + 1 < gp.max_iterations) {
+            int32_t h = 0;
+            HIP_TRY(launch_gicp_active(w.state, npairs, active, st));
+            HIP_TRY(hipMemcpyAsync(&h, active, sizeof(h), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (h == 0) break;
+        }
+    }
+    if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
+    if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, a, w, npairs, mn, 1, 0, st))) return rc;
+    HIP_TRY(launch_finish(a, w, npairs, st));
+    HIP_TRY(hipEventRecord(be->stop, st));
+    return ICP4R_OK;
+}
+
+int gicp_kparams(const icp4r_gicp_params& gp, KParams* kp) {
+    icp4r_params ip;
+    icp4r_params_default(&ip);
+    ip.compute_fitness = gp.compute_fitness;
+    int rc = icp4r_pipe::make_kparams(&ip, kp);
+    if (rc) return rc;
+    kp->fit_max_range = DBL_MAX;  // Registration::getFitnessScore() default
+    return ICP4R_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void icp4r_gicp_params_default(icp4r_gicp_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->k_correspondences = 20;
+    p->max_iterations = 64;
+    p->rotation_epsilon = 2e-3;
+    p->transformation_epsilon = 5e-4;
+    p->max_correspondence_distance = FLT_MAX;
+    p->regularization = ICP4R_GICP_REG_PLANE;
+    p->lm_max_iterations = 10;
+    p->lm_init_lambda_factor = 1e-9;
+    p->compute_fitness = 1;
+}
+
+int icp4r_gicp_align_batch_device(icp4r_ctx* ctx, const icp4r_batch* b, const icp4r_gicp_params* params,
+                                  icp4r_result* results, void* hip_stream) {
+    if (!ctx || !b || !results) return fail(ICP4R_E_INVALID, "ctx/batch/results is NULL");
+    if (b->npairs < 0) return fail(ICP4R_E_INVALID, "npairs < 0");
+    if (b->npairs == 0) return ICP4R_OK;
+    if (!b->src || !b->tgt || !b->src_off || !b->src_n || !b->tgt_off || !b->tgt_n)
+        return fail(ICP4R_E_INVALID, "batch has a NULL device array");
+    if (b->max_src_n < 0 || b->max_tgt_n < 0) return fail(ICP4R_E_INVALID, "negative max sizes");
+    icp4r_gicp_params gp;
+    if (params) gp = *params;
+    else icp4r_gicp_params_default(&gp);
+    int rc;
+    if ((rc = check_params(&gp))) return rc;
+    PairArgs a;
+    if ((rc = gicp_kparams(gp, &a.kp))) return rc;
+    HIP_TRY(hipSetDevice(ctx->device));
+    a.src = reinterpret_cast<const float4*>(b->src);
+    a.tgt = reinterpret_cast<const float4*>(b->tgt);
+    a.src_off = b->src_off;
+    a.src_n = b->src_n;
+    a.tgt_off = b->tgt_off;
+    a.tgt_n = b->tgt_n;
+    a.guess = b->guess;
+    a.aligned = reinterpret_cast<float4*>(b->aligned);
+    a.results = reinterpret_cast<Result*>(results);
+    hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    return run_gicp(ctx, a, b->npairs, b->max_src_n, b->max_tgt_n, gp, st);
+}
+
+int icp4r_gicp_align(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_bytes, const float* tgt,
+                     int32_t m, int32_t tgt_stride_bytes, const float* guess, const icp4r_gicp_params* params,
+                     icp4r_result* out, float* aligned_out, int32_t out_stride_bytes) {
+    using namespace icp4r_host;
+    if (!ctx || !out) return fail(ICP4R_E_INVALID, "ctx/out is NULL");
+    int rc;
+    if ((rc = check_cloud(src, n, src_stride_bytes, "source"))) return rc;
+    if ((rc = check_cloud(tgt, m, tgt_stride_bytes, "target"))) return rc;
+    if (aligned_out && (out_stride_bytes < 12 || out_stride_bytes % 4))
+        return fail(ICP4R_E_INVALID, "aligned_out stride %d bytes", out_stride_bytes);
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> hs, ht;
+    pack_host(src, n, src_stride_bytes, hs);
+    pack_host(tgt, m, tgt_stride_bytes, ht);
+    const int64_t zero64 = 0;
+    HIP_TRY(ctx->src.ensure(hs.size() * sizeof(float) + 16));
+    HIP_TRY(ctx->tgt.ensure(ht.size() * sizeof(float) + 16));
+    HIP_TRY(ctx->src_off.ensure(16));
+    HIP_TRY(ctx->tgt_off.ensure(16));
+    HIP_TRY(ctx->src_n.ensure(16));
+    HIP_TRY(ctx->tgt_n.ensure(16));
+    HIP_TRY(ctx->guess.ensure(16 * sizeof(float)));
+    HIP_TRY(ctx->results.ensure(sizeof(icp4r_result)));
+    HIP_TRY(ctx->aligned.ensure(hs.size() * sizeof(float) + 16));
+    hipStream_t st = ctx->stream;
+    if (!hs.empty()) HIP_TRY(hipMemcpyAsync(ctx->src.p, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    if (!ht.empty()) HIP_TRY(hipMemcpyAsync(ctx->tgt.p, ht.data(), ht.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_n.p, &n, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_n.p, &m, 4, hipMemcpyHostToDevice, st));
+    if (guess) HIP_TRY(hipMemcpyAsync(ctx->guess.p, guess, 16 * sizeof(float), hipMemcpyHostToDevice, st));
+    icp4r_batch b;
+    memset(&b, 0, sizeof(b));
+    b.src = static_cast<const float*>(ctx->src.p);
+    b.tgt = static_cast<const float*>(ctx->tgt.p);
+    b.src_off = static_cast<const int64_t*>(ctx->src_off.p);
+    b.tgt_off = static_cast<const int64_t*>(ctx->tgt_off.p);
+    b.src_n = static_cast<const int32_t*>(ctx->src_n.p);
+    b.tgt_n = static_cast<const int32_t*>(ctx->tgt_n.p);
+    b.guess = guess ? static_cast<const float*>(ctx->guess.p) : nullptr;
+    b.aligned = aligned_out ? static_cast<float*>(ctx->aligned.p) : nullptr;
+    b.npairs = 1;
+    b.max_src_n = n;
+    b.max_tgt_n = m;
+    if ((rc = icp4r_gicp_align_batch_device(ctx, &b, params, static_cast<icp4r_result*>(ctx->results.p), st))) return rc;
+    HIP_TRY(hipMemcpyAsync(out, ctx->results.p, sizeof(icp4r_result), hipMemcpyDeviceToHost, st));
+    std::vector<float> ha;
+    if (aligned_out && n > 0) {
+        ha.resize((size_t)n * 4);
+        HIP_TRY(hipMemcpyAsync(ha.data(), ctx->aligned.p, ha.size() * sizeof(float), hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (aligned_out && n > 0) {
+        unsigned char* o = reinterpret_cast<unsigned char*>(aligned_out);
+        for (int32_t i = 0; i < n; ++i) {
+            float* q = reinterpret_cast<float*>(o + (size_t)i * out_stride_bytes);
+            q[0] = ha[4 * (size_t)i];
+            q[1] = ha[4 * (size_t)i + 1];
+            q[2] = ha[4 * (size_t)i + 2];
+            if (out_stride_bytes >= 16) q[3] = ha[4 * (size_t)i + 3];
+        }
+    }
+    if (out->status != ICP4R_OK) {
+        const char* what = out->status == ICP4R_E_EMPTY ? "No input target dataset was given!"
+                           : out->status == ICP4R_E_NONFINITE ? "non-finite coordinate in an input cloud"
+                                                              : "registration failed";
+        return fail(out->status, "[icp4r::FastGICP::computeTransformation] %s", what);
+    }
+    return ICP4R_OK;
+}
+
+int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_t stride_bytes, int32_t k,
+                           int32_t regularization, double* cov_out) {
+    using namespace icp4r_host;
+    if (!ctx || (!cov_out && n > 0)) return fail(ICP4R_E_INVALID, "ctx/cov_out is NULL");
+    if (k < 1 || k > 32) return fail(ICP4R_E_INVALID, "k %d outside [1, 32]", k);
+    if (regularization < ICP4R_GICP_REG_NONE || regularization > ICP4R_GICP_REG_FROBENIUS)
+        return fail(ICP4R_E_INVALID, "unknown regularization %d", regularization);
+    int rc;
+    if ((rc = check_cloud(cloud, n, stride_bytes, "cloud"))) return rc;
+    if (n == 0) return ICP4R_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> hc;
+    pack_host(cloud, n, stride_bytes, hc);
+    const int64_t zero64 = 0;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(ctx->src.ensure(hc.size() * sizeof(float)));
+    HIP_TRY(ctx->src_off.ensure(16));
+    HIP_TRY(ctx->src_n.ensure(16));
+    HIP_TRY(ctx->gicp_cov_src.ensure((size_t)n * 6 * sizeof(double)));
+    HIP_TRY(hipMemcpyAsync(ctx->src.p, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_n.p, &n, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_gicp_cov(static_cast<const float4*>(ctx->src.p), static_cast<const int64_t*>(ctx->src_off.p),
+                            static_cast<const int32_t*>(ctx->src_n.p), 1, n, n, k, regularization,
+                            static_cast<double*>(ctx->gicp_cov_src.p), st));
+    std::vector<double> h6((size_t)n * 6);
+    HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    static const int idx[9] = {0, 1, 2, 1, 3, 4, 2, 4, 5};
+    for (int32_t i = 0; i < n; ++i)
+        for (int t = 0; t < 9; ++t) cov_out[(size_t)i * 9 + t] = h6[(size_t)i * 6 + idx[t]];
+    return ICP4R_OK;
+}
+
+}  // extern "C"

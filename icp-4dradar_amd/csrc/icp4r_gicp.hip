@@ -1,0 +1,538 @@
+// icp4r_gicp.hip — generalized ICP for gfx950 (include/icp4r/icp4r_gicp.h).
+//
+// fast_gicp's FastGICPSingleThread, as the reference's radar_odometry node runs it on the scan-to-map
+// path (radar_odometry.cpp:398-411), restated device-resident:
+//
+//   gicp_cov_kernel<K>   per point: exact K nearest neighbours in its own cloud (the point included;
+//                        (d², index) keys, the cloud streamed through LDS tiles), mean-centred
+//                        covariance in double, regularised (PLANE: U diag(1, 1, 1e-3) Uᵀ from a
+//                        cyclic-Jacobi eigendecomposition)
+//   per iteration        the exact NN pass of the ICP core (pruned / brute / LDS kernels, unchanged)
+//                        over X = float(x0) · src, then
+//   gicp_iter_kernel     one workgroup per pair: Mahalanobis M_i = (C_B + R C_A Rᵀ)⁻¹, the
+//                        Gauss-Newton system (H = Σ JᵀMJ, g = Σ JᵀMe, y = Σ eᵀMe, J = [skew(T a), -I])
+//                        in double with a fixed-order reduction, then Levenberg-Marquardt trials —
+//                        thread 0 solves (H + λI) d = -g by LDLᵀ and forms delta = [so3_exp | t]; the
+//                        whole workgroup re-evaluates the error at delta · x0 on the cached
+//                        correspondences; accept / reject / converge as LsqRegistration::step_lm;
+//                        then X := float(x0) · src for the next NN pass.
+//
+// Per-pair flags (PairState.phase) stop converged / failed pairs; the host launches the iterations
+// in short runs and checks the flags in between.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "icp4r_internal.hpp"
+
+namespace icp4r {
+
+// ---- small double linear algebra (device)
+
+// symmetric 3x3 eigendecomposition by cyclic Jacobi: a (row-major) -> w (descending), V (columns)
+__device__ void gicp_sym_eig3(const double* a_in, double* w, double* V) {
+    double a[9];
+    for (int i = 0; i < 9; ++i) a[i] = a_in[i];
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        if (a[1] * a[1] + a[2] * a[2] + a[5] * a[5] == 0.0) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                const double apq = a[3 * p + q];
+                if (apq == 0.0) continue;
+                const double theta = (a[3 * q + q] - a[3 * p + p]) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 3; ++k) {
+                    const double akp = a[3 * k + p], akq = a[3 * k + q];
+                    a[3 * k + p] = c * akp - s * akq;
+                    a[3 * k + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double apk = a[3 * p + k], aqk = a[3 * q + k];
+                    a[3 * p + k] = c * apk - s * aqk;
+                    a[3 * q + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double vkp = V[3 * k + p], vkq = V[3 * k + q];
+                    V[3 * k + p] = c * vkp - s * vkq;
+                    V[3 * k + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < 3; ++i) w[i] = a[4 * i];
+    for (int i = 0; i < 2; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (w[j] > w[i]) {
+                const double tw = w[i];
+                w[i] = w[j];
+                w[j] = tw;
+                for (int k = 0; k < 3; ++k) {
+                    const double tv = V[3 * k + i];
+                    V[3 * k + i] = V[3 * k + j];
+                    V[3 * k + j] = tv;
+                }
+            }
+}
+
+// Eigen-style cofactor inverse of a 3x3 (row-major)
+__device__ __forceinline__ void gicp_inv3(const double* m, double* r) {
+    const double c0 = m[4] * m[8] - m[5] * m[7];
+    const double c1 = m[7] * m[2] - m[8] * m[1];
+    const double c2 = m[1] * m[5] - m[2] * m[4];
+    const double id = 1.0 / (c0 * m[0] + c1 * m[3] + c2 * m[6]);
+    r[0] = c0 * id;
+    r[1] = c1 * id;
+    r[2] = c2 * id;
+    r[3] = (m[5] * m[6] - m[3] * m[8]) * id;
+    r[4] = (m[8] * m[0] - m[6] * m[2]) * id;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    r[6] = (m[3] * m[7] - m[4] * m[6]) * id;
+    r[7] = (m[6] * m[1] - m[7] * m[0]) * id;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// fast_gicp::RegularizationMethod applied to a 3x3 covariance (row-major, symmetric)
+__device__ void gicp_regularize(const double* c, int reg, double* o) {
+    if (reg == ICP4R_GICP_REG_NONE) {
+        for (int t = 0; t < 9; ++t) o[t] = c[t];
+        return;
+    }
+    if (reg == ICP4R_GICP_REG_FROBENIUS) {
+        double C[9], Ci[9], nrm = 0.0;
+        for (int t = 0; t < 9; ++t) C[t] = c[t];
+        for (int t = 0; t < 3; ++t) C[4 * t] += 1e-3;
+        gicp_inv3(C, Ci);
+        for (int t = 0; t < 9; ++t) nrm += Ci[t] * Ci[t];
+        nrm = sqrt(nrm);
+        for (int t = 0; t < 9; ++t) Ci[t] /= nrm;
+        gicp_inv3(Ci, o);
+        return;
+    }
+    double w[3], V[9], v[3];
+    gicp_sym_eig3(c, w, V);
+    for (int t = 0; t < 3; ++t) {
+        if (reg == ICP4R_GICP_REG_PLANE) {
+            v[t] = t < 2 ? 1.0 : 1e-3;
+        } else if (reg == ICP4R_GICP_REG_MIN_EIG) {
+            v[t] = fmax(w[t], 1e-3);
+        } else {  // NORMALIZED_MIN_EIG
+            v[t] = fmax(w[0] != 0.0 ? w[t] / w[0] : 0.0, 1e-3);
+        }
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int s = 0; s < 3; ++s) o[3 * r + s] = V[3 * r] * v[0] * V[3 * s] + V[3 * r + 1] * v[1] * V[3 * s + 1] + V[3 * r + 2] * v[2] * V[3 * s + 2];
+}
+
+// ---- covariances
+constexpr int kCovWG = 256;
+constexpr int kCovTile = 1024;
+
+template <int K>
+__global__ __launch_bounds__(kCovWG) void gicp_cov_kernel(const float4* __restrict__ cloud, const int64_t* __restrict__ off,
+                                                          const int32_t* __restrict__ cnt, int64_t stride, int k, int reg,
+                                                          double* __restrict__ cov_out) {
+    __shared__ float4 tile[kCovTile];
+    const int p = blockIdx.y;
+    const int n = cnt[p];
+    const int i = blockIdx.x * kCovWG + threadIdx.x;
+    if (blockIdx.x * kCovWG >= n) return;
+    const float4* c = cloud + off[p];
+    const float4 q = c[min(i, n - 1)];
+    uint64_t best[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) best[s] = ~0ull;
+    for (int j0 = 0; j0 < n; j0 += kCovTile) {
+        const int len = min(kCovTile, n - j0);
+        __syncthreads();
+        for (int t = threadIdx.x; t < len; t += kCovWG) tile[t] = c[j0 + t];
+        __syncthreads();
+        for (int t = 0; t < len; ++t) {
+            const float4 v = tile[t];
+            const float dx = q.x - v.x, dy = q.y - v.y, dz = q.z - v.z;
+            float d2 = dx * dx;
+            d2 = d2 + dy * dy;
+            d2 = d2 + dz * dz;
+            uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)(j0 + t);
+            if (key < best[K - 1]) {  // bubble into the sorted top-K (ascending (d², index))
+#pragma unroll
+                for (int s = 0; s < K; ++s) {
+                    const uint64_t lo = key < best[s] ? key : best[s];
+                    key = key < best[s] ? best[s] : key;
+                    best[s] = lo;
+                }
+            }
+        }
+    }
+    if (i >= n) return;
+    const int kk = min(k, n);
+    double mean[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (s >= kk) break;
+        const float4 v = c[(uint32_t)best[s]];
+        mean[0] += (double)v.x;
+        mean[1] += (double)v.y;
+        mean[2] += (double)v.z;
+    }
+    for (int r = 0; r < 3; ++r) mean[r] /= (double)kk;
+    double cv[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (s >= kk) break;
+        const float4 v = c[(uint32_t)best[s]];
+        const double d[3] = {(double)v.x - mean[0], (double)v.y - mean[1], (double)v.z - mean[2]};
+        for (int r = 0; r < 3; ++r)
+            for (int t = 0; t < 3; ++t) cv[3 * r + t] += d[r] * d[t];
+    }
+    for (int t = 0; t < 9; ++t) cv[t] /= (double)k;
+    double o[9];
+    gicp_regularize(cv, reg, o);
+    double* out = cov_out + ((int64_t)p * stride + i) * 6;
+    out[0] = o[0];
+    out[1] = o[1];
+    out[2] = o[2];
+    out[3] = o[4];
+    out[4] = o[5];
+    out[5] = o[8];
+}
+
+// ---- per-iteration update
+constexpr int kGicpWG = 1024;
+constexpr int kGicpWaves = kGicpWG / 64;
+constexpr int kGicpSys = 21 + 6 + 1 + 1;  // H (upper triangle), g, y, |valid|
+
+__device__ __forceinline__ void sym_unpack(const double* s, double* m) {
+    m[0] = s[0]; m[1] = s[1]; m[2] = s[2];
+    m[3] = s[1]; m[4] = s[3]; m[5] = s[4];
+    m[6] = s[2]; m[7] = s[4]; m[8] = s[5];
+}
+
+// so3_exp (fast_gicp so3.hpp) then Eigen's Quaternion::toRotationMatrix
+__device__ void gicp_so3_exp(const double* w, double* R) {
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double imag, real;
+    if (th2 < 1e-10) {
+        const double th4 = th2 * th2;
+        imag = 0.5 - 1.0 / 48.0 * th2 + 1.0 / 3840.0 * th4;
+        real = 1.0 - 1.0 / 8.0 * th2 + 1.0 / 384.0 * th4;
+    } else {
+        const double th = sqrt(th2), half = 0.5 * th;
+        imag = sin(half) / th;
+        real = cos(half);
+    }
+    const double qw = real, qx = imag * w[0], qy = imag * w[1], qz = imag * w[2];
+    const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+    const double twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+// (A) x = b, A symmetric positive definite 6x6 (row-major), LDLᵀ without pivoting
+__device__ void gicp_ldlt6(const double* A, const double* b, double* x) {
+    double L[36], D[6], y[6];
+    for (int t = 0; t < 36; ++t) L[t] = 0.0;
+    for (int j = 0; j < 6; ++j) {
+        double s = A[6 * j + j];
+        for (int k = 0; k < j; ++k) s -= L[6 * j + k] * L[6 * j + k] * D[k];
+        D[j] = s;
+        L[6 * j + j] = 1.0;
+        for (int i = j + 1; i < 6; ++i) {
+            double t = A[6 * i + j];
+            for (int k = 0; k < j; ++k) t -= L[6 * i + k] * L[6 * j + k] * D[k];
+            L[6 * i + j] = D[j] != 0.0 ? t / D[j] : t;  // Eigen: a zero pivot leaves its column undivided
+        }
+    }
+    for (int i = 0; i < 6; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[6 * i + k] * y[k];
+        y[i] = s;
+    }
+    for (int i = 0; i < 6; ++i) y[i] = fabs(D[i]) > DBL_MIN ? y[i] / D[i] : 0.0;  // Eigen's LDLT::solve
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i];
+        for (int k = i + 1; k < 6; ++k) s -= L[6 * k + i] * x[k];
+        x[i] = s;
+    }
+}
+
+__device__ __forceinline__ bool gicp_converged(const double* R, const double* t, double rot_eps, double trans_eps) {
+    double m = 0.0;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) m = fmax(m, 1.0 / rot_eps * fabs(R[3 * r + c] - (r == c ? 1.0 : 0.0)));
+    for (int r = 0; r < 3; ++r) m = fmax(m, 1.0 / trans_eps * fabs(t[r]));
+    return m < 1.0;
+}
+
+struct GicpShared {
+    double red[kGicpWaves * kGicpSys];
+    double sys[kGicpSys];
+    double R[9], t[3];    // the transform the error pass evaluates
+    double dR[9], dt[3];  // the trial delta
+    int32_t stop;
+};
+
+// Σ eᵀMe (and with `lin` the system) over this thread's valid correspondences at transform (R, t).
+template <bool LIN>
+__device__ __forceinline__ void gicp_accumulate(const float4* src, const float4* tgt, const NNKey* key, const double* mah,
+                                                int n, double max_d2, const double* R, const double* t,
+                                                double (&acc)[kGicpSys]) {
+    for (int i = threadIdx.x; i < n; i += kGicpWG) {
+        const NNKey kk = key[i];
+        if (!((double)key_d2(kk) < max_d2)) continue;
+        const float4 sa = src[i], sb = tgt[key_idx(kk)];
+        const double a[3] = {sa.x, sa.y, sa.z};
+        double ta[3];
+        for (int r = 0; r < 3; ++r) ta[r] = R[3 * r] * a[0] + R[3 * r + 1] * a[1] + R[3 * r + 2] * a[2] + t[r];
+        const double e[3] = {(double)sb.x - ta[0], (double)sb.y - ta[1], (double)sb.z - ta[2]};
+        double M[9];
+        sym_unpack(mah + (int64_t)i * 6, M);
+        double Me[3];
+        for (int r = 0; r < 3; ++r) Me[r] = M[3 * r] * e[0] + M[3 * r + 1] * e[1] + M[3 * r + 2] * e[2];
+        acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+        if (!LIN) continue;
+        acc[28] += 1.0;
+        // J = [skew(ta), -I]; H = JᵀMJ, g = JᵀMe
+        const double J[18] = {0.0, -ta[2], ta[1], -1.0, 0.0, 0.0,
+                              ta[2], 0.0, -ta[0], 0.0, -1.0, 0.0,
+                              -ta[1], ta[0], 0.0, 0.0, 0.0, -1.0};
+        double MJ[18];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 6; ++c) MJ[6 * r + c] = M[3 * r] * J[c] + M[3 * r + 1] * J[6 + c] + M[3 * r + 2] * J[12 + c];
+        int u = 0;
+        for (int r = 0; r < 6; ++r) {
+            for (int c = r; c < 6; ++c) acc[u++] += J[r] * MJ[c] + J[6 + r] * MJ[6 + c] + J[12 + r] * MJ[12 + c];
+            acc[21 + r] += J[r] * Me[0] + J[6 + r] * Me[1] + J[12 + r] * Me[2];
+        }
+    }
+}
+
+__device__ __forceinline__ void gicp_block_sum(double (&v)[kGicpSys], GicpShared& sh) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kGicpSys; ++k) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    }
+    if (lane == 0)
+        for (int k = 0; k < kGicpSys; ++k) sh.red[wave * kGicpSys + k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < kGicpSys) {
+        double t = 0.0;
+        for (int w = 0; w < kGicpWaves; ++w) t += sh.red[w * kGicpSys + threadIdx.x];
+        sh.sys[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kGicpWG) void gicp_iter_kernel(PairArgs a, WorkArgs w, GicpArgs g, int it) {
+    __shared__ GicpShared sh;
+    const int p = blockIdx.x;
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return;
+    GicpState& gs = g.gs[p];
+    const int n = a.src_n[p];
+    const float4* src = a.src + a.src_off[p];
+    const float4* tgt = a.tgt + a.tgt_off[p];
+    const NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    double* mah = g.mah + (int64_t)p * w.x_stride * 6;
+    const double* cs = g.cov_src + (int64_t)p * w.x_stride * 6;
+    const double* ct = g.cov_tgt + (int64_t)p * g.t_stride * 6;
+    double R[9], t[3];
+    for (int k = 0; k < 9; ++k) R[k] = gs.R[k];
+    for (int k = 0; k < 3; ++k) t[k] = gs.t[k];
+    // update_correspondences: Mahalanobis of every valid correspondence
+    for (int i = threadIdx.x; i < n; i += kGicpWG) {
+        const NNKey kk = key[i];
+        if (!((double)key_d2(kk) < g.max_d2)) continue;
+        double CA[9], CB[9], RC[9], RCR[9], Mi[9];
+        sym_unpack(cs + (int64_t)i * 6, CA);
+        sym_unpack(ct + (int64_t)key_idx(kk) * 6, CB);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) RC[3 * r + c] = R[3 * r] * CA[c] + R[3 * r + 1] * CA[3 + c] + R[3 * r + 2] * CA[6 + c];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                RCR[3 * r + c] = CB[3 * r + c] + (RC[3 * r] * R[3 * c] + RC[3 * r + 1] * R[3 * c + 1] + RC[3 * r + 2] * R[3 * c + 2]);
+        gicp_inv3(RCR, Mi);
+        double* o = mah + (int64_t)i * 6;
+        o[0] = Mi[0];
+        o[1] = Mi[1];
+        o[2] = Mi[2];
+        o[3] = Mi[4];
+        o[4] = Mi[5];
+        o[5] = Mi[8];
+    }
+    __syncthreads();  // workgroup-scope visibility of the Mahalanobis array
+    double acc[kGicpSys];
+    for (int k = 0; k < kGicpSys; ++k) acc[k] = 0.0;
+    gicp_accumulate<true>(src, tgt, key, mah, n, g.max_d2, R, t, acc);
+    gicp_block_sum(acc, sh);
+    // step_lm
+    double H[36], gv[6], y0 = 0.0, lambda = 0.0, nu = 2.0;
+    if (threadIdx.x == 0) {
+        int u = 0;
+        for (int r = 0; r < 6; ++r)
+            for (int c = r; c < 6; ++c) H[6 * r + c] = H[6 * c + r] = sh.sys[u++];
+        for (int r = 0; r < 6; ++r) gv[r] = sh.sys[21 + r];
+        y0 = sh.sys[27];
+        lambda = gs.lambda;
+        if (lambda < 0.0) {
+            double mx = 0.0;
+            for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(H[7 * k]));
+            lambda = g.lm_init * mx;
+        }
+        st.ncorr = (int)sh.sys[28];
+    }
+    int outcome = 0;  // 1 accepted, 2 converged on a rejected step, 0 failed
+    double d[6];
+    for (int trial = 0; trial < g.lm_max_iterations; ++trial) {
+        if (threadIdx.x == 0) {
+            double A[36], nb[6];
+            for (int k = 0; k < 36; ++k) A[k] = H[k];
+            for (int k = 0; k < 6; ++k) A[7 * k] += lambda;
+            for (int k = 0; k < 6; ++k) nb[k] = -gv[k];
+            gicp_ldlt6(A, nb, d);
+            gicp_so3_exp(d, sh.dR);
+            sh.dt[0] = d[3];
+            sh.dt[1] = d[4];
+            sh.dt[2] = d[5];
+            // xi = delta * x0
+            for (int r = 0; r < 3; ++r) {
+                for (int c = 0; c < 3; ++c)
+                    sh.R[3 * r + c] = sh.dR[3 * r] * R[c] + sh.dR[3 * r + 1] * R[3 + c] + sh.dR[3 * r + 2] * R[6 + c];
+                sh.t[r] = sh.dR[3 * r] * t[0] + sh.dR[3 * r + 1] * t[1] + sh.dR[3 * r + 2] * t[2] + sh.dt[r];
+            }
+        }
+        __syncthreads();
+        double ri[9], ti[3];
+        for (int k = 0; k < 9; ++k) ri[k] = sh.R[k];
+        for (int k = 0; k < 3; ++k) ti[k] = sh.t[k];
+        for (int k = 0; k < kGicpSys; ++k) acc[k] = 0.0;
+        gicp_accumulate<false>(src, tgt, key, mah, n, g.max_d2, ri, ti, acc);
+        gicp_block_sum(acc, sh);
+        if (threadIdx.x == 0) {
+            const double yi = sh.sys[27];
+            double den = 0.0;
+            for (int k = 0; k < 6; ++k) den += d[k] * (lambda * d[k] - gv[k]);
+            const double rho = (y0 - yi) / den;
+            sh.stop = 0;
+            if (rho < 0) {
+                if (gicp_converged(sh.dR, sh.dt, g.rot_eps, g.trans_eps)) {
+                    sh.stop = 2;
+                } else {
+                    lambda = nu * lambda;
+                    nu = 2 * nu;
+                }
+            } else {
+                for (int k = 0; k < 9; ++k) R[k] = sh.R[k];
+                for (int k = 0; k < 3; ++k) t[k] = sh.t[k];
+                lambda = lambda * fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
+                sh.stop = 1;
+            }
+        }
+        __syncthreads();
+        outcome = sh.stop;
+        __syncthreads();  // every thread read sh.stop before the next trial rewrites it
+        if (outcome) break;
+    }
+    if (threadIdx.x == 0) {
+        st.iterations = it;  // nr_iterations_ = i
+        gs.lambda = lambda;
+        for (int k = 0; k < 9; ++k) gs.R[k] = R[k];
+        for (int k = 0; k < 3; ++k) gs.t[k] = t[k];
+        // final_transformation_ = x0.cast<float>() (column-major)
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) st.final_T[4 * c + r] = (float)R[3 * r + c];
+            st.final_T[12 + r] = (float)t[r];
+            st.final_T[4 * r + 3] = 0.0f;
+        }
+        st.final_T[15] = 1.0f;
+        if (!outcome) {
+            st.phase = kPhaseFailed;  // step_lm returned false: "lm not converged!!", break
+        } else if (gicp_converged(sh.dR, sh.dt, g.rot_eps, g.trans_eps)) {
+            st.phase = kPhaseConverged;
+            st.conv_state = 2;
+        } else if (it + 1 >= g.max_iterations) {
+            st.conv_state = 1;
+        }
+        for (int k = 0; k < 9; ++k) sh.R[k] = R[k];
+        for (int k = 0; k < 3; ++k) sh.t[k] = t[k];
+    }
+    __syncthreads();
+    if (st.phase != kPhaseActive) return;
+    // X := trans.cast<float>() * src for the next NN pass (float, Eigen's order)
+    float Rf[9], tf[3];
+    for (int k = 0; k < 9; ++k) Rf[k] = (float)sh.R[k];
+    for (int k = 0; k < 3; ++k) tf[k] = (float)sh.t[k];
+    float4* X = w.X + (int64_t)p * w.x_stride;
+    for (int i = threadIdx.x; i < n; i += kGicpWG) {
+        const float4 s = src[i];
+        float o[3];
+        for (int r = 0; r < 3; ++r) {
+            float v = Rf[3 * r] * s.x;
+            v = v + Rf[3 * r + 1] * s.y;
+            v = v + Rf[3 * r + 2] * s.z;
+            o[r] = v + tf[r];
+        }
+        X[i] = make_float4(o[0], o[1], o[2], s.w);
+    }
+}
+
+__global__ void gicp_init_kernel(const float* guess, GicpState* gs, int npairs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npairs) return;
+    GicpState& s = gs[p];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) s.R[3 * r + c] = guess ? (double)guess[(int64_t)p * 16 + 4 * c + r] : (r == c ? 1.0 : 0.0);
+        s.t[r] = guess ? (double)guess[(int64_t)p * 16 + 12 + r] : 0.0;
+    }
+    s.lambda = -1.0;
+}
+
+// number of pairs still iterating -> *out (the host's early exit between runs of iterations)
+__global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out) {
+    __shared__ int32_t tot;
+    if (threadIdx.x == 0) tot = 0;
+    __syncthreads();
+    int c = 0;
+    for (int p = threadIdx.x; p < npairs; p += blockDim.x) c += st[p].phase == kPhaseActive;
+    if (c) atomicAdd(&tot, c);
+    __syncthreads();
+    if (threadIdx.x == 0) *out = tot;
+}
+
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(gicp_active_kernel, dim3(1), dim3(1024), 0, s, st, npairs, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gicp_init(const float* guess, GicpState* gs, int npairs, hipStream_t st) {
+    hipLaunchKernelGGL(gicp_init_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, guess, gs, npairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, int npairs, int max_n,
+                           int64_t stride, int k, int reg, double* cov, hipStream_t st) {
+    if (npairs <= 0 || max_n <= 0) return hipSuccess;
+    const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
+    if (k <= 8)
+        hipLaunchKernelGGL(gicp_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else if (k <= 16)
+        hipLaunchKernelGGL(gicp_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else if (k <= 32)
+        hipLaunchKernelGGL(gicp_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int it,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(gicp_iter_kernel, dim3(npairs), dim3(kGicpWG), 0, st, a, w, g, it);
+    return hipGetLastError();
+}
+
+}  // namespace icp4r

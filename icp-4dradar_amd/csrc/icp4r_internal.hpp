@@ -6,6 +6,7 @@
 
 #include "icp4r/icp4r.h"
 #include "icp4r/icp4r_ego.h"
+#include "icp4r/icp4r_gicp.h"
 #include "icp4r_math.hpp"
 
 namespace icp4r {
@@ -183,5 +184,27 @@ struct EgoArgs {
 };
 hipError_t launch_ego(const EgoArgs& e, int nscans, int max_n, float4* xyzi, hipStream_t st);
 hipError_t launch_ego_features(const EgoArgs& e, int nscans, int max_n, float4* xyzi, hipStream_t st);
+
+// ---- generalized ICP (icp4r_gicp.hip): fast_gicp's LsqRegistration state per pair
+struct GicpState {
+    double R[9], t[3];  // x0 (row-major rotation, translation)
+    double lambda;      // lm_lambda_ (< 0: not yet initialised)
+};
+struct GicpArgs {
+    GicpState* gs;        // [npairs]
+    const double* cov_src;  // [npairs * x_stride * 6] regularised source covariances (upper triangle)
+    const double* cov_tgt;  // [npairs * t_stride * 6]
+    double* mah;          // [npairs * x_stride * 6] Mahalanobis of the current correspondences
+    int64_t t_stride;
+    double max_d2;        // corr_dist_threshold_² (float) as double
+    double rot_eps, trans_eps, lm_init;
+    int32_t lm_max_iterations, max_iterations;
+};
+hipError_t launch_gicp_init(const float* guess, GicpState* gs, int npairs, hipStream_t st);
+hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, int npairs, int max_n,
+                           int64_t stride, int k, int reg, double* cov, hipStream_t st);
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s);
+hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int it,
+                            hipStream_t st);
 
 }  // namespace icp4r

@@ -32,7 +32,7 @@ library_path = os.path.join(HERE, "_lib", "libicp4r.so")
 OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 NUMERICS_PCL, NUMERICS_F64 = 0, 1
 NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED, NN_PRUNED = 0, 1, 2, 3
-STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH = 0, 1, 2, 3
+STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH, STAGE_GICP_COV = 0, 1, 2, 3, 4
 DBL_MAX = sys.float_info.max
 
 _STATUS = {OK: "ICP4R_OK", E_INVALID: "ICP4R_E_INVALID", E_EMPTY: "ICP4R_E_EMPTY",
@@ -50,6 +50,10 @@ EXPORTED_SYMBOLS = [
 # include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
 EGO_EXPORTED_SYMBOLS = [
     "icp4r_ego_params_default", "icp4r_radar_features", "icp4r_ego_velocity", "icp4r_ego_velocity_batch_device",
+]
+# include/icp4r/icp4r_gicp.h (generalized ICP; icp4r.gicp)
+GICP_EXPORTED_SYMBOLS = [
+    "icp4r_gicp_params_default", "icp4r_gicp_align", "icp4r_gicp_align_batch_device", "icp4r_gicp_covariances",
 ]
 # include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
 MAP_EXPORTED_SYMBOLS = [

@@ -171,12 +171,14 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx);
  * launch stream), and how many launches it averages.  ICP4R_STAGE_NN is what icp4r_kernel_time_ms
  * reports: the batched search kernel (nn_lds_kernel) of the LDS plan, the whole NN launch of the
  * others; ICP4R_STAGE_NN_TEST the cached-neighbour test kernel; ICP4R_STAGE_UPDATE the Umeyama /
- * convergence update; ICP4R_STAGE_BATCH a whole registration call. */
+ * convergence update (generalized ICP: its Gauss-Newton / LM iteration kernel); ICP4R_STAGE_BATCH a
+ * whole registration call; ICP4R_STAGE_GICP_COV the generalized ICP's covariance kernel. */
 typedef enum icp4r_stage {
     ICP4R_STAGE_NN = 0,
     ICP4R_STAGE_NN_TEST = 1,
     ICP4R_STAGE_UPDATE = 2,
-    ICP4R_STAGE_BATCH = 3
+    ICP4R_STAGE_BATCH = 3,
+    ICP4R_STAGE_GICP_COV = 4
 } icp4r_stage;
 int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* launches);
 

@@ -63,6 +63,17 @@ class OracleTrace(C.Structure):
     ]
 
 
+class GicpOracleParams(C.Structure):
+    _fields_ = [("k", C.c_int32), ("max_iterations", C.c_int32), ("rotation_epsilon", C.c_double),
+                ("transformation_epsilon", C.c_double), ("max_correspondence_distance", C.c_double),
+                ("regularization", C.c_int32), ("lm_max_iterations", C.c_int32), ("lm_init_lambda_factor", C.c_double)]
+
+
+class GicpOracleResult(C.Structure):
+    _fields_ = [("T", C.c_double * 16), ("iterations", C.c_int32), ("converged", C.c_int32),
+                ("lm_failed", C.c_int32), ("n_valid", C.c_int32)]
+
+
 _lib = None
 
 
@@ -110,6 +121,13 @@ def lib():
         L.ego_split_lsq.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double, C.c_void_p,
                                     C.c_void_p]
         L.ego_split_lsq.restype = C.c_int32
+        L.gicp_oracle_params_default.argtypes = [C.POINTER(GicpOracleParams)]
+        L.gicp_oracle_params_default.restype = None
+        L.gicp_oracle_covariances.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+        L.gicp_oracle_covariances.restype = None
+        L.gicp_oracle_align.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p,
+                                        C.POINTER(GicpOracleParams), C.POINTER(GicpOracleResult)]
+        L.gicp_oracle_align.restype = C.c_int
         _lib = L
     return _lib
 
@@ -256,3 +274,43 @@ def ego_split_lsq(feat: np.ndarray, A: float, b: float, dyn_threshold: float = 0
     ns = lib().ego_split_lsq(feat.ctypes.data if n else None, n, A, b, dyn_threshold, mask.ctypes.data if n else None,
                              V.ctypes.data)
     return V, mask, ns
+
+
+# ---- GICP (gicp_oracle.c)
+GICP_REG_NONE, GICP_REG_MIN_EIG, GICP_REG_NORMALIZED_MIN_EIG, GICP_REG_PLANE, GICP_REG_FROBENIUS = 0, 1, 2, 3, 4
+
+
+def gicp_params(**kw) -> GicpOracleParams:
+    p = GicpOracleParams()
+    lib().gicp_oracle_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _xyz4(a: np.ndarray) -> np.ndarray:
+    a = np.asarray(a, np.float32)
+    out = np.zeros((len(a), 4), np.float32)
+    out[:, :3] = a[:, :3]
+    return out
+
+
+def gicp_covariances(cloud: np.ndarray, k: int = 20, regularization: int = GICP_REG_PLANE) -> np.ndarray:
+    c = _xyz4(cloud)
+    out = np.zeros((len(c), 9), np.float64)
+    if len(c):
+        lib().gicp_oracle_covariances(c.ctypes.data, len(c), k, regularization, out.ctypes.data)
+    return out.reshape(-1, 3, 3)
+
+
+def gicp_align(src: np.ndarray, tgt: np.ndarray, guess: np.ndarray | None = None, **params) -> dict:
+    """FastGICPSingleThread restated: T (4x4 float64: the double x0; final_transformation_ is its
+    float), iterations (nr_iterations_), converged, lm_failed, n_valid."""
+    s, t = _xyz4(src), _xyz4(tgt)
+    p = gicp_params(**params)
+    r = GicpOracleResult()
+    g = None if guess is None else np.ascontiguousarray(np.asarray(guess, np.float64).reshape(16))
+    rc = lib().gicp_oracle_align(s.ctypes.data if len(s) else None, len(s), t.ctypes.data if len(t) else None,
+                                 len(t), g.ctypes.data if g is not None else None, C.byref(p), C.byref(r))
+    return {"rc": rc, "T": np.array(r.T, np.float64).reshape(4, 4), "iterations": r.iterations,
+            "converged": bool(r.converged), "lm_failed": bool(r.lm_failed), "n_valid": r.n_valid}

@@ -13,10 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r.h")
 MAP_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_map.h")
 EGO_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_ego.h")
+GICP_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_gicp.h")
 
 
 def header_functions(path=None):
-    paths = [path] if path else [HEADER, MAP_HEADER, EGO_HEADER]
+    paths = [path] if path else [HEADER, MAP_HEADER, EGO_HEADER, GICP_HEADER]
     names = set()
     for p in paths:
         names |= set(re.findall(r"^\s*(?:const\s+char\s*\*|int|void)\s+(icp4r_\w+)\s*\(", open(p).read(), re.M))
@@ -34,6 +35,7 @@ def test_library_exports_every_declared_symbol():
     assert sorted(icp4r.EXPORTED_SYMBOLS) == header_functions(HEADER)
     assert sorted(icp4r.MAP_EXPORTED_SYMBOLS) == header_functions(MAP_HEADER)
     assert sorted(icp4r.EGO_EXPORTED_SYMBOLS) == header_functions(EGO_HEADER)
+    assert sorted(icp4r.GICP_EXPORTED_SYMBOLS) == header_functions(GICP_HEADER)
 
 
 def test_nm_shows_c_linkage():
