@@ -1,0 +1,61 @@
+// icp4r_device.hpp — device-side helpers shared by the kernel translation units
+// (icp4r_kernels.hip, icp4r_gicp.hip): scalar-cache pointers, the XCD-aware work mapping, the
+// slotted work counters and the NN key.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "icp4r_internal.hpp"
+
+namespace icp4r {
+
+using v4f = float __attribute__((ext_vector_type(4)));
+// Target pointers are re-typed into the AMDGPU constant address space (4): with a wave-uniform
+// address every load becomes an s_load (scalar cache -> SGPRs) whatever alias analysis can prove.
+using cv4f_ptr = const __attribute__((address_space(4))) v4f*;
+
+// The address is also made PROVABLY wave-uniform (readfirstlane of both halves, once), so hipcc
+// keeps it in SGPRs instead of re-reading it with v_readfirstlane inside the sweep loop.
+__device__ __forceinline__ cv4f_ptr as_const(const float4* p) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return reinterpret_cast<cv4f_ptr>(((uint64_t)hi << 32) | lo);
+}
+
+// Wave-uniform scalar reads of per-pair metadata (read-only during a launch) via s_load, so counts,
+// offsets and loop bounds stay in SGPRs.
+template <typename T>
+__device__ __forceinline__ T uload(const T* p) {
+    return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
+// XCD-aware work mapping.  Workgroups are dispatched round-robin over the 8 XCDs (linear id mod 8),
+// each with its own L2.  Remap linear id L of `total` so that XCD x receives the contiguous work
+// range [x*per + min(x, rem), ...): every workgroup of a pair then runs on one XCD, and a pair's
+// target index / correspondence records are fetched into one L2 instead of eight.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+    const int per = total / kXcds, rem = total % kXcds;
+    const int xcd = L % kXcds, slot = L / kXcds;
+    return xcd * per + min(xcd, rem) + slot;
+}
+
+// Work counters: add v to counter k of this wave's slot.  Call from one lane.
+__device__ __forceinline__ void count_add(unsigned long long* ctr, int k, unsigned long long v) {
+    if (v == 0) return;
+    const uint32_t blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const uint32_t slot = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kCountSlots;
+    atomicAdd(ctr + (size_t)slot * kCountStride + k, v);
+}
+
+__device__ __forceinline__ NNKey make_key(float d2, uint32_t idx) {
+    return ((NNKey)__float_as_uint(d2) << 32) | idx;
+}
+
+// Box pruning is conservative in float: a box lower bound is shrunk by 2^-16 before its `<=` test
+// against a d², which covers the few-ulp rounding of both the bound and l2_simple.
+constexpr float kLbShrink = 1.0f - 1.0f / 65536.0f;
+
+}  // namespace icp4r

@@ -4,8 +4,9 @@
 // launch sequence per batch, on the ICP core's device machinery:
 //
 //   init_kernel + gicp_init        validate, X := guess * src, x0 := guess, lambda := -1
-//   index_kernel                   (pruned plans) Morton sort / block boxes of the targets, once
-//   gicp_cov x 2                   source and target covariances (calculate_covariances)
+//   covariances x 2                source and target (calculate_covariances): k-NN over each cloud's
+//                                  Morton index (pruned plans; the target's stays for the NN passes)
+//                                  or brute force
 //   repeat                         NN pass (exact 1-NN of X in the target) + gicp_iter_kernel
 //                                  (Mahalanobis, H / g, LM trials, x0 update, X := float(x0) src);
 //                                  every 4 iterations the host reads how many pairs still iterate
@@ -46,6 +47,24 @@ int check_params(const icp4r_gicp_params* p) {
     return ICP4R_OK;
 }
 
+// k-NN covariances of the clouds (cloud, off, cnt) of npairs pairs: pruned over a Morton index of each
+// cloud (index_kernel with the cloud as its target; w's index buffers must fit max_n points) when
+// the plan prunes, brute force otherwise (ICP4R_GICP_COV_BRUTE=1 forces brute force).
+int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, const float4* cloud, const int64_t* off,
+             const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st) {
+    if (pl.pruned && !icp4r_pipe::env_int("ICP4R_GICP_COV_BRUTE", 0)) {
+        PairArgs ai = a;
+        ai.tgt = cloud;
+        ai.tgt_off = off;
+        ai.tgt_n = cnt;
+        HIP_TRY(launch_index(ai, w, npairs, st));
+        HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, w, npairs, max_n, stride, k, reg, out, st));
+    } else {
+        HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, st));
+    }
+    return ICP4R_OK;
+}
+
 // The registration of a device-resident batch (pointers in `a`), results into a.results.
 int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m, const icp4r_gicp_params& gp,
              hipStream_t st) {
@@ -57,7 +76,10 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     pl.cache = false;  // gicp_iter_kernel moves X without maintaining the cached-neighbour bounds
     WorkArgs w;
     int rc;
-    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, false, st, w))) return rc;
+    // pruned plans index the source too (its k-NN covariances): the index strides fit both clouds
+    const int idx_m = pl.pruned ? (max_n > max_m ? max_n : max_m) : max_m;
+    if (pl.lds && idx_m > kLdsMaxTargets) pl.lds = false;  // the batched search stages t_stride targets
+    if ((rc = setup_work(ctx, pl, npairs, max_n, idx_m, false, st, w))) return rc;
     const int64_t xs = w.x_stride;
     const int64_t ts = mm;
     HIP_TRY(ctx->gicp_gs.ensure((size_t)npairs * sizeof(GicpState)));
@@ -84,14 +106,19 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     HIP_TRY(hipEventRecord(be->start, st));
     HIP_TRY(launch_init(a, w, npairs, st));
     HIP_TRY(launch_gicp_init(a.guess, g.gs, npairs, st));
-    if (pl.pruned) HIP_TRY(launch_index(a, w, npairs, st));
     EventPair* ce;
     if ((rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
+    double* cs = static_cast<double*>(ctx->gicp_cov_src.p);
+    double* ct = static_cast<double*>(ctx->gicp_cov_tgt.p);
     HIP_TRY(hipEventRecord(ce->start, st));
-    HIP_TRY(launch_gicp_cov(a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization,
-                            static_cast<double*>(ctx->gicp_cov_src.p), st));
-    HIP_TRY(launch_gicp_cov(a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization,
-                            static_cast<double*>(ctx->gicp_cov_tgt.p), st));
+    // source covariances first: the target's index (built last) stays for the NN passes
+    if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
+                       st)))
+        return rc;
+    if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
+                       st)))
+        return rc;
+    if (pl.pruned && icp4r_pipe::env_int("ICP4R_GICP_COV_BRUTE", 0)) HIP_TRY(launch_index(a, w, npairs, st));
     HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
     for (int it = 0; it < gp.max_iterations; ++it) {
@@ -267,9 +294,18 @@ int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_
     HIP_TRY(hipMemcpyAsync(ctx->src.p, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->src_off.p, &zero64, 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->src_n.p, &n, 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_gicp_cov(static_cast<const float4*>(ctx->src.p), static_cast<const int64_t*>(ctx->src_off.p),
-                            static_cast<const int32_t*>(ctx->src_n.p), 1, n, n, k, regularization,
-                            static_cast<double*>(ctx->gicp_cov_src.p), st));
+    PairArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = a.tgt = static_cast<const float4*>(ctx->src.p);
+    a.src_off = a.tgt_off = static_cast<const int64_t*>(ctx->src_off.p);
+    a.src_n = a.tgt_n = static_cast<const int32_t*>(ctx->src_n.p);
+    const icp4r_pipe::Plan pl = icp4r_pipe::make_plan(1, n, n, ICP4R_NN_AUTO);
+    WorkArgs w;
+    if ((rc = icp4r_pipe::setup_work(ctx, pl, 1, n, n, false, st, w))) return rc;
+    HIP_TRY(hipMemsetAsync(w.state, 0, sizeof(PairState), st));  // phase = active: index_kernel runs
+    if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, 1, n, n, k, regularization,
+                       static_cast<double*>(ctx->gicp_cov_src.p), st)))
+        return rc;
     std::vector<double> h6((size_t)n * 6);
     HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -3,10 +3,11 @@
 // fast_gicp's FastGICPSingleThread, as the reference's radar_odometry node runs it on the scan-to-map
 // path (radar_odometry.cpp:398-411), restated device-resident:
 //
-//   gicp_cov_kernel<K>   per point: exact K nearest neighbours in its own cloud (the point included;
-//                        (d², index) keys, the cloud streamed through LDS tiles), mean-centred
-//                        covariance in double, regularised (PLANE: U diag(1, 1, 1e-3) Uᵀ from a
-//                        cyclic-Jacobi eigendecomposition)
+//   gicp_knn_cov_kernel<K>  per point: exact K nearest neighbours in its own cloud (the point
+//   / gicp_cov_kernel<K>    included; (d², index) keys) — pruned over the ICP core's Morton index of
+//                        the cloud, or brute force through LDS tiles for small clouds — then the
+//                        mean-centred covariance in double, regularised (PLANE: U diag(1, 1, 1e-3) Uᵀ
+//                        from a cyclic-Jacobi eigendecomposition)
 //   per iteration        the exact NN pass of the ICP core (pruned / brute / LDS kernels, unchanged)
 //                        over X = float(x0) · src, then
 //   gicp_iter_kernel     one workgroup per pair: Mahalanobis M_i = (C_B + R C_A Rᵀ)⁻¹, the
@@ -24,7 +25,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "icp4r_device.hpp"
 #include "icp4r_internal.hpp"
+#include "icp4r_math.hpp"
 
 namespace icp4r {
 
@@ -125,6 +128,57 @@ __device__ void gicp_regularize(const double* c, int reg, double* o) {
         for (int s = 0; s < 3; ++s) o[3 * r + s] = V[3 * r] * v[0] * V[3 * s] + V[3 * r + 1] * v[1] * V[3 * s + 1] + V[3 * r + 2] * v[2] * V[3 * s + 2];
 }
 
+// mean-centred covariance of the kk nearest neighbours (sorted keys), divided by k as
+// calculate_covariances does, regularised; out: the upper triangle (xx, xy, xz, yy, yz, zz)
+// (the index is clamped to the cloud: an unfilled slot can never address outside it)
+template <int K>
+__device__ __forceinline__ void gicp_cov_from_knn(const uint64_t (&best)[K], int kk, int k, int reg, const float4* c,
+                                                  int n, double* out) {
+    double mean[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (s < kk) {
+            const float4 v = c[min((uint32_t)best[s], (uint32_t)(n - 1))];
+            mean[0] += (double)v.x;
+            mean[1] += (double)v.y;
+            mean[2] += (double)v.z;
+        }
+    }
+    for (int r = 0; r < 3; ++r) mean[r] /= (double)kk;
+    double cv[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        if (s < kk) {
+            const float4 v = c[min((uint32_t)best[s], (uint32_t)(n - 1))];
+            const double d[3] = {(double)v.x - mean[0], (double)v.y - mean[1], (double)v.z - mean[2]};
+            for (int r = 0; r < 3; ++r)
+                for (int t = 0; t < 3; ++t) cv[3 * r + t] += d[r] * d[t];
+        }
+    }
+    for (int t = 0; t < 9; ++t) cv[t] /= (double)k;
+    double o[9];
+    gicp_regularize(cv, reg, o);
+    out[0] = o[0];
+    out[1] = o[1];
+    out[2] = o[2];
+    out[3] = o[4];
+    out[4] = o[5];
+    out[5] = o[8];
+}
+
+// insert key into the ascending top-K list (registers: a fully unrolled compare-exchange chain)
+template <int K>
+__device__ __forceinline__ void knn_insert(uint64_t (&best)[K], uint64_t key) {
+    if (key < best[K - 1]) {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            const uint64_t lo = key < best[s] ? key : best[s];
+            key = key < best[s] ? best[s] : key;
+            best[s] = lo;
+        }
+    }
+}
+
 // ---- covariances
 constexpr int kCovWG = 256;
 constexpr int kCovTile = 1024;
@@ -150,52 +204,99 @@ __global__ __launch_bounds__(kCovWG) void gicp_cov_kernel(const float4* __restri
         __syncthreads();
         for (int t = 0; t < len; ++t) {
             const float4 v = tile[t];
-            const float dx = q.x - v.x, dy = q.y - v.y, dz = q.z - v.z;
-            float d2 = dx * dx;
-            d2 = d2 + dy * dy;
-            d2 = d2 + dz * dz;
-            uint64_t key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)(j0 + t);
-            if (key < best[K - 1]) {  // bubble into the sorted top-K (ascending (d², index))
-#pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    const uint64_t lo = key < best[s] ? key : best[s];
-                    key = key < best[s] ? best[s] : key;
-                    best[s] = lo;
-                }
-            }
+            const float d2 = l2_simple(q.x, q.y, q.z, v.x, v.y, v.z);
+            knn_insert<K>(best, make_key(d2, (uint32_t)(j0 + t)));
         }
     }
     if (i >= n) return;
-    const int kk = min(k, n);
-    double mean[3] = {0.0, 0.0, 0.0};
+    gicp_cov_from_knn<K>(best, min(k, n), k, reg, c, n, cov_out + ((int64_t)p * stride + i) * 6);
+}
+
+// Pruned exact k-NN over the cloud's own Morton index (index_kernel of the ICP core, built with the
+// cloud as target: tsort / tbox / sbox).  One query per lane, the queries of a wave Morton-contiguous
+// (sorted position = query); the wave walks superblocks outward from its own and skips a
+// (super)block whose box lower bound exceeds every lane's current K-th best d² (kLbShrink margin).
+// Keys are (d², index): the K smallest are exactly the brute-force set, ties to the lowest index.
+__device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, float x, float y, float z) {
+    const float gx = fmaxf(fmaxf(lo.x - x, x - hi.x), 0.0f);
+    const float gy = fmaxf(fmaxf(lo.y - y, y - hi.y), 0.0f);
+    const float gz = fmaxf(fmaxf(lo.z - z, z - hi.z), 0.0f);
+    return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
-    for (int s = 0; s < K; ++s) {
-        if (s >= kk) break;
-        const float4 v = c[(uint32_t)best[s]];
-        mean[0] += (double)v.x;
-        mean[1] += (double)v.y;
-        mean[2] += (double)v.z;
-    }
-    for (int r = 0; r < 3; ++r) mean[r] /= (double)kk;
-    double cv[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
+}
+__device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
-    for (int s = 0; s < K; ++s) {
-        if (s >= kk) break;
-        const float4 v = c[(uint32_t)best[s]];
-        const double d[3] = {(double)v.x - mean[0], (double)v.y - mean[1], (double)v.z - mean[2]};
-        for (int r = 0; r < 3; ++r)
-            for (int t = 0; t < 3; ++t) cv[3 * r + t] += d[r] * d[t];
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
+}
+
+template <int K>
+__global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __restrict__ cloud,
+                                                              const int64_t* __restrict__ off,
+                                                              const int32_t* __restrict__ cnt, WorkArgs w,
+                                                              int64_t stride, int k, int reg,
+                                                              double* __restrict__ cov_out) {
+    constexpr int B = 16;
+    const int chunks = gridDim.x;
+    const int g = xcd_remap(blockIdx.x + chunks * blockIdx.y, chunks * gridDim.y);
+    const int p = g / chunks, ch = g - p * chunks;
+    const int n = uload(cnt + p);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int base = ch * kCovWG + wave * 64;
+    if (base >= n) return;
+    const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
+    const float4 qv = tsg[min(base + lane, n - 1)];
+    const float x = qv.x, y = qv.y, z = qv.z;
+    // empty slots hold (+inf, ~0): a real d² bound for the pruning tests (all-ones bits would be a NaN
+    // d² that no box bound passes) that every finite key beats
+    uint64_t best[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) best[s] = make_key(INFINITY, 0xFFFFFFFFu);
+    float qlo[3] = {wave_min(x), wave_min(y), wave_min(z)};
+    float qhi[3] = {wave_max(x), wave_max(y), wave_max(z)};
+    float qmax = INFINITY;
+    const int nb = (n + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
+    const int sb0 = base / (B * kSuper);
+    const cv4f_ptr ts = as_const(tsg);
+    const cv4f_ptr tb = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
+    const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
+    auto maybe = [&](const v4f lo, const v4f hi) {
+        const float gx = fmaxf(fmaxf(lo.x - qhi[0], qlo[0] - hi.x), 0.0f);
+        const float gy = fmaxf(fmaxf(lo.y - qhi[1], qlo[1] - hi.y), 0.0f);
+        const float gz = fmaxf(fmaxf(lo.z - qhi[2], qlo[2] - hi.z), 0.0f);
+        return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx)) * kLbShrink <= qmax;
+    };
+    auto needed = [&](const v4f lo, const v4f hi) {
+        return __any(box_lb(lo, hi, x, y, z) * kLbShrink <= __uint_as_float((uint32_t)(best[K - 1] >> 32)));
+    };
+    int up = sb0, dn = sb0 - 1;
+    unsigned long long swept = 0;
+    for (int it = 0; it < nsb; ++it) {
+        const int sb = (up < nsb && (dn < 0 || !(it & 1))) ? up++ : dn--;
+        const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+        if (!maybe(slo, shi) || !needed(slo, shi)) continue;
+        for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {
+            const v4f blo = tb[2 * b], bhi = tb[2 * b + 1];
+            if (!maybe(blo, bhi) || !needed(blo, bhi)) continue;
+            const cv4f_ptr blk = ts + (int64_t)b * B;
+#pragma unroll
+            for (int t = 0; t < B; ++t) {
+                const v4f v = blk[t];
+                knn_insert<K>(best, make_key(l2_simple(x, y, z, v.x, v.y, v.z), __float_as_uint(v.w)));
+            }
+            ++swept;
+        }
+        qmax = wave_max(__uint_as_float((uint32_t)(best[K - 1] >> 32)));
     }
-    for (int t = 0; t < 9; ++t) cv[t] /= (double)k;
-    double o[9];
-    gicp_regularize(cv, reg, o);
-    double* out = cov_out + ((int64_t)p * stride + i) * 6;
-    out[0] = o[0];
-    out[1] = o[1];
-    out[2] = o[2];
-    out[3] = o[4];
-    out[4] = o[5];
-    out[5] = o[8];
+    if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, 64));
+    if (base + lane >= n) return;
+    const uint32_t oi = __float_as_uint(qv.w);
+    gicp_cov_from_knn<K>(best, min(k, n), k, reg, cloud + off[p], n, cov_out + ((int64_t)p * stride + oi) * 6);
 }
 
 // ---- per-iteration update
@@ -524,6 +625,22 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
         hipLaunchKernelGGL(gicp_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
     else if (k <= 32)
         hipLaunchKernelGGL(gicp_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
+                               int npairs, int max_n, int64_t stride, int k, int reg, double* cov, hipStream_t st) {
+    if (npairs <= 0 || max_n <= 0) return hipSuccess;
+    if (w.leaf != 16) return hipErrorInvalidValue;
+    const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
+    if (k <= 8)
+        hipLaunchKernelGGL(gicp_knn_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
+    else if (k <= 16)
+        hipLaunchKernelGGL(gicp_knn_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
+    else if (k <= 32)
+        hipLaunchKernelGGL(gicp_knn_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
