@@ -218,6 +218,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     if (pl.pruned) {
         const int64_t span = (int64_t)pl.leaf * kSuper;
         w.leaf = pl.leaf;
+        w.kd_index = env_int("ICP4R_KD", 3);  // bit 0: targets, bit 1: sources (0: Morton for both)
         w.t_stride = ((max_m > 0 ? max_m : 1) + span - 1) / span * span;
         w.b_stride = w.t_stride / pl.leaf;
         w.sb_stride = w.b_stride / kSuper;

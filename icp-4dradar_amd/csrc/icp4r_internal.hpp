@@ -101,13 +101,15 @@ struct WorkArgs {
     int64_t x_stride;   // >= max source points per pair
     int32_t splits;     // brute force: target splits per pair (1 for batches; >1 for single-pair latency)
     int32_t leaf;       // pruned: targets per block (16 or 32); 0 = brute force
+    int32_t kd_index;   // clouds of <= 8192 points get the balanced kd order (index_kernel), else Morton;
+                        // bit 0: targets, bit 1: sources
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):
-    float4* tsort;      // [npairs * t_stride] targets in Morton-cell order, .w = original index bits;
+    float4* tsort;      // [npairs * t_stride] targets in index order (kd / Morton), .w = original index bits;
                         // positions [m, t_stride): +inf coordinates (never a match)
     int32_t* tinv;      // [npairs * t_stride] original target index -> sorted position
     float4* tbox;       // [npairs * 2 * b_stride] per block: lo, hi (empty blocks: +inf, -inf)
     float4* sbox;       // [npairs * 2 * sb_stride] per superblock of kSuper blocks: lo, hi
-    int32_t* sperm;     // [npairs * x_stride] source indices in Morton-cell order
+    int32_t* sperm;     // [npairs * x_stride] source indices in index order (kd / Morton)
     int64_t t_stride, b_stride, sb_stride;
     float4* corr;       // PCL numerics: [npairs * x_stride * 2] per source point {s.xyz, w}, {d.xyz, d²}
     // Cached-neighbour test (nn_lds_kernel<true>; nullptr = off):

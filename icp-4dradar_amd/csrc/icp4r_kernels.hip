@@ -287,12 +287,59 @@ __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int f
 // ---------------------------------------------------------------------------------------------
 // index_kernel: the pruned search's per-pair index (once per registration; the target never moves
 // and a rigid motion keeps the source's spatial order).  blockIdx.x = pair, blockIdx.y = 0 target /
-// 1 source.  A counting sort over 2^14 Morton cells of the cloud's bounding box (x, y: 32 cells,
-// z: 16 — radar scans are flat) in LDS; order inside a cell is whatever the LDS atomics give, which
-// is fine: the search is exact for any order, the order only decides how well blocks prune.
+// 1 source.  The order only decides how well blocks prune — the search is exact for any order.
+//
+//  * n <= kKdMaxN (every scan of the benchmark): a balanced kd-tree order.  Segment [s, e) splits at
+//    the median of its widest axis into a left part of floor(units / 2) whole units (unit = one
+//    superblock of leaf * kSuper points while the segment is larger than that, else one leaf), so
+//    every block of `leaf` consecutive positions is a kd leaf and every superblock a kd subtree.
+//    Measured on the benchmark pairs (CPU model of the exact pruning, blocks whose box can reach
+//    the second-nearest distance): 2.4 blocks / 1.6 superblocks per query vs 6.6 / 4.7 for the
+//    Morton-cell order — the Morton blocks straddle cell boundaries and their boxes are long.
+//    Built in LDS with the classic presorted-lists method: the points sorted once per axis
+//    (bitonic, unique keys (coordinate, index), so deterministic), then per level a stable
+//    partition of all three lists by "left of the split", which keeps each list sorted inside
+//    every segment.
+//  * larger clouds (the C5 scan-to-map target): a counting sort over 2^14 Morton cells of the
+//    bounding box (x, y: 32 cells, z: 16 — radar scans are flat); order inside a cell is whatever
+//    the LDS atomics give.
 constexpr int kIdxWG = 1024;
 constexpr int kIdxWaves = kIdxWG / 64;
 constexpr int kCellBins = 1 << 14;
+constexpr int kKdMaxN = 8192;
+constexpr int kKdPer = kKdMaxN / kIdxWG;  // consecutive list positions per thread
+
+constexpr int kKdBins = 2048;             // counting-sort bins per axis (11-bit quantised coordinate)
+
+struct KdShared {
+    uint16_t L[3][kKdMaxN];  // per axis: the point indices, sorted by that axis inside every segment
+    uint16_t q[3][kKdMaxN];  // per point: its quantised coordinates (the sort keys; segment extents)
+    union {
+        uint32_t hist[3][kKdBins];  // the per-axis counting sorts
+        struct {
+            uint8_t left[kKdMaxN];     // per point: left of its segment's split
+            uint16_t tpre[3][kIdxWG];  // per list: exclusive prefix of "left" at each thread's first position
+        } p;
+        float4 bbox[2 * kKdMaxN / 16];  // index_kernel: block boxes (lo, hi) for the superblock boxes
+    } u;
+    uint16_t seg_mid[kIdxWG];  // per segment, at the thread owning its first position: split position
+    uint8_t seg_ax[kIdxWG];    // ... and axis (3: leaf)
+    alignas(16) uint16_t wsum[3][kIdxWaves];
+    float red[kIdxWaves][6];
+    float lo[3], sc[3];
+};
+
+struct MortonShared {
+    uint32_t bins[kCellBins];
+    float red[kIdxWaves][6];
+    uint32_t wsum[kIdxWaves];
+    float lo_s[3], sc_s[3];
+};
+
+union IndexShared {
+    KdShared kd;
+    MortonShared mo;
+};
 
 __device__ __forceinline__ uint32_t cell_code(float x, float y, float z, const float* lo, const float* sc) {
     const int cx = min(31, max(0, (int)((x - lo[0]) * sc[0])));
@@ -308,11 +355,256 @@ __device__ __forceinline__ uint32_t cell_code(float x, float y, float z, const f
     return c;
 }
 
+// float -> u32 with the same order (finite inputs)
+__device__ __forceinline__ uint32_t ord_key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// The split of segment [s, e) (see above): left part [s, s + h); h = 0 for a leaf.
+__device__ __forceinline__ int kd_split(int S, int leaf) {
+    if (S <= leaf) return 0;
+    const int unit = S > leaf * kSuper ? leaf * kSuper : leaf;
+    return (((S + unit - 1) / unit) >> 1) * unit;
+}
+
+// Balanced kd order of pts[0, n) (n <= kKdMaxN) into sh.L[0][0, n).  The per-axis orders are
+// counting sorts of the coordinate quantised to kKdBins levels over the cloud's extent; the order
+// of equal keys (LDS atomics) is arbitrary, which only moves points between the two sides of a
+// split among equals — the search is exact for any order.
+__device__ void kd_order(KdShared& sh, const float4* pts, int n, int leaf, uint64_t* tk) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
+    // 1. bounding box -> quantisation
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = tid; i < n; i += kIdxWG) {
+        const float4 v = pts[i];
+        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
+        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], off, 64));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off, 64));
+        }
+    if (lane == 0)
+        for (int k = 0; k < 3; ++k) {
+            sh.red[wave][k] = mn[k];
+            sh.red[wave][3 + k] = mx[k];
+        }
+    for (int b = tid; b < 3 * kKdBins; b += kIdxWG) (&sh.u.hist[0][0])[b] = 0;
+    __syncthreads();
+    if (tid < 3) {
+        float l = INFINITY, h = -INFINITY;
+        for (int v = 0; v < kIdxWaves; ++v) {
+            l = fminf(l, sh.red[v][tid]);
+            h = fmaxf(h, sh.red[v][3 + tid]);
+        }
+        sh.lo[tid] = l;
+        sh.sc[tid] = h > l ? (float)kKdBins / (h - l) : 0.0f;
+    }
+    __syncthreads();
+    const float lo[3] = {sh.lo[0], sh.lo[1], sh.lo[2]}, sc[3] = {sh.sc[0], sh.sc[1], sh.sc[2]};
+    auto bin = [&](float c, int ax) { return min(kKdBins - 1, max(0, (int)((c - lo[ax]) * sc[ax]))); };
+    // 2. three counting sorts at once: histogram, exclusive scan, scatter
+    for (int i = tid; i < n; i += kIdxWG) {
+        const float4 v = pts[i];
+        atomicAdd(&sh.u.hist[0][bin(v.x, 0)], 1u);
+        atomicAdd(&sh.u.hist[1][bin(v.y, 1)], 1u);
+        atomicAdd(&sh.u.hist[2][bin(v.z, 2)], 1u);
+    }
+    __syncthreads();
+    {
+        constexpr int per = 3 * kKdBins / kIdxWG;  // 6 bins per thread; an axis = 2048 / 6 threads (not whole)
+        static_assert(3 * kKdBins % kIdxWG == 0, "bins per thread");
+        uint32_t* hb = &sh.u.hist[0][0];
+        uint32_t loc[per], run = 0;
+        // scan each axis separately: a thread's bins may straddle two axes, so carry the axis start
+#pragma unroll
+        for (int k = 0; k < per; ++k) {
+            const int gb = tid * per + k;
+            loc[k] = run;
+            run += hb[gb];
+        }
+        uint32_t incl = run;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        if (lane == 63) sh.red[wave][0] = __uint_as_float(incl);  // (the bbox partials are consumed)
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (int v = 0; v < wave; ++v) wbase += __float_as_uint(sh.red[v][0]);
+        const uint32_t tbase = wbase + incl - run;  // exclusive prefix over all 3 axes' bins
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < per; ++k) {
+            const int gb = tid * per + k;
+            hb[gb] = tbase + loc[k] - (uint32_t)(gb / kKdBins) * (uint32_t)n;  // axis a's bins start at a * n
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kIdxWG) {
+        const float4 v = pts[i];
+        const int bx = bin(v.x, 0), by = bin(v.y, 1), bz = bin(v.z, 2);
+        sh.L[0][atomicAdd(&sh.u.hist[0][bx], 1u)] = (uint16_t)i;
+        sh.L[1][atomicAdd(&sh.u.hist[1][by], 1u)] = (uint16_t)i;
+        sh.L[2][atomicAdd(&sh.u.hist[2][bz], 1u)] = (uint16_t)i;
+        sh.q[0][i] = (uint16_t)bx;
+        sh.q[1][i] = (uint16_t)by;
+        sh.q[2][i] = (uint16_t)bz;
+    }
+    __syncthreads();
+    if (tk) tk[1] = __builtin_amdgcn_s_memrealtime();
+    // 3. levels: split every non-leaf segment at the median of its widest axis.  Segment bounds are
+    // multiples of 16 >= kKdPer, so a thread's positions [p0, p0 + kKdPer) share one segment [s, e),
+    // tracked per thread; the thread owning a segment's first position decides its split.
+    const int p0 = tid * kKdPer;
+    int s = 0, e = n;
+    for (;;) {
+        bool any = false;
+        if (p0 == s && p0 < n) {
+            const int h = kd_split(e - s, leaf);
+            uint8_t ax = 3;
+            if (h) {
+                float ext[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) ext[a] = (float)(sh.q[a][sh.L[a][e - 1]] - sh.q[a][sh.L[a][s]]) / sc[a];
+                ax = ext[0] >= ext[1] && ext[0] >= ext[2] ? 0 : (ext[1] >= ext[2] ? 1 : 2);
+                any = true;
+            }
+            sh.seg_mid[tid] = (uint16_t)(s + h);
+            sh.seg_ax[tid] = ax;
+        }
+        if (!__syncthreads_or(any)) {
+            if (tk) tk[2] = __builtin_amdgcn_s_memrealtime();
+            break;
+        }
+        int mid = 0, ax = 3;
+        if (p0 < n) {
+            mid = sh.seg_mid[s / kKdPer];
+            ax = sh.seg_ax[s / kKdPer];
+        }
+        // this thread's list entries (one 16-B LDS read per list; entries >= n are never used)
+        uint16_t v[3][kKdPer];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[a][p0]);
+            const uint32_t w4[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int k = 0; k < kKdPer / 2; ++k) {
+                v[a][2 * k] = (uint16_t)(w4[k] & 0xffffu);
+                v[a][2 * k + 1] = (uint16_t)(w4[k] >> 16);
+            }
+        }
+        const int nv = min(kKdPer, n - p0);  // valid entries (<= 0: none)
+        if (ax < 3)  // "left" per point, from the split axis' list
+#pragma unroll
+            for (int k = 0; k < kKdPer; ++k)
+                if (k < nv) sh.u.p.left[ax == 0 ? v[0][k] : (ax == 1 ? v[1][k] : v[2][k])] = p0 + k < mid;  // (no dynamic register index: scratch)
+        __syncthreads();
+        // stable partition of the three lists: exclusive prefix of "left" in list order; the flags
+        // of this thread's entries as bit masks (the split axis' own need no gather)
+        uint32_t fb[3] = {0u, 0u, 0u};
+        if (ax < 3)
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int k = 0; k < kKdPer; ++k) {
+                    const uint32_t f = k >= nv ? 0u : (a == ax ? (uint32_t)(p0 + k < mid) : (uint32_t)sh.u.p.left[v[a][k]]);
+                    fb[a] |= f << k;
+                }
+        const int cnt[3] = {__builtin_popcount(fb[0]), __builtin_popcount(fb[1]), __builtin_popcount(fb[2])};
+        int incl[3] = {cnt[0], cnt[1], cnt[2]};
+        for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int o = __shfl_up(incl[a], off, 64);
+                if (lane >= off) incl[a] += o;
+            }
+        if (lane == 63)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) sh.wsum[a][wave] = (uint16_t)incl[a];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sh.u.p.tpre[a][tid] = (uint16_t)(incl[a] - cnt[a]);  // in-wave exclusive
+        __syncthreads();  // wave totals and in-wave prefixes visible; every thread holds its entries in v
+        const int sw = (s / kKdPer) >> 6;  // the wave owning the segment's first position
+        if (nv > 0 && ax < 3) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (a == ax) continue;  // already partitioned: every entry stays where it is
+                // the wave totals before `wave` and before `sw` (16 u16 in two LDS reads)
+                const uint4 w0 = *reinterpret_cast<const uint4*>(&sh.wsum[a][0]);
+                const uint4 w1 = *reinterpret_cast<const uint4*>(&sh.wsum[a][8]);
+                const uint32_t ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                int bw = 0, bs = 0;
+#pragma unroll
+                for (int k = 0; k < kIdxWaves; ++k) {
+                    const int c = (int)((ww[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+                    bw += k < wave ? c : 0;
+                    bs += k < sw ? c : 0;
+                }
+                // "left" points before p0 inside the segment
+                int ones = (bw + incl[a] - cnt[a]) - (bs + (int)sh.u.p.tpre[a][s / kKdPer]);
+#pragma unroll
+                for (int k = 0; k < kKdPer; ++k) {
+                    if (k >= nv) break;
+                    const int f = (fb[a] >> k) & 1;
+                    const int np = f ? s + ones : mid + (p0 + k - s) - ones;
+                    ones += f;
+                    sh.L[a][np] = v[a][k];
+                }
+            }
+            if (p0 < mid) e = mid;
+            else s = mid;
+        }
+        __syncthreads();
+    }
+}
+
+__device__ void index_boxes(const WorkArgs& w, int p, int n) {
+    const int tid = threadIdx.x;
+    float4* ts = w.tsort + (int64_t)p * w.t_stride;
+    __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
+    // 5. tail duplicates, block boxes, superblock boxes
+    // padding: +inf coordinates (d² = +inf never beats a real target, and no padding entry
+    // can pose as a second-nearest duplicate of a real one); .w = the last target's index
+    const float4 last = ts[n - 1];
+    for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = make_float4(INFINITY, INFINITY, INFINITY, last.w);
+    const int B = w.leaf;
+    const int nb = (n + B - 1) / B;
+    float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+    for (int b = tid; b < w.b_stride; b += kIdxWG) {
+        float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        if (b < nb) {
+            const int e = min(n, (b + 1) * B);
+            for (int k = b * B; k < e; ++k) {
+                const float4 v = ts[k];
+                l.x = fminf(l.x, v.x); l.y = fminf(l.y, v.y); l.z = fminf(l.z, v.z);
+                h.x = fmaxf(h.x, v.x); h.y = fmaxf(h.y, v.y); h.z = fmaxf(h.z, v.z);
+            }
+        }
+        tb[2 * b] = l;
+        tb[2 * b + 1] = h;
+    }
+    __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
+    float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
+    for (int s = tid; s < w.sb_stride; s += kIdxWG) {
+        float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        for (int b = s * kSuper; b < (s + 1) * kSuper; ++b) {
+            const float4 bl = tb[2 * b], bh = tb[2 * b + 1];
+            l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
+            h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
+        }
+        sbx[2 * s] = l;
+        sbx[2 * s + 1] = h;
+    }
+}
+
 __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
-    __shared__ uint32_t bins[kCellBins];
-    __shared__ float red[kIdxWaves][6];
-    __shared__ uint32_t wsum[kIdxWaves];
-    __shared__ float lo_s[3], sc_s[3];
+    __shared__ IndexShared shu;
     const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * 2);
     const int p = g >> 1;
     const bool is_tgt = (g & 1) == 0;
@@ -321,6 +613,74 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
     if (n <= 0) return;
     const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
+    if ((w.kd_index & (is_tgt ? 1 : 2)) && n <= kKdMaxN && (!is_tgt || w.t_stride <= kKdMaxN)) {
+        uint64_t* tk = (w.ticks && p == 0 && is_tgt && tid == 0) ? w.ticks + 12 : nullptr;
+        kd_order(shu.kd, pts, n, is_tgt ? w.leaf : 16, tk);
+        const uint16_t* ord = shu.kd.L[0];
+        if (is_tgt) {
+            // sorted targets, padding (+inf coordinates, .w = the last target's index: never a match,
+            // never a second-nearest duplicate), and block boxes reduced over `leaf` adjacent lanes
+            float4* ts = w.tsort + (int64_t)p * w.t_stride;
+            int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+            float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+            const float lastw = __uint_as_float((uint32_t)ord[n - 1]);
+            const int B = w.leaf;
+            for (int pos = tid; pos < (int)w.t_stride; pos += kIdxWG) {
+                float4 v = make_float4(INFINITY, INFINITY, INFINITY, lastw);
+                float4 l = v, h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+                if (pos < n) {
+                    const int i = ord[pos];
+                    const float4 c = pts[i];
+                    v = make_float4(c.x, c.y, c.z, __uint_as_float((uint32_t)i));
+                    tinv[i] = pos;
+                    l = v;
+                    h = v;
+                }
+                ts[pos] = v;
+                for (int off = 1; off < B; off <<= 1) {
+                    l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
+                    l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
+                    l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
+                }
+                if ((lane & (B - 1)) == 0) {
+                    const int b = pos / B;
+                    l.w = 0.f;
+                    h.w = 0.f;
+                    tb[2 * b] = l;
+                    tb[2 * b + 1] = h;
+                    shu.kd.u.bbox[2 * b] = l;
+                    shu.kd.u.bbox[2 * b + 1] = h;
+                }
+            }
+            __syncthreads();
+            float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
+            for (int sb = tid; sb < w.sb_stride; sb += kIdxWG) {
+                float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+                for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {
+                    const float4 bl = shu.kd.u.bbox[2 * b], bh = shu.kd.u.bbox[2 * b + 1];
+                    l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
+                    h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
+                }
+                sbx[2 * sb] = l;
+                sbx[2 * sb + 1] = h;
+            }
+            if (tk) tk[3] = __builtin_amdgcn_s_memrealtime();
+        } else {
+            int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
+            int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
+            for (int pos = tid; pos < n; pos += kIdxWG) {
+                const int i = ord[pos];
+                sp[pos] = i;
+                if (si) si[i] = pos;
+            }
+        }
+        return;
+    }
+    uint32_t* bins = shu.mo.bins;
+    float(*red)[6] = shu.mo.red;
+    uint32_t* wsum = shu.mo.wsum;
+    float* lo_s = shu.mo.lo_s;
+    float* sc_s = shu.mo.sc_s;
     // 1. bounding box
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = tid; i < n; i += kIdxWG) {
@@ -392,40 +752,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             ts[pos] = make_float4(v.x, v.y, v.z, __uint_as_float((uint32_t)i));
             tinv[i] = (int32_t)pos;
         }
-        __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
-        // 5. tail duplicates, block boxes, superblock boxes
-        // padding: +inf coordinates (d² = +inf never beats a real target, and no padding entry
-        // can pose as a second-nearest duplicate of a real one); .w = the last target's index
-        const float4 last = ts[n - 1];
-        for (int64_t pos = n + tid; pos < w.t_stride; pos += kIdxWG) ts[pos] = make_float4(INFINITY, INFINITY, INFINITY, last.w);
-        const int B = w.leaf;
-        const int nb = (n + B - 1) / B;
-        float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
-        for (int b = tid; b < w.b_stride; b += kIdxWG) {
-            float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-            if (b < nb) {
-                const int e = min(n, (b + 1) * B);
-                for (int k = b * B; k < e; ++k) {
-                    const float4 v = ts[k];
-                    l.x = fminf(l.x, v.x); l.y = fminf(l.y, v.y); l.z = fminf(l.z, v.z);
-                    h.x = fmaxf(h.x, v.x); h.y = fmaxf(h.y, v.y); h.z = fmaxf(h.z, v.z);
-                }
-            }
-            tb[2 * b] = l;
-            tb[2 * b + 1] = h;
-        }
-        __syncthreads();  // workgroup-scope release/acquire: the scatter above is visible to this WG
-        float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
-        for (int s = tid; s < w.sb_stride; s += kIdxWG) {
-            float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-            for (int b = s * kSuper; b < (s + 1) * kSuper; ++b) {
-                const float4 bl = tb[2 * b], bh = tb[2 * b + 1];
-                l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
-                h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
-            }
-            sbx[2 * s] = l;
-            sbx[2 * s + 1] = h;
-        }
+        index_boxes(w, p, n);
     } else {
         int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
         int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
