@@ -204,7 +204,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
-        const size_t nt = 16 + 4 * (size_t)npairs;
+        const size_t nt = 32 + 4 * (size_t)npairs;  // (see the kernels' debug tick slots)
         if (ctx->ticks.cap < nt * sizeof(uint64_t)) {
             HIP_TRY(ctx->ticks.ensure(nt * sizeof(uint64_t)));
             HIP_TRY(hipMemsetAsync(ctx->ticks.p, 0, nt * sizeof(uint64_t), st));
@@ -233,8 +233,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.sbox = static_cast<float4*>(ctx->sbox.p);
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
         if (pl.lds) {
-            HIP_TRY(ctx->plist.ensure((size_t)npairs * sizeof(int32_t)));
-            HIP_TRY(ctx->plist_n.ensure(2 * sizeof(int32_t)));
+            HIP_TRY(ctx->plist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
+            HIP_TRY(ctx->plist_n.ensure(4 * sizeof(int32_t)));  // items, queue, part size
             w.plist = static_cast<int32_t*>(ctx->plist.p);
             w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
             w.queue = w.plist_n + 1;
@@ -254,6 +254,15 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.qlist = static_cast<int32_t*>(ctx->qlist.p);
             w.need = static_cast<uint32_t*>(ctx->need.p);
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
+            w.light_max = env_int("ICP4R_LIGHT_MAX", kDefaultLightMax);
+            w.part_size = env_int("ICP4R_PART", kDefaultPartSize);
+            if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
+            if (w.light_max > 0) {
+                HIP_TRY(ctx->ilist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
+                HIP_TRY(ctx->ilist_n.ensure(2 * sizeof(int32_t)));
+                w.ilist = static_cast<int32_t*>(ctx->ilist.p);
+                w.ilist_n = static_cast<int32_t*>(ctx->ilist_n.p);
+            }
             // the search clears what it consumed; a fresh registration starts from zero anyway
             HIP_TRY(hipMemsetAsync(w.need, 0, (size_t)npairs * w.need_stride * sizeof(uint32_t), st));
             HIP_TRY(hipMemsetAsync(w.miss_cnt, 0, (size_t)npairs * sizeof(int32_t), st));
@@ -450,7 +459,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
-                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
+                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ilist, &ctx->ilist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})
         b->release();

@@ -16,6 +16,8 @@ constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_ke
 constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.py)
 constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
+constexpr int kDefaultLightMax = 0;  // batched search: pairs with at most this many misses -> nn_light_kernel (0: off; measured slower)
+constexpr int kDefaultPartSize = 1024;  // batched search: misses per work item of a heavy pair  // batched search: pairs with at most this many misses -> nn_light_kernel
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
 constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
@@ -124,9 +126,16 @@ struct WorkArgs {
     int64_t need_stride;
     int32_t* miss_cnt;  // [npairs] misses of the current pass (cleared by the search)
     // Batched search (nn_lds_kernel): the pass's pair work list, heaviest first, and its queue
-    int32_t* plist;     // [npairs]
-    int32_t* plist_n;   // [1]
+    int32_t* plist;     // [npairs * ceil(x_stride / 64)] items (pair << 10 | part)
+    int32_t* plist_n;   // [4]: items, (queue), the pass's part size (nn_order_kernel)
     int32_t* queue;     // [1] next work-list index (reset by nn_order_kernel)
+    // nn_light_kernel (nullptr = off): items (pair << 10 | chunk of 64 misses) of the pairs with
+    // 1..light_max misses; ilist_n[0] = items, ilist_n[1] = the light queue
+    int32_t* ilist;     // [npairs * ceil(x_stride / 64)]
+    int32_t* ilist_n;   // [2]
+    int32_t light_max;
+    int32_t part_size;  // nn_lds_kernel: misses per work item of a heavy pair (0: one item per pair);
+                        // plist holds items (pair << 10 | part)
     unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,
                                 // cached-neighbour hits (count_add; the host sums the slots)
     uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase

@@ -1014,6 +1014,15 @@ __device__ __forceinline__ bool pass_wants(int phase, int fitness_pass) {
     return fitness_pass ? (phase != kPhaseInvalid) : (phase == kPhaseActive);
 }
 
+// The update that follows an NN pass clears the pair's miss bitmap and count (the next test kernel
+// ORs into them; nn_light_kernel's work items all read the bitmap, so none of them can clear it).
+__device__ __forceinline__ void clear_need(const WorkArgs& w, int p, int n, int tid, int nthreads) {
+    if (!w.need) return;
+    uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+    for (int k = tid; k < (n + 31) >> 5; k += nthreads) gneed[k] = 0u;
+    if (tid == 0) w.miss_cnt[p] = 0;
+}
+
 // ---- nn_cache_test_kernel: grid (chunks of kTestWG * kTestPer queries, npairs), XCD-aware.
 constexpr int kTestWG = 256;
 constexpr int kTestPer = 8;
@@ -1107,16 +1116,55 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
 // CACHE), work = its source count.
 constexpr int kOrderWG = 1024;
 constexpr int kOrderBuckets = 32;
+constexpr int kLightWG = 256;
+constexpr int kLightQ = 64;  // nn_light_kernel: queries per work item
+constexpr int kLightChunkBits = 10;
+static_assert(kCacheMaxN / kLightQ <= (1 << kLightChunkBits), "chunk field");
+constexpr int kLightCand = 64;  // nn_light_kernel: candidate blocks per query held in LDS
 
 __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
-                                                            int all) {
+                                                            int all, int ncu) {
     __shared__ int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
+    __shared__ int32_t nitem;
+    __shared__ unsigned long long tot_s;
     const int tid = threadIdx.x;
     if (tid < kOrderBuckets) bcnt[tid] = 0;
+    if (tid == 0) {
+        nitem = 0;
+        tot_s = 0;
+    }
     __syncthreads();
+    if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
+        unsigned long long t = 0;
+        for (int p = tid; p < npairs; p += kOrderWG)
+            t += pass_wants(w.state[p].phase, fitness_pass) ? (unsigned long long)w.miss_cnt[p] : 0ull;
+        t = wave_sum(t);
+        if ((tid & 63) == 0) atomicAdd(&tot_s, t);
+    }
+    __syncthreads();
+    // light: a pair with 1..light_max misses goes to nn_light_kernel as ceil(misses / 64) items
+    const bool light_ok = !all && w.ilist != nullptr;
+    auto work = [&](int p) {
+        return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
+    };
+    // a heavy pair's misses are cut into parts of part_size (first pass: one part, all queries), so
+    // the few slowly converging pairs with thousands of misses spread over several CUs
+    // (at least part_size, and large enough that the pass has about 2 items per CU: a part costs a
+    // target staging, so only the heavy tail of a light pass is worth cutting)
+    const int ps = (!all && w.part_size > 0) ? max(w.part_size, (int)((tot_s + 2ull * ncu - 1) / (2ull * ncu))) : (1 << 30);
+    auto heavy_parts = [&](int c) { return (c + ps - 1) / ps; };
+    auto heavy_size = [&](int c, int k) { return min(ps, c - k * ps); };
     for (int p = tid; p < npairs; p += kOrderWG) {
-        const int c = !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
-        if (c > 0) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)c)], 1);
+        const int c = work(p);
+        if (w.ticks) w.ticks[32 + p] = (uint64_t)c;  // debug: this pass' work per pair (tools/miss_hist.py)
+        if (c <= 0) continue;
+        if (light_ok && c <= w.light_max) {
+            const int ni = (c + kLightQ - 1) / kLightQ;
+            const int at = atomicAdd(&nitem, ni);
+            for (int k = 0; k < ni; ++k) w.ilist[at + k] = (p << kLightChunkBits) | k;
+        } else {
+            for (int k = 0, np = heavy_parts(c); k < np; ++k) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1);
+        }
     }
     __syncthreads();
     if (tid == 0) {
@@ -1127,11 +1175,206 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
         }
         *w.plist_n = run;
         *w.queue = 0;
+        w.plist_n[2] = ps == (1 << 30) ? 0 : ps;  // nn_lds_kernel: misses per part (0: whole pairs)
+        if (w.ilist) {
+            w.ilist_n[0] = nitem;
+            w.ilist_n[1] = 0;
+        }
     }
     __syncthreads();
     for (int p = tid; p < npairs; p += kOrderWG) {
-        const int c = !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
-        if (c > 0) w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)c)], 1)] = p;
+        const int c = work(p);
+        if (c > 0 && !(light_ok && c <= w.light_max))
+            for (int k = 0, np = heavy_parts(c); k < np; ++k)
+                w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1)] = (p << kLightChunkBits) | k;
+    }
+}
+
+// ---- nn_light_kernel: the cached-neighbour misses of pairs with few of them (<= light_max).
+// Each query is searched on its own by a 16-lane group straight from the index, with the pair's
+// block and superblock boxes staged in LDS: the pruning bound is known up front (U of the previous
+// search: an upper bound of the second-nearest distance), so the superblock tests (4 per lane), the
+// block tests (8 lanes per superblock) and the evaluations (lane gl takes target gl of a candidate
+// block, 4 blocks' loads in flight) are lane-parallel; after each candidate list the bound drops to
+// the second-nearest found so far.  The result is the same exact (best key, second-nearest) pair as
+// nn_lds_kernel<true> (tests/test_gpu_parity.py::test_light_search_identical).  Work items
+// (pair << 10 | chunk) of <= 64 queries come from nn_order_kernel.
+// Off by default (light_max = 0): on the C3 workload it adds ~40 us per pass while the LDS search
+// it relieves is bound by its heavy pairs, not by the light ones.
+__global__ __launch_bounds__(kLightWG) void nn_light_kernel(PairArgs a, WorkArgs w) {
+    __shared__ v4f boxes[2 * (kLdsTargets / kLdsLeaf)];  // the pair's block boxes (lo, hi)
+    __shared__ v4f sboxes[2 * (kLdsTargets / kLdsLeaf / kSuper)];
+    __shared__ int16_t cand[kLightWG / 16][kLightCand];  // per group: candidate blocks of its query
+    __shared__ int32_t qs[kLightQ];
+    __shared__ int32_t wtot[kLightWG / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int gl = tid & 15, gw = (tid >> 4) & 3, g = tid >> 4;  // lane in group, group in wave, group
+    const int nitems = uload(w.ilist_n);
+    unsigned long long evals = 0, tests = 0;
+    // items are near-equal (<= 64 queries): a static round-robin, no shared queue counter (thousands
+    // of workgroups on one atomic word serialise at its L2 channel: ~40 us per launch, measured)
+    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const int item = w.ilist[it];
+        const int p = item >> kLightChunkBits, lo = (item & ((1 << kLightChunkBits) - 1)) * kLightQ;
+        const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+        const int64_t xs = w.x_stride;
+        const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
+        {  // the pair's boxes into LDS (all loads first)
+            const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
+            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+            constexpr int PB = 2 * (kLdsTargets / kLdsLeaf) / kLightWG;
+            v4f t[PB];
+#pragma unroll
+            for (int k = 0; k < PB; ++k) t[k] = tbv[min(tid + k * kLightWG, 2 * nb - 1)];
+            const v4f sv = sbv[min(tid, 2 * nsb - 1)];
+#pragma unroll
+            for (int k = 0; k < PB; ++k)
+                if (tid + k * kLightWG < 2 * nb) boxes[tid + k * kLightWG] = t[k];
+            if (tid < 2 * nsb) sboxes[tid] = sv;
+        }
+        // misses with rank [lo, lo + kLightQ) in index order, from the pair's bitmap
+        {
+            constexpr int W = kNeedWords / kLightWG;
+            const int nwords = (n + 31) >> 5;
+            const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+            const int32_t* sperm = w.sperm + (int64_t)p * xs;
+            uint32_t f[W];
+            int c = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const int wi = tid * W + k;
+                f[k] = wi < nwords ? gneed[wi] : 0u;
+                c += __builtin_popcount(f[k]);
+            }
+            int incl = c;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int o = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += o;
+            }
+            if (lane == 63) wtot[wave] = incl;
+            __syncthreads();
+            int r = incl - c;
+            for (int v = 0; v < wave; ++v) r += wtot[v];
+            if (r < lo + kLightQ && r + c > lo) {
+#pragma unroll
+                for (int k = 0; k < W; ++k) {
+                    uint32_t bits = f[k];
+                    while (bits) {
+                        const int b = __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        if (r >= lo && r < lo + kLightQ) qs[r - lo] = sperm[(tid * W + k) * 32 + b];
+                        ++r;
+                    }
+                }
+            }
+        }
+        const int total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        const int cnt = min(kLightQ, total - lo);
+        __syncthreads();  // qs, boxes complete; wtot is rewritten only after the next barrier
+        const float4* ts = w.tsort + (int64_t)p * w.t_stride;
+        const float4* tgt = a.tgt + uload(a.tgt_off + p);
+        for (int j = g; j < cnt; j += kLightWG / 16) {  // group-uniform
+            const int o = qs[j];
+            const int64_t slot = (int64_t)p * xs + o;
+            const float4 X = w.X[slot];
+            // pruning bound: U of the previous search, moved since — an upper bound of the
+            // second-nearest distance, so every target that can be the nearest or the second-nearest
+            // lies within it
+            const float u = w.nn_lu[slot].y;
+            const float bnd = u * u * 1.00001f;
+            auto lbox = [&](const v4f l, const v4f h, float bound) {
+                const float gx = fmaxf(fmaxf(l.x - X.x, X.x - h.x), 0.0f);
+                const float gy = fmaxf(fmaxf(l.y - X.y, X.y - h.y), 0.0f);
+                const float gz = fmaxf(fmaxf(l.z - X.z, X.z - h.z), 0.0f);
+                return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx)) * kLbShrink <= bound;
+            };
+            uint64_t smask = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int sb = gl + 16 * r;
+                const bool need = sb < nsb && lbox(sboxes[2 * sb], sboxes[2 * sb + 1], bnd);
+                smask |= ((__ballot(need) >> (16 * gw)) & 0xffffull) << (16 * r);
+            }
+            const int nsbc = __builtin_popcountll(smask);
+            NNKey kb = ~0ull;            // this lane's best key
+            uint32_t ls = 0x7f800000u;   // the smallest d² (bits) that lost a comparison on this lane
+            int nev = 0;                 // blocks evaluated
+            // Candidate blocks are gathered two superblocks per step (lanes 0-7 / 8-15 test their
+            // blocks) into the group's LDS list and evaluated a list at a time, lane gl taking target
+            // gl of 4 blocks per round trip; after each list the bound drops to the second-nearest
+            // found so far (a far-off query with a loose U would otherwise evaluate most blocks).
+            float cb = bnd;
+            while (smask) {
+                int nc = 0;  // group-uniform
+                while (smask && nc <= kLightCand - 2 * kSuper) {
+                    const int sa = __builtin_ctzll(smask);
+                    smask &= smask - 1;
+                    const int sb2 = smask ? __builtin_ctzll(smask) : -1;
+                    if (sb2 >= 0) smask &= smask - 1;
+                    const int mysb = gl < kSuper ? sa : sb2;
+                    const int b = mysb * kSuper + (gl & (kSuper - 1));
+                    const bool need = mysb >= 0 && b < nb && lbox(boxes[2 * b], boxes[2 * b + 1], cb);
+                    const uint32_t bm = (uint32_t)((__ballot(need) >> (16 * gw)) & 0xffffu);
+                    if (need) cand[g][nc + __builtin_popcount(bm & ((1u << gl) - 1))] = (int16_t)b;
+                    nc += __builtin_popcount(bm);
+                }
+                for (int c0 = 0; c0 < nc; c0 += 4) {
+                    float4 t4[4];
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) t4[u4] = ts[(int)cand[g][min(c0 + u4, nc - 1)] * kLdsLeaf + gl];
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) {
+                        if (c0 + u4 >= nc) break;
+                        const NNKey kn = make_key(l2_simple(X.x, X.y, X.z, t4[u4].x, t4[u4].y, t4[u4].z), __float_as_uint(t4[u4].w));
+                        ls = min(ls, (uint32_t)((kn < kb ? kb : kn) >> 32));
+                        kb = kn < kb ? kn : kb;
+                    }
+                }
+                nev += nc;
+                if (smask) {  // tighten: the group's second-nearest so far
+                    NNKey K = kb;
+#pragma unroll
+                    for (int off = 1; off < 16; off <<= 1) {
+                        const uint32_t hi = __shfl_xor((uint32_t)(K >> 32), off, 64);
+                        const uint32_t lw = __shfl_xor((uint32_t)K, off, 64);
+                        const NNKey o2 = ((NNKey)hi << 32) | lw;
+                        K = o2 < K ? o2 : K;
+                    }
+                    uint32_t S = kb != K ? min(ls, (uint32_t)(kb >> 32)) : ls;
+#pragma unroll
+                    for (int off = 1; off < 16; off <<= 1) S = min(S, (uint32_t)__shfl_xor(S, off, 64));
+                    cb = fminf(cb, __uint_as_float(S));
+                }
+            }
+            // the group's best key and second-nearest d² (bits): every key but the winner lost once
+            NNKey K = kb;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const uint32_t hi = __shfl_xor((uint32_t)(K >> 32), off, 64);
+                const uint32_t lw = __shfl_xor((uint32_t)K, off, 64);
+                const NNKey o2 = ((NNKey)hi << 32) | lw;
+                K = o2 < K ? o2 : K;
+            }
+            uint32_t S = kb != K ? min(ls, (uint32_t)(kb >> 32)) : ls;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) S = min(S, (uint32_t)__shfl_xor(S, off, 64));
+            if (gl == 0) {
+                w.nn_key[slot] = K;
+                w.nn_lu[slot] = lu_from_sec(__uint_as_float(S));
+                const float4 t = tgt[key_idx(K)];
+                w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(K)));
+                evals += (unsigned long long)nev * kLdsLeaf;
+                tests += (unsigned long long)(nsb + kSuper * nsbc);
+            }
+        }
+        __syncthreads();  // qs / wtot / boxes are rewritten by the next item
+    }
+    evals = wave_sum(evals);
+    tests = wave_sum(tests);
+    if (lane == 0) {
+        count_add(w.evals, 0, evals);
+        count_add(w.evals, 1, tests);
     }
 }
 
@@ -1154,7 +1397,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // the pairs of the launch into ticks[8..10], pairs in ticks[11]
         const bool tk = w.ticks != nullptr && tid == 0;
         uint64_t tk0 = tk ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = tk0, tk2 = tk0;
-        const int p = w.plist[idx];
+        const int item = w.plist[idx];
+        const int p = item >> kLightChunkBits, part = item & ((1 << kLightChunkBits) - 1);
         const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
         const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
         float4* X = w.X + (int64_t)p * w.x_stride;
@@ -1162,13 +1406,17 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
         const float4* tgt = a.tgt + uload(a.tgt_off + p);
 
-        // the queries to search: all (first pass / no CACHE) or the test kernel's misses, compacted
-        // from the pair's bitmap in Morton order (stable); the bitmap is cleared for the next pass
+        // the queries to search: all (first pass / no CACHE) or the test kernel's misses with rank
+        // [lo, lo + part_size) (this item's part), compacted from the pair's bitmap in index order
+        // (stable).  The update kernel clears the bitmap (other parts may still be reading it).
         int nlist = n;
         const int32_t* list = sperm;
         if (CACHE && !first) {
             int32_t* qlist = w.qlist + (int64_t)p * w.x_stride;
-            uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+            const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+            const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
+            const int lo = ps > 0 ? part * ps : 0;
+            const int hi = ps > 0 ? lo + ps : (1 << 30);
             const int nwords = (n + 31) >> 5;
             const uint32_t f = tid < nwords ? gneed[tid] : 0u;
             const int c = __builtin_popcount(f);
@@ -1186,24 +1434,26 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 base += v < wave ? s : 0;
                 total += s;
             }
-            if (f) {  // all 32 source indices of the word in one go (no load behind a store)
+            int o = base + incl - c;
+            if (f && o < hi && o + c > lo) {  // all 32 source indices of the word in one go (no load behind a store)
                 int4 sv[8];
                 const int4* s4 = reinterpret_cast<const int4*>(sperm + tid * 32);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sv[e] = s4[e];
-                int o = base + incl - c;
+                auto put = [&](int v) {
+                    if (o >= lo && o < hi) qlist[o] = v;
+                    ++o;
+                };
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    if ((f >> (4 * e)) & 1) qlist[o++] = sv[e].x;
-                    if ((f >> (4 * e + 1)) & 1) qlist[o++] = sv[e].y;
-                    if ((f >> (4 * e + 2)) & 1) qlist[o++] = sv[e].z;
-                    if ((f >> (4 * e + 3)) & 1) qlist[o++] = sv[e].w;
+                    if ((f >> (4 * e)) & 1) put(sv[e].x);
+                    if ((f >> (4 * e + 1)) & 1) put(sv[e].y);
+                    if ((f >> (4 * e + 2)) & 1) put(sv[e].z);
+                    if ((f >> (4 * e + 3)) & 1) put(sv[e].w);
                 }
-                gneed[tid] = 0;
             }
-            if (tid == 0) w.miss_cnt[p] = 0;
-            nlist = total;
-            list = qlist;
+            nlist = min(hi, total) - lo;
+            list = qlist + lo;
             __syncthreads();  // qlist (global, this workgroup's) visible to the whole workgroup
             if (tk) tk1 = __builtin_amdgcn_s_memrealtime();
         }
@@ -1230,28 +1480,45 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const int rounds = (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q);
         const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
         for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
+            const bool rt = w.ticks != nullptr && lane == 0;  // debug: run phase clocks (tools/nn_phases.py)
+            const uint64_t r0 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             const int cend = min(base + per, nlist);
             float x[Q], y[Q], z[Q];
             float bnd[Q];  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
                            // -1 on idle lanes (never queue work, never widen the coarse bound)
             int orig[Q];
-            int seed_pos0 = 0;
+            // the run's query data in three dependent rounds, every load of a round issued together
+            // (list -> X, key, U -> the previous match's sorted position)
+            int sidx[Q], o_[Q];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const int s0 = base + lane + q * 64;
-                const int s = s0 < cend ? s0 : base;  // idle lanes shadow the run's first query
-                const int o = list[s];
-                orig[q] = s0 < cend ? o : -1;
-                const float4 v = X[o];
-                x[q] = v.x;
-                y[q] = v.y;
-                z[q] = v.z;
-                // seed: the previous match (first pass: the target at the same relative Morton
+                sidx[q] = s0 < cend ? s0 : base;  // idle lanes shadow the run's first query
+                o_[q] = list[sidx[q]];
+            }
+            float4 v[Q];
+            NNKey pk[Q];
+            float uu[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                orig[q] = base + lane + q * 64 < cend ? o_[q] : -1;
+                v[q] = X[o_[q]];
+                pk[q] = first ? 0ull : key[o_[q]];
+                uu[q] = (CACHE && !first) ? w.nn_lu[(int64_t)p * w.x_stride + o_[q]].y : 0.0f;
+            }
+            int pj[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) pj[q] = first ? (int)(((int64_t)sidx[q] * m) / n) : tinv[key_idx(pk[q])];
+            const int seed_pos0 = pj[0];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                x[q] = v[q].x;
+                y[q] = v[q].y;
+                z[q] = v[q].z;
+                // seed: the previous match (first pass: the target at the same relative index
                 // position) and the rest of its 16-target block, evaluated up front from LDS — tight
                 // initial bounds, so the coarse tests below already prune with them
-                const int pj = first ? (int)(((int64_t)s * m) / n) : tinv[key_idx(key[o])];
-                if (q == 0) seed_pos0 = pj;
-                const int bj = pj / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
+                const int bj = pj[q] / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
                 const v4f* tb = sh.tl + bj * kLdsLeaf;
                 NNKey lo = ~0ull, hi = ~0ull;  // the two smallest distinct keys seen
 #pragma unroll
@@ -1265,10 +1532,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     // U of the previous search, moved since: an upper bound of the second-nearest
                     // distance even if no evaluated target attains it (first pass: none)
                     uint32_t sec0 = (uint32_t)(hi >> 32);
-                    if (!first) {
-                        const float u = w.nn_lu[(int64_t)p * w.x_stride + o].y;
-                        sec0 = min(sec0, __float_as_uint(u * u * 1.00001f));
-                    }
+                    if (!first) sec0 = min(sec0, __float_as_uint(uu[q] * uu[q] * 1.00001f));
                     bestl[q * 64 + lane] = lo;
                     secl[q * 64 + lane] = sec0;
                     bnd[q] = orig[q] >= 0 ? __uint_as_float(sec0) : -1.0f;
@@ -1278,6 +1542,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
                 evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
             }
+            const uint64_t r1 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             float qlo[3], qhi[3], qmax = 0.0f;
             qlo[0] = qhi[0] = x[0];
             qlo[1] = qhi[1] = y[0];
@@ -1414,11 +1679,19 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
             }
             if (tail != head) drain(tail - head);
+            const uint64_t r2 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
+            // every load before the first store (on gfx9 a load waits behind earlier stores on vmcnt)
+            NNKey kbq[Q];
+            float4 tq[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) kbq[q] = bestl[q * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) tq[q] = tgt[key_idx(kbq[q])];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (orig[q] < 0) continue;
-                const NNKey kb = bestl[q * 64 + lane];
-                const float4 t = tgt[key_idx(kb)];
+                const NNKey kb = kbq[q];
+                const float4 t = tq[q];
                 key[orig[q]] = kb;
                 if (CACHE) {  // the update reads X, nn_t and the key: no correspondence record
                     const int64_t slot = (int64_t)p * w.x_stride + orig[q];
@@ -1427,6 +1700,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 } else if (corr) {
                     write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
                 }
+            }
+            if (rt) {
+                unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
+                atomicAdd(tt + 24, (unsigned long long)(r1 - r0));
+                atomicAdd(tt + 25, (unsigned long long)(r2 - r1));
+                atomicAdd(tt + 26, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r2));
+                atomicAdd(tt + 27, 1ull);
             }
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
@@ -1635,6 +1915,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     if (st.phase != kPhaseActive) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = a.src_n[p];
+    clear_need(w, p, n, tid, kFoldWG);
     const int64_t xs = w.x_stride;
     const KParams& kp = a.kp;
     const bool weighted = kp.huber_delta < INFINITY;
@@ -1810,6 +2091,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
     if (st.phase != kPhaseActive) return;
     const int tid = threadIdx.x;
     const int n = a.src_n[p];
+    clear_need(w, p, n, tid, kUpdWG);
     const float4* tgt = a.tgt + a.tgt_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
     const int64_t slot0 = (int64_t)p * w.x_stride;
@@ -2005,13 +2287,15 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
         if (ev.test_stop && (e = hipEventRecord(ev.test_stop, st)) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(nn_order_kernel, dim3(1), dim3(kOrderWG), 0, st, a, w, npairs, fitness_pass,
-                       (first || !cache) ? 1 : 0);
+                       (first || !cache) ? 1 : 0, ncu);
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
     if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
     if (cache)
         hipLaunchKernelGGL(nn_lds_kernel<true>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     else
         hipLaunchKernelGGL(nn_lds_kernel<false>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    if (cache && !first && w.ilist)
+        hipLaunchKernelGGL(nn_light_kernel, dim3(ncu * 8), dim3(kLightWG), 0, st, a, w);
     if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -258,6 +258,31 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
             assert (cached[k]["T"].reshape(4, 4).T == o["T"]).all() and cached[k]["fitness"] == o["fitness"]
 
 
+def test_light_search_identical(gpu_ctx, oracle_mod, monkeypatch):
+    """nn_light_kernel (per-query 16-lane search from the index in HBM, for pairs with few cache
+    misses) returns exactly what the LDS work-list search returns: the batch is bit-identical with
+    the light path off, at its default threshold, and taking every pass-2+ pair; PCL defaults
+    (early stops live) and the oracle on sampled pairs."""
+    import icp4r
+
+    npairs, n = 256, 8192
+    pairs = [_pair(900 + k, n) for k in range(npairs)]
+    args = _batch(pairs)
+    p = icp4r.default_params(max_iterations=20)
+    out = {}
+    for lm in ("0", "1024", "16384"):
+        monkeypatch.setenv("ICP4R_LIGHT_MAX", lm)
+        gpu_ctx.reset_timers()
+        out[lm] = gpu_ctx.align_batch_host(*args, params=p)
+        assert (out[lm]["status"] == 0).all()
+    assert out["0"].tobytes() == out["1024"].tobytes() == out["16384"].tobytes()
+    for k in (0, 77, 255):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20)
+        r = out["16384"][k]
+        assert (r["T"].reshape(4, 4).T == o["T"]).all() and r["fitness"] == o["fitness"]
+        assert r["iterations"] == o["iterations"] and r["converged"] == o["converged"]
+
+
 def test_pruned_evaluates_fewer_pairs(gpu_ctx):
     """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer."""
     import icp4r

@@ -1,14 +1,13 @@
-"""Per-pass phase times of the persistent batched search (diagnostic; ICP4R_PHASE_TICKS=1).
+"""Per-pass distribution of cached-neighbour misses over the pairs of the benchmark batch
+(diagnostic; ICP4R_PHASE_TICKS=1 makes nn_order_kernel record each pair's work of the last pass).
 
-    python tools/nn_phases.py [--pairs 1024] [--iters 20]
-
-For pass k (a run of k iterations minus a run of k-1): pairs searched, and per searched pair the
-wall time of compaction, target staging and the search itself (workgroup thread 0's clock).
+    python tools/miss_hist.py [--pairs 1024] [--iters 20]
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import json
 import os
 import sys
 
@@ -37,31 +36,17 @@ def main():
     ctx = icp4r.Context(0)
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
-
-    def ticks():
-        buf = (C.c_uint64 * 32)()
-        return np.array(list(buf), np.float64) if lib.icp4r__debug_ticks(ctx._h, buf, 32) == 0 else None
-
-    prev = None
     for k in range(1, a.iters + 1):
         p = icp4r.default_params(max_iterations=k, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
                                  compute_fitness=0)
-        t0 = ticks()
-        ctx.reset_timers()
         ctx.align_batch_host(src, off, cnt, tgt, off, cnt, params=p)
-        t1 = ticks()
-        ms, _ = ctx.kernel_time_ms()
-        if t0 is None:
-            t0 = np.zeros(32)
-        d = t1 - t0
-        last = d - prev if prev is not None else d
-        prev = d
-        pr = max(last[11], 1)
-        runs = max(last[27], 1)
-        print(f"pass {k:2d}: items {int(last[11]):5d}  per item: compact {last[8] / pr * 0.01:6.1f} us  "
-              f"stage {last[9] / pr * 0.01:6.1f} us  search {last[10] / pr * 0.01:7.1f} us | runs {int(last[27]):6d} "
-              f"per run: setup {last[24] / runs * 0.01:5.1f} us  traverse {last[25] / runs * 0.01:6.1f} us  "
-              f"write {last[26] / runs * 0.01:5.1f} us   (avg search launch {ms:.3f} ms)")
+        buf = (C.c_uint64 * (32 + P))()
+        lib.icp4r__debug_ticks(ctx._h, buf, 32 + P)
+        m = np.array(list(buf), np.int64)[32:32 + P]
+        s = np.sort(m)[::-1]
+        print(json.dumps({"pass": k, "pairs": int((m > 0).sum()), "misses": int(m.sum()),
+                          "top": s[:8].tolist(), "p50": int(np.median(m[m > 0])) if (m > 0).any() else 0,
+                          "over1024": int((m > 1024).sum()), "work_over1024": int(m[m > 1024].sum())}), flush=True)
 
 
 if __name__ == "__main__":
