@@ -960,17 +960,17 @@ constexpr int kLdsTargets = 8192;
 constexpr int kLdsLeaf = 16;
 constexpr int kLdsWG = 1024;
 constexpr int kLdsWaves = kLdsWG / 64;
-constexpr int kLdsQ = 2;
+constexpr int kLdsQ = 1;  // queries per lane (2 measured no faster: smaller runs prune better)
 constexpr int kRing = 128;  // work items per wave (<= 63 pending + 64 appended per query slot)
 constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
 struct LdsNN {
-    v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, Morton order
-    unsigned long long best[kLdsWaves][64 * kLdsQ];    // 16 KB: best (d², index) key per query
+    v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
+    unsigned long long best[kLdsWaves][64 * kLdsQ];    // 8 KB: best (d², index) key per query
     union {
-        uint32_t sec[kLdsWaves][64 * kLdsQ];           // 8 KB: second-smallest d² bits (CACHE search)
+        uint32_t sec[kLdsWaves][64 * kLdsQ];           // 4 KB: second-smallest d² bits (CACHE search)
         int32_t wsum[kLdsWaves];                       // compaction
     } u;
     uint16_t items[kLdsWaves][kRing];                  // 4 KB: (query slot << 9) | block
