@@ -1480,7 +1480,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const int rounds = (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q);
         const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
         for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
-            const bool rt = w.ticks != nullptr && lane == 0;  // debug: run phase clocks (tools/nn_phases.py)
+            const bool rt = w.ticks != nullptr;  // debug (wave-uniform): run phase clocks (tools/nn_phases.py)
             const uint64_t r0 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             const int cend = min(base + per, nlist);
             float x[Q], y[Q], z[Q];

@@ -61,7 +61,7 @@ def main():
         print(f"pass {k:2d}: items {int(last[11]):5d}  per item: compact {last[8] / pr * 0.01:6.1f} us  "
               f"stage {last[9] / pr * 0.01:6.1f} us  search {last[10] / pr * 0.01:7.1f} us | runs {int(last[27]):6d} "
               f"per run: setup {last[24] / runs * 0.01:5.1f} us  traverse {last[25] / runs * 0.01:6.1f} us  "
-              f"write {last[26] / runs * 0.01:5.1f} us   (avg search launch {ms:.3f} ms)")
+              f"write {last[26] / runs * 0.01:5.1f} us (drains {last[28] / runs * 0.01:5.1f} us)   (avg search launch {ms:.3f} ms)")
 
 
 if __name__ == "__main__":
