@@ -1653,10 +1653,18 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 tests += nsb;
             }
             const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos0) / (kLdsLeaf * kSuper);
-            int up = sb0, dn = sb0 - 1;
-            for (int k = 0; k < nsb; ++k) {
-                const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
-                if (!((cmask >> sb) & 1)) continue;
+            // the candidate superblocks outward from the seed's, alternating up / down (only set bits
+            // of cmask are visited: a scalar loop over all nsb cost ~10 SALU per superblock per run)
+            uint64_t um = sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
+            for (bool upnext = true; um | dm; upnext = !upnext) {
+                int sb;
+                if (um && (upnext || !dm)) {
+                    sb = __builtin_ctzll(um);
+                    um &= um - 1;
+                } else {
+                    sb = 63 - __builtin_clzll(dm);
+                    dm &= ~(1ull << sb);
+                }
                 const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
                 tests += 64 * Q + kSuper;
                 uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
