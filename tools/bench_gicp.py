@@ -4,8 +4,9 @@ the oracle on one host core.
     python tools/bench_gicp.py [--case map|scan|batch] [--steps 3]
 
 Cases:
-  map    the reference node's call (radar_odometry.cpp:399-405): one 8k-point scan against a 64k-point
-         submap (synth.make_map_pair), k = 5 (setCorrespondenceRandomness(5))
+  map    the reference node's call (radar_odometry.cpp:399-405): one 8k-point scan, associated to the map
+         frame with a slightly wrong odometry prediction, against a 64k-point submap
+         (synth.make_map_pair), k = 5 (setCorrespondenceRandomness(5))
   scan   one 8k/8k scan pair, fast_gicp defaults (k = 20)
   batch  --pairs independent 8k/8k pairs, k = 5, one device batch (throughput mode)
 
@@ -54,8 +55,17 @@ def main():
     dev = torch.device("cuda", 0)
     torch.zeros(1, device=dev)
     if a.case == "map":
+        # as the node calls it: the scan already associated to the map frame with the odometry's
+        # prediction (pointAssociateToMap, radar_odometry.cpp:382-385) — here the true pose composed
+        # with a 0.3 m / 1 degree prediction error
         pr = synth.make_map_pair(0, n_src=a.points)
-        pairs = [(pr.src, pr.tgt)]
+        yaw = np.deg2rad(1.0)
+        err = np.array([[np.cos(yaw), -np.sin(yaw), 0.0, 0.3], [np.sin(yaw), np.cos(yaw), 0.0, -0.2],
+                        [0.0, 0.0, 1.0, 0.05], [0.0, 0.0, 0.0, 1.0]])
+        Tp = pr.T_gt @ err
+        src_map = pr.src.copy()
+        src_map[:, :3] = (pr.src[:, :3].astype(np.float64) @ Tp[:3, :3].T + Tp[:3, 3]).astype(np.float32)
+        pairs = [(src_map, pr.tgt)]
         k = 5
     elif a.case == "scan":
         pr = synth.make_pair(0, a.points)
