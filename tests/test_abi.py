@@ -103,12 +103,12 @@ def test_fails_loudly_without_library(tmp_path, monkeypatch):
 
 
 def test_cpp_facade_compiles():
-    """include/icp4r/pcl_compat.hpp and ikd_compat.hpp + the reference's call blocks (ICP and the
-    radar_odometry map calls) compile and link against the library (running them needs the GPU:
+    """include/icp4r/pcl_compat.hpp, ikd_compat.hpp and fast_gicp_compat.hpp + the reference's call
+    blocks (ICP, the radar_odometry map calls and its GICP) compile and link against the library (running them needs the GPU:
     tests/test_gpu_parity.py, tests/test_map.py)."""
     r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    for exe in ("callsite", "map_callsite"):
+    for exe in ("callsite", "map_callsite", "gicp_callsite"):
         assert os.access(os.path.join(ROOT, "tests", "cpp", "_build", exe), os.X_OK), exe
 
 

@@ -255,3 +255,33 @@ def test_gpu_fast_gicp_facade(gpu_ctx):
     dt, dr = pose_err(reg.getFinalTransformation(), T)
     assert dt < TOL_KAT_T and dr < TOL_KAT_R
     assert 0.0 <= reg.getFitnessScore() < 1e-3
+
+
+@pytest.mark.gpu
+def test_gpu_fast_gicp_cpp_callsite(gpu_ctx, oracle_mod, tmp_path):
+    """tests/cpp/gicp_callsite.cpp: radar_odometry's GICP block (radar_odometry.cpp:398-411) through
+    include/icp4r/fast_gicp_compat.hpp — the same bits as the Python facade on the same inputs, and the
+    oracle's pose within the GICP bar."""
+    import os
+    import subprocess
+
+    gicp = _gicp()
+    src, tgt, T = _scene(4, 1500)
+    rec = lambda xyz: np.concatenate([xyz, np.ones((len(xyz), 1), np.float32), np.zeros((len(xyz), 1), np.float32)], 1)
+    a, b = tmp_path / "scan_map.bin", tmp_path / "submap.bin"
+    synth.write_bin(a, rec(src))
+    synth.write_bin(b, rec(tgt))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "_build", "gicp_callsite")
+    r = subprocess.run([exe, str(a), str(b)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    head, tl = r.stdout.strip().split("\n")[:2]
+    conv, score, iters, nout = head.split()
+    Tc = np.array([float(v) for v in tl.split()], np.float32).reshape(4, 4).T  # column-major
+    res, _ = gicp.align(src, tgt, gicp.default_params(k_correspondences=5), ctx=gpu_ctx)
+    assert (Tc == res.matrix()).all()
+    assert int(conv) == int(res.converged) and int(iters) == res.iterations and int(nout) == len(src)
+    assert float(score) == res.fitness
+    o = oracle_mod.gicp_align(src, tgt, k=5)
+    dt, dr = pose_err(Tc, o["T"])
+    assert dt < 1e-5 and dr < 1e-5, (dt, dr)
