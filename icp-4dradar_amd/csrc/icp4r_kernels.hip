@@ -973,7 +973,7 @@ struct LdsNN {
         uint32_t sec[kLdsWaves][64 * kLdsQ];           // 4 KB: second-smallest d² bits (CACHE search)
         int32_t wsum[kLdsWaves];                       // compaction
     } u;
-    uint16_t items[kLdsWaves][kRing];                  // 4 KB: (query slot << 9) | block
+    uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query slot << 9) | block; + a spare slot per lane
     int32_t cur;                                       // the pair this workgroup works on
 };
 
@@ -1480,8 +1480,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const int rounds = (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q);
         const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
         for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
-            const bool rt = w.ticks != nullptr;  // debug (wave-uniform): run phase clocks (tools/nn_phases.py)
-            const uint64_t r0 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             const int cend = min(base + per, nlist);
             float x[Q], y[Q], z[Q];
             float bnd[Q];  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
@@ -1542,7 +1540,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
                 evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
             }
-            const uint64_t r1 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             float qlo[3], qhi[3], qmax = 0.0f;
             qlo[0] = qhi[0] = x[0];
             qlo[1] = qhi[1] = y[0];
@@ -1635,10 +1632,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     const bool need = lbd * kLbShrink <= bnd[q];
                     const uint64_t mask = __ballot(need);
                     if (mask == 0) continue;
-                    if (need) {
+                    {  // every lane writes (no exec-mask branch): lanes that do not need b write their own
+                       // spare slot past the ring
                         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                        ring[(tail + rank) & (kRing - 1)] = (uint16_t)(((uint32_t)(q * 64 + lane) << 9) | (uint32_t)b);
+                        const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
+                        ring[at] = (uint16_t)(((uint32_t)(q * 64 + lane) << 9) | (uint32_t)b);
                     }
                     tail += (uint32_t)__builtin_popcountll(mask);
                     if (tail - head >= 64) drain(64);
@@ -1679,15 +1678,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 if (qslots == 0) continue;
                 // coarse test of the superblock's blocks at once (lanes 0..7)
                 const int bl = sb * kSuper + (lane & (kSuper - 1));
-                uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
-                while (bmask) {
-                    const int b = sb * kSuper + __builtin_ctz(bmask);
-                    bmask &= bmask - 1;
-                    push(b, tbx[2 * b], tbx[2 * b + 1], qslots);
-                }
+                const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
+                const cv4f_ptr sbb = tbx + 2 * sb * kSuper;  // the superblock's block boxes: immediate offsets
+#pragma unroll
+                for (int k = 0; k < kSuper; ++k)
+                    if ((bmask >> k) & 1) push(sb * kSuper + k, sbb[2 * k], sbb[2 * k + 1], qslots);
             }
             if (tail != head) drain(tail - head);
-            const uint64_t r2 = rt ? __builtin_amdgcn_s_memrealtime() : 0;
             // every load before the first store (on gfx9 a load waits behind earlier stores on vmcnt)
             NNKey kbq[Q];
             float4 tq[Q];
@@ -1708,13 +1705,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 } else if (corr) {
                     write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
                 }
-            }
-            if (rt) {
-                unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
-                atomicAdd(tt + 24, (unsigned long long)(r1 - r0));
-                atomicAdd(tt + 25, (unsigned long long)(r2 - r1));
-                atomicAdd(tt + 26, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - r2));
-                atomicAdd(tt + 27, 1ull);
             }
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair

@@ -27,7 +27,8 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-library_path = os.path.join(HERE, "_lib", "libicp4r.so")
+# ICP4R_LIBRARY: an alternative build of the same library (A/B experiments); default: the in-tree build
+library_path = os.environ.get("ICP4R_LIBRARY") or os.path.join(HERE, "_lib", "libicp4r.so")
 
 OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 NUMERICS_PCL, NUMERICS_F64 = 0, 1
