@@ -234,7 +234,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
         if (pl.lds) {
             HIP_TRY(ctx->plist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
-            HIP_TRY(ctx->plist_n.ensure(4 * sizeof(int32_t)));  // items, queue, part size
+            HIP_TRY(ctx->plist_n.ensure(4 * kMaxGroups * sizeof(int32_t)));  // per group: items, queue, part size
             w.plist = static_cast<int32_t*>(ctx->plist.p);
             w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
             w.queue = w.plist_n + 1;
@@ -259,7 +259,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
             if (w.light_max > 0) {
                 HIP_TRY(ctx->ilist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
-                HIP_TRY(ctx->ilist_n.ensure(2 * sizeof(int32_t)));
+                HIP_TRY(ctx->ilist_n.ensure(2 * kMaxGroups * sizeof(int32_t)));
                 w.ilist = static_cast<int32_t*>(ctx->ilist.p);
                 w.ilist_n = static_cast<int32_t*>(ctx->ilist_n.p);
             }
@@ -274,7 +274,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
 // One NN pass over every active pair, timed with events: the roofline's kernel is the batched
 // search (nn_lds_kernel) or, for the other plans, the NN launch itself.
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st) {
+            int fitness_pass, int first, hipStream_t st, int ncu) {
     EventPair* ne;
     int r;
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
@@ -288,7 +288,7 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
             ev.test_start = te->start;
             ev.test_stop = te->stop;
         }
-        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ctx->ncu, st, ev));
+        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev));
         return ICP4R_OK;
     }
     HIP_TRY(hipEventRecord(ne->start, st));
@@ -302,7 +302,55 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
     return ICP4R_OK;
 }
 
+static_assert(sizeof(icp4r_ctx::aux_stream) / sizeof(hipStream_t) == kMaxGroups, "aux streams");
+
+// Pairs [p0, p0 + np) of a batch as a batch of their own: every per-pair array offset by p0, the
+// pass-scoped lists / counters of group g in their own slots.
+void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& ag, WorkArgs& wg) {
+    ag = a;
+    ag.src_off += p0;
+    ag.src_n += p0;
+    ag.tgt_off += p0;
+    ag.tgt_n += p0;
+    if (ag.guess) ag.guess += (int64_t)p0 * 16;
+    ag.results += p0;
+    wg = w;
+    const int64_t xs = (int64_t)p0 * w.x_stride;
+    wg.X += xs;
+    wg.nn_key += xs;
+    wg.state += p0;
+    if (wg.corr) wg.corr += xs * 2;
+    if (wg.tsort) {
+        wg.tsort += (int64_t)p0 * w.t_stride;
+        wg.tinv += (int64_t)p0 * w.t_stride;
+        wg.tbox += (int64_t)p0 * 2 * w.b_stride;
+        wg.sbox += (int64_t)p0 * 2 * w.sb_stride;
+        wg.sperm += xs;
+    }
+    if (wg.nn_lu) {
+        wg.nn_lu += xs;
+        wg.nn_t += xs;
+        wg.sinv += xs;
+        wg.qlist += xs;
+        wg.need += (int64_t)p0 * w.need_stride;
+        wg.miss_cnt += p0;
+    }
+    if (wg.plist) {
+        wg.plist += (int64_t)p0 * ((w.x_stride + 63) / 64);
+        wg.plist_n += 4 * g;
+        wg.queue = wg.plist_n + 1;
+    }
+    if (wg.ilist) {
+        wg.ilist += (int64_t)p0 * ((w.x_stride + 63) / 64);
+        wg.ilist_n += 2 * g;
+    }
+    if (g > 0) wg.ticks = nullptr;  // debug slots are pair-0 / global
+}
+
 // The whole registration of a device-resident batch as one stream-ordered launch sequence.
+// Large batched (LDS-plan) batches run as `groups` independent pair groups on their own streams,
+// forked from and joined back into `st`: a group's HBM-bound kernels (cache test, fold) overlap the
+// latency/issue-bound search of another (ICP4R_GROUPS, default kDefaultGroups).
 int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m, int max_iterations,
               int nn_mode, hipStream_t st) {
     if (npairs <= 0) return ICP4R_OK;
@@ -315,21 +363,56 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
-    HIP_TRY(launch_init(a, w, npairs, st));
-    if (pl.pruned) HIP_TRY(launch_index(a, w, npairs, st));
+    int groups = pl.lds ? env_int("ICP4R_GROUPS", kDefaultGroups) : 1;
+    if (groups < 1) groups = 1;
+    if (groups > kMaxGroups) groups = kMaxGroups;
+    while (groups > 1 && npairs / groups < kLdsMinPairs / 2) --groups;
+    PairArgs ag[kMaxGroups];
+    WorkArgs wg[kMaxGroups];
+    hipStream_t gs[kMaxGroups];
+    int gn[kMaxGroups];
+    for (int g = 0; g < groups; ++g) {
+        const int p0 = (int)((int64_t)npairs * g / groups), p1 = (int)((int64_t)npairs * (g + 1) / groups);
+        gn[g] = p1 - p0;
+        group_view(a, w, p0, g, ag[g], wg[g]);
+        gs[g] = st;
+        if (g > 0) {
+            if (!ctx->aux_stream[g]) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream[g], hipStreamNonBlocking));
+            if (!ctx->fork_ev[g]) HIP_TRY(hipEventCreateWithFlags(&ctx->fork_ev[g], hipEventDisableTiming));
+            gs[g] = ctx->aux_stream[g];
+        }
+    }
+    for (int g = 1; g < groups; ++g) HIP_TRY(hipStreamWaitEvent(gs[g], be->start, 0));  // fork
+    // persistent search grid per group: CUs / groups (ICP4R_SEARCH_CU_DIV overrides), so the other
+    // groups' kernels find CUs without a 150-KB search workgroup on them (C3: 2 groups on 128 CUs
+    // each 91.5k pairs/s, on 256 CUs each 89.5k, one group 88.4k — measured in one session)
+    const int cdiv = env_int("ICP4R_SEARCH_CU_DIV", groups);
+    const int search_cu = cdiv > 1 ? (ctx->ncu + cdiv - 1) / cdiv : 0;
+    for (int g = 0; g < groups; ++g) {
+        HIP_TRY(launch_init(ag[g], wg[g], gn[g], gs[g]));
+        if (pl.pruned) HIP_TRY(launch_index(ag[g], wg[g], gn[g], gs[g]));
+    }
     // PCL's do { ... } while (!converged): at least one iteration even for max_iterations == 0.
     const int iters = max_iterations > 0 ? max_iterations : 1;
     for (int it = 0; it < iters; ++it) {
-        if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
-        EventPair* ue;
-        if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
-        HIP_TRY(hipEventRecord(ue->start, st));
-        HIP_TRY(launch_update(a, w, npairs, mn, pcl && !pl.pruned, st));
-        HIP_TRY(hipEventRecord(ue->stop, st));
+        for (int g = 0; g < groups; ++g) {
+            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu))) return rc;
+            EventPair* ue;
+            if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
+            HIP_TRY(hipEventRecord(ue->start, gs[g]));
+            HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g]));
+            HIP_TRY(hipEventRecord(ue->stop, gs[g]));
+        }
     }
-    if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));
-    if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, a, w, npairs, mn, 1, 0, st))) return rc;
-    HIP_TRY(launch_finish(a, w, npairs, st));
+    for (int g = 0; g < groups; ++g) {
+        if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g]));
+        if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu))) return rc;
+        HIP_TRY(launch_finish(ag[g], wg[g], gn[g], gs[g]));
+    }
+    for (int g = 1; g < groups; ++g) {  // join
+        HIP_TRY(hipEventRecord(ctx->fork_ev[g], gs[g]));
+        HIP_TRY(hipStreamWaitEvent(st, ctx->fork_ev[g], 0));
+    }
     HIP_TRY(hipEventRecord(be->stop, st));
     return ICP4R_OK;
 }
@@ -456,6 +539,10 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     if (!ctx) return ICP4R_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    for (int g = 0; g < kMaxGroups; ++g) {
+        if (ctx->aux_stream[g]) (void)hipStreamDestroy(ctx->aux_stream[g]);
+        if (ctx->fork_ev[g]) (void)hipEventDestroy(ctx->fork_ev[g]);
+    }
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,

@@ -61,6 +61,9 @@ void pack_host(const float* c, int64_t n, int32_t stride_bytes, std::vector<floa
 struct icp4r_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // run_pairs' pair groups 1.. run on their own streams, joined back into the launch stream
+    hipStream_t aux_stream[4] = {};  // icp4r::kMaxGroups (static_assert in icp4r_capi.cpp)
+    hipEvent_t fork_ev[4] = {};
     // staging for the host-buffer entry points
     icp4r_host::DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace

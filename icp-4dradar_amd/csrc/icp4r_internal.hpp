@@ -17,6 +17,8 @@ constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.
 constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
 constexpr int kDefaultLightMax = 0;  // batched search: pairs with at most this many misses -> nn_light_kernel (0: off; measured slower)
+constexpr int kMaxGroups = 4;        // batched plans: pair groups on their own streams (run_pairs)
+constexpr int kDefaultGroups = 2;
 constexpr int kDefaultPartSize = 1024;  // batched search: misses per work item of a heavy pair  // batched search: pairs with at most this many misses -> nn_light_kernel
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)

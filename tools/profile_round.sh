@@ -7,6 +7,8 @@ set -eu
 TAG=${1:-round1}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+# kernel-level profiles of the single-stream configuration (bench.py prices its kernels on the same)
+export ICP4R_GROUPS=1
 mkdir -p gpurun_out
 ARGS="--steps 5 --warmup 1 --no-cpu --check 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- \
