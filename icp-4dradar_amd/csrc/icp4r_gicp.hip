@@ -39,7 +39,9 @@ __device__ void gicp_sym_eig3(const double* a_in, double* w, double* V) {
     for (int i = 0; i < 9; ++i) a[i] = a_in[i];
     for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 50; ++sweep) {
-        if (a[1] * a[1] + a[2] * a[2] + a[5] * a[5] == 0.0) break;
+        // converged: the off-diagonal mass is below 1e-30 of the diagonal's (~1e-15 relative per
+        // element, the double rounding level; waiting for an exact zero took many more sweeps)
+        if (a[1] * a[1] + a[2] * a[2] + a[5] * a[5] <= 1e-30 * (a[0] * a[0] + a[4] * a[4] + a[8] * a[8])) break;
         for (int p = 0; p < 2; ++p)
             for (int q = p + 1; q < 3; ++q) {
                 const double apq = a[3 * p + q];
@@ -274,12 +276,10 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
     auto needed = [&](const v4f lo, const v4f hi) {
         return __any(box_lb(lo, hi, x, y, z) * kLbShrink <= __uint_as_float((uint32_t)(best[K - 1] >> 32)));
     };
-    int up = sb0, dn = sb0 - 1;
     unsigned long long swept = 0;
-    for (int it = 0; it < nsb; ++it) {
-        const int sb = (up < nsb && (dn < 0 || !(it & 1))) ? up++ : dn--;
+    auto visit = [&](int sb, bool test) {  // sweep superblock sb's needed blocks, then refresh the bound
         const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
-        if (!maybe(slo, shi) || !needed(slo, shi)) continue;
+        if (test && (!maybe(slo, shi) || !needed(slo, shi))) return;
         for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {
             const v4f blo = tb[2 * b], bhi = tb[2 * b + 1];
             if (!maybe(blo, bhi) || !needed(blo, bhi)) continue;
@@ -292,6 +292,31 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
             ++swept;
         }
         qmax = wave_max(__uint_as_float((uint32_t)(best[K - 1] >> 32)));
+    };
+    if (nsb <= 64) {
+        // the wave's own superblock first (a finite K-th bound for every lane), then one lane-parallel
+        // coarse test of every superblock against the wave's query box with that bound, and only the
+        // survivors, outward from the own one (a scalar walk over all superblocks cost a box load and
+        // ~10 SALU per superblock per wave)
+        visit(sb0, false);
+        const int sl = min(lane, nsb - 1);
+        const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+        const uint64_t cm = __ballot(lane < nsb && lane != sb0 && maybe(sbv[2 * sl], sbv[2 * sl + 1]));
+        uint64_t um = sb0 < 63 ? (cm >> (sb0 + 1)) << (sb0 + 1) : 0ull, dm = cm & ~um;
+        for (bool upnext = true; um | dm; upnext = !upnext) {
+            int sb;
+            if (um && (upnext || !dm)) {
+                sb = __builtin_ctzll(um);
+                um &= um - 1;
+            } else {
+                sb = 63 - __builtin_clzll(dm);
+                dm &= ~(1ull << sb);
+            }
+            visit(sb, true);
+        }
+    } else {  // large clouds (the scan-to-map submap): outward walk over every superblock
+        int up = sb0, dn = sb0 - 1;
+        for (int it = 0; it < nsb; ++it) visit((up < nsb && (dn < 0 || !(it & 1))) ? up++ : dn--, true);
     }
     if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, 64));
     if (base + lane >= n) return;
@@ -619,10 +644,16 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
                            int64_t stride, int k, int reg, double* cov, hipStream_t st) {
     if (npairs <= 0 || max_n <= 0) return hipSuccess;
     const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
-    if (k <= 8)
+    // the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default
+    // 20 have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
+    if (k <= 5)
+        hipLaunchKernelGGL(gicp_cov_kernel<5>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else if (k <= 8)
         hipLaunchKernelGGL(gicp_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
     else if (k <= 16)
         hipLaunchKernelGGL(gicp_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
+    else if (k <= 20)
+        hipLaunchKernelGGL(gicp_cov_kernel<20>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
     else if (k <= 32)
         hipLaunchKernelGGL(gicp_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
     else
@@ -635,10 +666,16 @@ hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const in
     if (npairs <= 0 || max_n <= 0) return hipSuccess;
     if (w.leaf != 16) return hipErrorInvalidValue;
     const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
-    if (k <= 8)
+    // the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default
+    // 20 have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
+    if (k <= 5)
+        hipLaunchKernelGGL(gicp_knn_cov_kernel<5>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
+    else if (k <= 8)
         hipLaunchKernelGGL(gicp_knn_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
     else if (k <= 16)
         hipLaunchKernelGGL(gicp_knn_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
+    else if (k <= 20)
+        hipLaunchKernelGGL(gicp_knn_cov_kernel<20>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
     else if (k <= 32)
         hipLaunchKernelGGL(gicp_knn_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
     else

@@ -36,8 +36,10 @@ static void sym_eig3(const double* a_in, double* w, double* V) {
     memcpy(a, a_in, sizeof(a));
     for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 50; ++sweep) {
+        /* converged: the off-diagonal mass is below 1e-30 of the diagonal's (~1e-15 relative per
+         * element, the double rounding level; waiting for an exact zero took many more sweeps) */
         const double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
-        if (off == 0.0) break;
+        if (off <= 1e-30 * (a[0] * a[0] + a[4] * a[4] + a[8] * a[8])) break;
         for (int p = 0; p < 2; ++p)
             for (int q = p + 1; q < 3; ++q) {
                 const double apq = a[3 * p + q];

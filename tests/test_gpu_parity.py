@@ -388,3 +388,50 @@ def test_kernel_timing_api(gpu_ctx):
     ms, k = gpu_ctx.kernel_time_ms()
     bms, bk = gpu_ctx.batch_time_ms()
     assert k == 6 and ms > 0 and bk == 1 and bms >= ms
+
+
+def _brute_nn(q, t):
+    """Exact 1-NN with FLANN's L2_Simple float order, lowest index on ties (numpy)."""
+    q = q[:, :3].astype(np.float32)
+    t = t[:, :3].astype(np.float32)
+    idx = np.empty(len(q), np.int32)
+    d2o = np.empty(len(q), np.float32)
+    for s in range(0, len(q), 256):
+        d = q[s:s + 256, None, :] - t[None, :, :]
+        d2 = (d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]
+        i = np.argmin(d2, axis=1)  # first minimum = lowest index
+        idx[s:s + 256] = i
+        d2o[s:s + 256] = d2[np.arange(len(i)), i]
+    return idx, d2o
+
+
+@pytest.mark.parametrize("shape", ["identical", "collinear", "duplicates", "lattice", "slab", "clustered"])
+@pytest.mark.parametrize("m", [512, 513, 1000, 4097, 8191, 8192])
+def test_kd_index_degenerate_clouds(gpu_ctx, shape, m):
+    """The kd-tree index (index_kernel, clouds <= 8192 points) on degenerate targets: every point the
+    same, all on a line, many exact duplicates, an integer lattice (ties everywhere), a flat slab, tight
+    clusters — the pruned search over it returns brute force's keys exactly (lowest index on ties)."""
+    rng = np.random.default_rng(m * 7 + len(shape))
+    if shape == "identical":
+        t = np.tile(np.array([[3.0, -2.0, 1.0]], np.float32), (m, 1))
+    elif shape == "collinear":
+        t = np.outer(rng.uniform(-50, 50, m), [0.6, 0.8, 0.0]).astype(np.float32)
+    elif shape == "duplicates":
+        base = rng.uniform(-20, 20, (max(m // 8, 1), 3)).astype(np.float32)
+        t = base[rng.integers(0, len(base), m)]
+    elif shape == "lattice":
+        g = np.stack(np.meshgrid(np.arange(16), np.arange(16), np.arange(40)), -1).reshape(-1, 3)
+        t = g[rng.permutation(len(g))[:m]].astype(np.float32)
+    elif shape == "slab":
+        t = np.concatenate([rng.uniform(-60, 60, (m, 2)), np.zeros((m, 1))], 1).astype(np.float32)
+    else:
+        c = rng.uniform(-40, 40, (5, 3))
+        t = (c[rng.integers(0, 5, m)] + rng.normal(0, 0.01, (m, 3))).astype(np.float32)
+    tgt = np.concatenate([t, np.zeros((m, 1), np.float32)], 1)
+    q = (t[rng.integers(0, m, 700)] + rng.normal(0, 0.5, (700, 3))).astype(np.float32)
+    q = np.concatenate([q, t[:50]])  # exact hits
+    src = np.concatenate([q, np.zeros((len(q), 1), np.float32)], 1)
+    gi, gd = gpu_ctx.nearest(src, tgt)
+    bi, bd = _brute_nn(src, tgt)
+    assert (gd.view(np.uint32) == bd.view(np.uint32)).all()
+    assert (gi == bi).all()
