@@ -372,13 +372,14 @@ __device__ __forceinline__ int kd_split(int S, int leaf) {
 // counting sorts of the coordinate quantised to kKdBins levels over the cloud's extent; the order
 // of equal keys (LDS atomics) is arbitrary, which only moves points between the two sides of a
 // split among equals — the search is exact for any order.
-__device__ void kd_order(KdShared& sh, const float4* pts, int n, int leaf, uint64_t* tk) {
+template <typename Get>  // Get: int -> float4, point i of the cloud
+__device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
     // 1. bounding box -> quantisation
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts[i];
+        const float4 v = pts(i);
         mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
         mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
     }
@@ -410,7 +411,7 @@ __device__ void kd_order(KdShared& sh, const float4* pts, int n, int leaf, uint6
     auto bin = [&](float c, int ax) { return min(kKdBins - 1, max(0, (int)((c - lo[ax]) * sc[ax]))); };
     // 2. three counting sorts at once: histogram, exclusive scan, scatter
     for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts[i];
+        const float4 v = pts(i);
         atomicAdd(&sh.u.hist[0][bin(v.x, 0)], 1u);
         atomicAdd(&sh.u.hist[1][bin(v.y, 1)], 1u);
         atomicAdd(&sh.u.hist[2][bin(v.z, 2)], 1u);
@@ -447,7 +448,7 @@ __device__ void kd_order(KdShared& sh, const float4* pts, int n, int leaf, uint6
     }
     __syncthreads();
     for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts[i];
+        const float4 v = pts(i);
         const int bx = bin(v.x, 0), by = bin(v.y, 1), bz = bin(v.z, 2);
         sh.L[0][atomicAdd(&sh.u.hist[0][bx], 1u)] = (uint16_t)i;
         sh.L[1][atomicAdd(&sh.u.hist[1][by], 1u)] = (uint16_t)i;
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
     if ((w.kd_index & (is_tgt ? 1 : 2)) && n <= kKdMaxN && (!is_tgt || w.t_stride <= kKdMaxN)) {
         uint64_t* tk = (w.ticks && p == 0 && is_tgt && tid == 0) ? w.ticks + 12 : nullptr;
-        kd_order(shu.kd, pts, n, is_tgt ? w.leaf : 16, tk);
+        kd_order(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk);
         const uint16_t* ord = shu.kd.L[0];
         if (is_tgt) {
             // sorted targets, padding (+inf coordinates, .w = the last target's index: never a match,
@@ -762,6 +763,75 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             sp[pos] = i;
             if (si) si[i] = (int32_t)pos;
         }
+    }
+}
+
+// index_refine_kernel: targets too large for the in-LDS kd build (the C5 scan-to-map submap) are
+// Morton-sorted by index_kernel, then every 8192-position chunk of that order is re-ordered as a
+// balanced kd-tree on its own (one workgroup per chunk, the same builder): superblocks and blocks —
+// the units the search prunes with — become kd subtrees and leaves, only the chunk boundaries (every
+// 64 superblocks) stay Morton cuts.  Block and superblock boxes of the chunk are recomputed.
+__global__ __launch_bounds__(kIdxWG) void index_refine_kernel(PairArgs a, WorkArgs w) {
+    __shared__ IndexShared shu;
+    const int c = blockIdx.x, p = blockIdx.y;
+    if (w.state[p].phase == kPhaseInvalid) return;
+    const int m = a.tgt_n[p];
+    if (m <= 0 || (m <= kKdMaxN && w.t_stride <= kKdMaxN)) return;  // index_kernel's kd path did it
+    const int c0 = c * kKdMaxN;
+    if (c0 >= m) return;
+    const int len = min(kKdMaxN, m - c0);
+    const int tid = threadIdx.x, lane = tid & 63;
+    float4* ts = w.tsort + (int64_t)p * w.t_stride + c0;
+    kd_order(shu.kd, [&](int i) { return ts[i]; }, len, w.leaf, nullptr);
+    const uint16_t* ord = shu.kd.L[0];
+    float4 v[kKdPer];  // the chunk in its new order (read before anything is overwritten)
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {
+        const int pos = tid + k * kIdxWG;
+        v[k] = pos < len ? ts[ord[pos]] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+    }
+    __syncthreads();
+    int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+    float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+    const int B = w.leaf;
+    const int nbc = (len + B - 1) / B;  // blocks of the chunk (the last may be partial)
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {
+        const int pos = tid + k * kIdxWG;
+        const bool real = pos < len;
+        if (real) {
+            ts[pos] = v[k];
+            tinv[__float_as_uint(v[k].w)] = c0 + pos;
+        }
+        float4 l = real ? v[k] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+        float4 h = real ? v[k] : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        for (int off = 1; off < B; off <<= 1) {
+            l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
+            l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
+            l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
+        }
+        if ((lane & (B - 1)) == 0 && pos / B < nbc) {
+            const int b = pos / B;
+            l.w = 0.f;
+            h.w = 0.f;
+            tb[2 * (c0 / B + b)] = l;
+            tb[2 * (c0 / B + b) + 1] = h;
+            shu.kd.u.bbox[2 * b] = l;
+            shu.kd.u.bbox[2 * b + 1] = h;
+        }
+    }
+    __syncthreads();
+    float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
+    const int nsbc = (nbc + kSuper - 1) / kSuper, sb0 = c0 / (B * kSuper);
+    for (int sb = tid; sb < nsbc; sb += kIdxWG) {
+        float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        for (int b = sb * kSuper; b < min((sb + 1) * kSuper, nbc); ++b) {
+            const float4 bl = shu.kd.u.bbox[2 * b], bh = shu.kd.u.bbox[2 * b + 1];
+            l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
+            h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
+        }
+        sbx[2 * (sb0 + sb)] = l;
+        sbx[2 * (sb0 + sb) + 1] = h;
     }
 }
 
@@ -2266,6 +2336,9 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     hipLaunchKernelGGL(index_kernel, dim3(npairs, 2), dim3(kIdxWG), 0, st, a, w);
+    if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))
+        hipLaunchKernelGGL(index_refine_kernel, dim3((unsigned)((w.t_stride + kKdMaxN - 1) / kKdMaxN), npairs),
+                           dim3(kIdxWG), 0, st, a, w);
     return hipGetLastError();
 }
 
