@@ -216,14 +216,27 @@ def main():
     # cached-neighbour test kernel (HBM-bound): algorithmic bytes = per tested query X (16) + nn_t
     # (16) + L (4) + sinv (4) read; per hit its key (8) written, + its correspondence record (32)
     # in the iteration passes
+    # The iteration passes' tests run in the tail of fold_update_kernel (ICP4R_FUSE_TEST, default):
+    # their counts are tested_in_update / hits_in_update; the rest is the standalone kernel's (the
+    # fitness pass, or every pass with the fusion off).
     cache_test = None
+    t_own = st["cache_tested"] - st["tested_in_update"]
+    h_own = st["cache_hits"] - st["hits_in_update"]
     if test_launches:
-        tb = (st["cache_tested"] * 40 + st["cache_hits"] * 8 + st["records_written_by_test"] * 32) / test_launches
+        tb = (t_own * 40 + h_own * 8 + st["records_written_by_test"] * 32) / test_launches
         cache_test = {"kernel": "nn_cache_test_kernel", "bound": "hbm", "avg_launch_ms": test_ms,
                       "launches": test_launches, "bytes_per_launch": tb,
                       "achieved": tb / (test_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                       "frac": tb / (test_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                      "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1)}
+                      "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1),
+                      "tests_fused_into_update": st["tested_in_update"]}
+    # fold_update_kernel (HBM): two passes over X + nn_t (32 B per point each), and, fused, the next
+    # pass's test: X, nn_t, L/U, sinv read (44 B), X and L/U written (24 B), a key per hit (8 B)
+    update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches}
+    if upd_launches and upd_ms > 0:
+        ub = (P * n * 64 * upd_launches + st["tested_in_update"] * 68 + st["hits_in_update"] * 8) / upd_launches
+        update.update({"bound": "hbm", "bytes_per_launch": ub, "achieved": ub / (upd_ms * 1e-3) / 1e9,
+                       "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS})
 
     if rank == 0:
         cpu = None
@@ -277,7 +290,7 @@ def main():
                         "LDS-limited), see DESIGN.md",
             },
             "cache_test_kernel": cache_test,
-            "update_kernel": {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches},
+            "update_kernel": update,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
             "batch_device_ms": batch_ms,

@@ -70,7 +70,7 @@ namespace icp4r_pipe {
 constexpr size_t kCountBytes = (size_t)kCountSlots * kCountStride * sizeof(uint64_t);
 
 // Sum the per-slot work counters (evaluations, box tests, cache hits) since the last reset.
-constexpr int kNumCounters = 5;
+constexpr int kNumCounters = 7;
 int read_counters(icp4r_ctx* ctx, uint64_t (&out)[kNumCounters]) {
     for (int k = 0; k < kNumCounters; ++k) out[k] = 0;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -274,7 +274,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
 // One NN pass over every active pair, timed with events: the roofline's kernel is the batched
 // search (nn_lds_kernel) or, for the other plans, the NN launch itself.
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st, int ncu) {
+            int fitness_pass, int first, hipStream_t st, int ncu, int test_fused) {
     EventPair* ne;
     int r;
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
@@ -282,13 +282,13 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
         NNLdsEvents ev;
         ev.search_start = ne->start;
         ev.search_stop = ne->stop;
-        if (pl.cache && !first) {
+        if (pl.cache && !first && !test_fused) {
             EventPair* te;
             if ((r = next_event(ctx->test_events, ctx->test_used, &te))) return r;
             ev.test_start = te->start;
             ev.test_stop = te->stop;
         }
-        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev));
+        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev, test_fused));
         return ICP4R_OK;
     }
     HIP_TRY(hipEventRecord(ne->start, st));
@@ -394,13 +394,17 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     }
     // PCL's do { ... } while (!converged): at least one iteration even for max_iterations == 0.
     const int iters = max_iterations > 0 ? max_iterations : 1;
+    // the cached-neighbour test of iteration passes 2.. runs in the tail of the previous update
+    // (fold_update_kernel, PCL numerics; ICP4R_FUSE_TEST=0: its own kernel)
+    const bool fuse = pl.lds && pl.cache && pcl && env_int("ICP4R_FUSE_TEST", 1) != 0;
     for (int it = 0; it < iters; ++it) {
         for (int g = 0; g < groups; ++g) {
-            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu))) return rc;
+            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0)))
+                return rc;
             EventPair* ue;
             if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
             HIP_TRY(hipEventRecord(ue->start, gs[g]));
-            HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g]));
+            HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g], fuse && it + 1 < iters));
             HIP_TRY(hipEventRecord(ue->stop, gs[g]));
         }
     }
@@ -858,6 +862,8 @@ int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out) {
     out->cache_hits = v[2];
     out->cache_tested = v[3];
     out->records_written_by_test = v[4];
+    out->tested_in_update = v[5];
+    out->hits_in_update = v[6];
     return ICP4R_OK;
 }
 

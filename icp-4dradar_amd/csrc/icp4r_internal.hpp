@@ -155,11 +155,12 @@ struct NNLdsEvents {
     hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;
 };
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st, const NNLdsEvents& ev);
+                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused = 0);
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
-                         hipStream_t st);
+                         hipStream_t st,
+                         int tail_test = 0);
 hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);

@@ -1976,7 +1976,7 @@ struct FoldShared {
     SolveShared s;
 };
 
-__global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkArgs w) {
+__global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test) {
     __shared__ FoldShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     PairState& st = w.state[p];
@@ -2139,7 +2139,79 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
     if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
     if (!w.defer_xform) transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
-    __syncthreads();
+    // The next pass's cached-neighbour test, fused (tail_test: another iteration follows and the pair
+    // is still active): the same work as nn_cache_test_kernel for this pair — the deferred
+    // transformCloud(T_inc), the bounds moved, the test, hit keys, the miss bitmap — done here, where
+    // its HBM stream overlaps the other workgroups' latency-bound fold chains instead of taking a
+    // launch of its own.  The workgroup owns the pair, so the bitmap is built in LDS and stored whole.
+    if (tail_test && w.nn_lu && sh.s.flag == 0) {
+        uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
+        const int nwords = (n + 31) >> 5;
+        for (int k = tid; k < nwords; k += kFoldWG) need[k] = 0u;
+        float T[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
+        __syncthreads();
+        float4* X = w.X + (int64_t)p * xs;
+        NNKey* key = w.nn_key + (int64_t)p * xs;
+        float2* lu = w.nn_lu + (int64_t)p * xs;
+        const float4* nt = w.nn_t + (int64_t)p * xs;
+        const int32_t* sinv = w.sinv + (int64_t)p * xs;
+        constexpr int kPer = 4;  // points per thread in flight (8 pushed the kernel past 128 VGPRs: 3 workgroups per CU)
+        int hits = 0, misses = 0;
+        for (int i0 = 0; i0 < n; i0 += kFoldWG * kPer) {
+            float4 v[kPer], t[kPer];
+            float2 L[kPer];
+            int32_t sp[kPer];
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {  // every load before the first store
+                const int i = min(i0 + e * kFoldWG + tid, n - 1);
+                v[e] = X[i];
+                t[e] = nt[i];
+                L[e] = lu[i];
+                sp[e] = sinv[i];
+            }
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                const int i = i0 + e * kFoldWG + tid;
+                const bool valid = i < n;
+                float4 o = v[e];
+                xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
+                const float2 Ln = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+                const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
+                const bool hit = valid & cache_hit(Ln.x, d2);
+                if (valid) {
+                    X[i] = o;
+                    lu[i] = Ln;
+                }
+                if (hit) {
+                    key[i] = make_key(d2, __float_as_uint(t[e].w));
+                    ++hits;
+                } else if (valid) {
+                    atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
+                    ++misses;
+                }
+            }
+        }
+        hits = wave_sum(hits);
+        misses = wave_sum(misses);
+        if (lane == 0) {
+            sh.cnt[wave] = misses;
+            count_add(w.evals, 0, (unsigned long long)hits);
+            count_add(w.evals, 2, (unsigned long long)hits);
+            count_add(w.evals, 3, (unsigned long long)(hits + misses));
+            count_add(w.evals, 5, (unsigned long long)(hits + misses));  // ... of which in this tail
+            count_add(w.evals, 6, (unsigned long long)hits);
+        }
+        __syncthreads();
+        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+        for (int k = tid; k < nwords; k += kFoldWG) gneed[k] = need[k];
+        if (tid == 0) {
+            int tot = 0;
+            for (int k = 0; k < kFoldWaves; ++k) tot += sh.cnt[k];
+            w.miss_cnt[p] = tot;
+        }
+    }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2343,7 +2415,7 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 }
 
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st, const NNLdsEvents& ev) {
+                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
     const bool cache = w.nn_lu != nullptr;
     if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t ||
@@ -2351,7 +2423,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
     hipError_t e;
-    if (cache && !first) {
+    if (cache && !first && !test_fused) {  // (test_fused: the previous fold_update_kernel ran it)
         const int chunks = (max_n + kTestWG * kTestPer - 1) / (kTestWG * kTestPer);
         if (ev.test_start && (e = hipEventRecord(ev.test_start, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(nn_cache_test_kernel, dim3(chunks, npairs), dim3(kTestWG), 0, st, a, w, fitness_pass);
@@ -2397,11 +2469,12 @@ hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npa
     return hipGetLastError();
 }
 
-hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr, hipStream_t st) {
+hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr, hipStream_t st,
+                         int tail_test) {
     if (a.kp.numerics == kNumericsPCL) {
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
-        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w);
+        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test);
     } else {
         hipLaunchKernelGGL(update_f64_kernel, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
     }

@@ -258,6 +258,37 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
             assert (cached[k]["T"].reshape(4, 4).T == o["T"]).all() and cached[k]["fitness"] == o["fitness"]
 
 
+@pytest.mark.parametrize("early", [False, True])
+def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
+    """The cached-neighbour test run in the tail of fold_update_kernel (default) instead of its own
+    nn_cache_test_kernel launch: bit-identical batches, with fixed iterations and with PCL's early
+    stops live (pairs converging at different iterations, so some skip the fused tail), over ragged
+    shapes; the oracle on sampled pairs."""
+    import icp4r
+
+    shapes = [(8192, 8192)] * 200 + [(8000, 8100), (4096, 8192), (2048, 600), (1000, 1200), (37, 4000)] * 12
+    pairs = [_pair(1300 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    args = _batch(pairs)
+    assert icp4r.plan(len(pairs), 8192, 8192)["lds"] and icp4r.plan(len(pairs), 8192, 8192)["cache"]
+    kw = {} if early else dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    p = icp4r.default_params(max_iterations=20, **kw)
+    out = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("ICP4R_FUSE_TEST", fuse)
+        gpu_ctx.reset_timers()
+        out[fuse] = gpu_ctx.align_batch_host(*args, params=p)
+        st = gpu_ctx.nn_stats()
+        assert (st["tested_in_update"] > 0) == (fuse == "1")
+    assert out["1"].tobytes() == out["0"].tobytes()
+    assert (out["1"]["status"] == 0).all()
+    if early:
+        assert len(set(out["1"]["iterations"].tolist())) > 1  # pairs stop at different iterations
+    for k in (0, 199, 203, 204):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20, **kw)
+        assert (out["1"][k]["T"].reshape(4, 4).T == o["T"]).all() and out["1"][k]["fitness"] == o["fitness"]
+        assert out["1"][k]["iterations"] == o["iterations"]
+
+
 def test_light_search_identical(gpu_ctx, oracle_mod, monkeypatch):
     """nn_light_kernel (per-query 16-lane search from the index in HBM, for pairs with few cache
     misses) returns exactly what the LDS work-list search returns: the batch is bit-identical with
