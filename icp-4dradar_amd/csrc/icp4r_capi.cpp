@@ -70,7 +70,7 @@ namespace icp4r_pipe {
 constexpr size_t kCountBytes = (size_t)kCountSlots * kCountStride * sizeof(uint64_t);
 
 // Sum the per-slot work counters (evaluations, box tests, cache hits) since the last reset.
-constexpr int kNumCounters = 7;
+constexpr int kNumCounters = 8;
 int read_counters(icp4r_ctx* ctx, uint64_t (&out)[kNumCounters]) {
     for (int k = 0; k < kNumCounters; ++k) out[k] = 0;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -244,6 +244,9 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float2)));
             HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
             w.nn_t = static_cast<float4*>(ctx->nn_t.p);
+            HIP_TRY(ctx->nn_xs.ensure((size_t)slots * sizeof(float4)));
+            w.nn_xs = static_cast<float4*>(ctx->nn_xs.p);
+            w.second_chance = env_int("ICP4R_SECOND_CHANCE", 0) != 0 ? 1 : 0;
             HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
@@ -330,6 +333,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
     if (wg.nn_lu) {
         wg.nn_lu += xs;
         wg.nn_t += xs;
+        wg.nn_xs += xs;
         wg.sinv += xs;
         wg.qlist += xs;
         wg.need += (int64_t)p0 * w.need_stride;
@@ -549,7 +553,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     }
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->nn_xs, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ilist, &ctx->ilist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})
@@ -864,6 +868,7 @@ int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out) {
     out->records_written_by_test = v[4];
     out->tested_in_update = v[5];
     out->hits_in_update = v[6];
+    out->second_chance_hits = v[7];
     return ICP4R_OK;
 }
 

@@ -122,6 +122,10 @@ struct WorkArgs {
                         // set by a search, widened by every kernel that moves X_i
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index (bits)
+    float4* nn_xs;      // [npairs * x_stride] (X_i at its last search, Lo_i): Lo a lower bound, at that
+                        // position, on |X_i - t_k| for every target k outside the NN's kd leaf (the
+                        // second-chance test inside the leaf, nn_lds_kernel); .w = 0: no second chance
+    int32_t second_chance;  // 1: nn_lds_kernel<true> keeps Lo (block-level losers) and runs the second chance
     int32_t* sinv;      // [npairs * x_stride] source index -> Morton position (inverse of sperm)
     int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)
     uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed

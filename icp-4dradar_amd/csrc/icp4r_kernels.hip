@@ -1072,6 +1072,26 @@ __device__ __forceinline__ bool cache_hit(float L, float dj2) {
     return L * L * (1.0f - kCacheMargin) > dj2 * (1.0f + kCacheMargin);
 }
 
+// Smallest (d², index) key of LDS block b (lds_swz layout) for query (x, y, z); `cb` = that target.
+// s2: the second-smallest d² (bits) of the block's other targets (+inf bits when none).
+__device__ __forceinline__ NNKey lds_block_min(const v4f* tl, int b, float x, float y, float z, uint32_t& s2, v4f& cb) {
+    const v4f* tb = tl + b * kLdsLeaf;
+    const int sw = b & (kLdsLeaf - 1);
+    NNKey k1 = ~0ull;
+    s2 = 0x7f800000u;
+    cb = tb[sw];
+#pragma unroll
+    for (int t = 0; t < kLdsLeaf; ++t) {
+        const v4f c = tb[t ^ sw];
+        const float d2 = l2_simple(x, y, z, c.x, c.y, c.z);
+        const NNKey kn = make_key(d2, __float_as_uint(c.w));
+        s2 = kn < k1 ? (t == 0 ? s2 : (uint32_t)(k1 >> 32)) : min(s2, __float_as_uint(d2));
+        cb = kn < k1 ? c : cb;
+        k1 = kn < k1 ? kn : k1;
+    }
+    return k1;
+}
+
 __device__ __forceinline__ void write_corr_t(const WorkArgs& w, const PairArgs& a, int p, int i, float sx, float sy,
                                              float sz, float d2, const float4 t) {
     float4* C = w.corr + ((int64_t)p * w.x_stride + i) * 2;
@@ -1432,6 +1452,7 @@ __global__ __launch_bounds__(kLightWG) void nn_light_kernel(PairArgs a, WorkArgs
             if (gl == 0) {
                 w.nn_key[slot] = K;
                 w.nn_lu[slot] = lu_from_sec(__uint_as_float(S));
+                if (w.nn_xs) w.nn_xs[slot] = make_float4(0.f, 0.f, 0.f, 0.f);  // no Lo: no second chance
                 const float4 t = tgt[key_idx(K)];
                 w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(K)));
                 evals += (unsigned long long)nev * kLdsLeaf;
@@ -1448,16 +1469,23 @@ __global__ __launch_bounds__(kLightWG) void nn_light_kernel(PairArgs a, WorkArgs
     }
 }
 
-// ---- nn_lds_kernel<CACHE>: persistent search over the pair work list.
-template <bool CACHE>
+// ---- nn_lds_kernel<CACHE, SC>: persistent search over the pair work list.
+// SC (second chance, CACHE only): the pruning bound and the smallest-loser bookkeeping work on block
+// minima instead of single targets, so a search also yields Lo = the distance to the nearest target
+// outside the winner's 16-target kd leaf (every block is evaluated whole: the smallest losing block
+// minimum is that distance).  Stored with the query's position (nn_xs), it lets a later pass settle a
+// query the cached-neighbour test missed by evaluating just that leaf: when the leaf's best target is
+// closer than Lo - |X - X_s|, it is the exact NN (before any traversal, below).
+template <bool CACHE, bool SC>
 __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+    static_assert(CACHE || !SC, "the second chance needs the cached-neighbour state");
     constexpr int Q = kLdsQ;
     __shared__ LdsNN sh;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool corr = w.corr != nullptr && !fitness_pass;
     const int npl = uload(w.plist_n);
-    unsigned long long evals = 0, tests = 0;
+    unsigned long long evals = 0, tests = 0, sc_hits = 0;
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
@@ -1534,6 +1562,70 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int i = tid; i < nt; i += kLdsWG) sh.tl[lds_swz(i)] = tsg[i];
         }
         __syncthreads();
+        if (SC && !first && nlist > 0) {
+            // Second chance: a listed query (the test missed) whose previous NN's leaf still holds the
+            // exact NN — the leaf's best target closer than Lo moved by |X - X_s| — is settled here
+            // and dropped from the list (stable in-place compaction, chunk by chunk: a chunk's
+            // entries are all read before any of its survivors is written back, at or below them).
+            int32_t* lst = const_cast<int32_t*>(list);
+            const int32_t* tinv_p = w.tinv + (int64_t)p * w.t_stride;
+            float2* lup = w.nn_lu + (int64_t)p * w.x_stride;
+            const float4* xsp = w.nn_xs + (int64_t)p * w.x_stride;
+            float4* ntp = w.nn_t + (int64_t)p * w.x_stride;
+            int outc = 0;
+            for (int c0 = 0; c0 < nlist; c0 += kLdsWG) {
+                const int s = c0 + tid;
+                const bool in = s < nlist;
+                const int o = lst[in ? s : c0];
+                const float4 v = X[o];
+                const NNKey pk = key[o];
+                const float4 xs = xsp[o];
+                const float2 lu = lup[o];
+                const int pos = tinv_p[key_idx(pk)];
+                // the leaf's best target and runner-up d² (as lds_block_min; a partial unroll keeps the
+                // pass inside the run loop's register budget — a full one spilled)
+                const int bq = pos / kLdsLeaf, swq = bq & (kLdsLeaf - 1);
+                const v4f* tbq = sh.tl + bq * kLdsLeaf;
+                NNKey k1 = ~0ull;
+                uint32_t s2 = 0x7f800000u;
+                v4f cb = tbq[swq];
+#pragma unroll 2
+                for (int t = 0; t < kLdsLeaf; ++t) {
+                    const v4f c = tbq[t ^ swq];
+                    const float d2 = l2_simple(v.x, v.y, v.z, c.x, c.y, c.z);
+                    const NNKey kn = make_key(d2, __float_as_uint(c.w));
+                    s2 = kn < k1 ? (t == 0 ? s2 : (uint32_t)(k1 >> 32)) : min(s2, __float_as_uint(d2));
+                    cb = kn < k1 ? c : cb;
+                    k1 = kn < k1 ? kn : k1;
+                }
+                const float mx = v.x - xs.x, my = v.y - xs.y, mz = v.z - xs.z;
+                const float mv = sqrtf(mx * mx + my * my + mz * mz) * 1.00001f;
+                const float Lo = fmaxf((xs.w - mv) * 0.999999f, 0.0f);
+                const bool hit = in && cache_hit(Lo, key_d2(k1));
+                if (hit) {
+                    key[o] = k1;
+                    ntp[o] = make_float4(cb.x, cb.y, cb.z, cb.w);  // .w: the original index bits
+                    lup[o] = make_float2(fminf(lu_from_sec(__uint_as_float(s2)).x, Lo), lu.y);
+                }
+                const uint64_t km = __ballot(in && !hit);
+                evals += (unsigned long long)__builtin_popcountll(__ballot(in)) * kLdsLeaf;
+                sc_hits += (unsigned long long)__builtin_popcountll(__ballot(hit));
+                if (lane == 0) sh.u.wsum[wave] = __builtin_popcountll(km);
+                __syncthreads();
+                int base = 0, total = 0;
+                for (int u = 0; u < kLdsWaves; ++u) {
+                    const int c = sh.u.wsum[u];
+                    base += u < wave ? c : 0;
+                    total += c;
+                }
+                __syncthreads();  // every wsum read (and every entry of the chunk) before the writes
+                if (in && !hit)
+                    lst[outc + base + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))] = o;
+                outc += total;
+            }
+            nlist = outc;
+            __syncthreads();  // the compacted list visible to the whole workgroup
+        }
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
@@ -1547,7 +1639,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // runs of at most 64*Q (R = ceil(nlist / (kLdsWaves * 64 Q))), so every wave gets the same
         // share — a short list (the misses of a late pass) spreads over all waves, and the traversal,
         // latency-bound per wave, runs on small runs whose tight query box prunes most superblocks.
-        const int rounds = (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q);
+        const int rounds = max(1, (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q));
         const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
         for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
             const int cend = min(base + per, nlist);
@@ -1598,8 +1690,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
                 if (CACHE) {
                     // U of the previous search, moved since: an upper bound of the second-nearest
-                    // distance even if no evaluated target attains it (first pass: none)
+                    // distance (SC: of Lo) even if no evaluated target attains it (first pass: none)
                     uint32_t sec0 = (uint32_t)(hi >> 32);
+                    if (SC) {  // block minima: the seed leaf's and its kd sibling's (same superblock)
+                        uint32_t s2u;
+                        v4f cu;
+                        const NNKey ms = lds_block_min(sh.tl, bj ^ 1, x[q], y[q], z[q], s2u, cu);
+                        sec0 = (uint32_t)((ms > lo ? ms : lo) >> 32);
+                        lo = ms < lo ? ms : lo;
+                        evals += 64 * kLdsLeaf;
+                    }
                     if (!first) sec0 = min(sec0, __float_as_uint(uu[q] * uu[q] * 1.00001f));
                     bestl[q * 64 + lane] = lo;
                     secl[q * 64 + lane] = sec0;
@@ -1668,14 +1768,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         const v4f c = tb[t ^ sw];
                         const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
                         const NNKey kn = make_key(d2, __float_as_uint(c.w));
-                        if (CACHE) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
+                        if (CACHE && !SC) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
                         k1 = kn < k1 ? kn : k1;
                     }
                     if (CACHE) {
                         // every key but the final winner loses exactly one comparison: keep the smallest loser
                         const NNKey old = atomicMin(&bestl[qi], k1);
+                        // (SC: per block minimum — a block evaluated again yields the same minimum)
                         const uint32_t cand =
-                            k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
+                            SC ? (k1 < old ? (uint32_t)(old >> 32) : (k1 == old ? 0x7f800000u : (uint32_t)(k1 >> 32)))
+                               : (k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32)));
                         atomicMin(&secl[qi], cand);
                     } else {
                         atomicMin(&bestl[qi], k1);
@@ -1762,6 +1864,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) kbq[q] = bestl[q * 64 + lane];
 #pragma unroll
             for (int q = 0; q < Q; ++q) tq[q] = tgt[key_idx(kbq[q])];
+            int wpos[Q];  // SC: the winner's sorted position (its leaf)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) wpos[q] = SC ? tinv[key_idx(kbq[q])] : 0;
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (orig[q] < 0) continue;
@@ -1770,7 +1875,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 key[orig[q]] = kb;
                 if (CACHE) {  // the update reads X, nn_t and the key: no correspondence record
                     const int64_t slot = (int64_t)p * w.x_stride + orig[q];
-                    w.nn_lu[slot] = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                    float2 lu = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                    if (SC) {
+                        // secl is Lo: L (every target but the NN) also needs the winner leaf's runner-up
+                        uint32_t s2;
+                        v4f cw;
+                        (void)lds_block_min(sh.tl, wpos[q] / kLdsLeaf, x[q], y[q], z[q], s2, cw);
+                        w.nn_xs[slot] = make_float4(x[q], y[q], z[q], lu.x);
+                        lu.x = fminf(lu.x, lu_from_sec(__uint_as_float(s2)).x);
+                    }
+                    w.nn_lu[slot] = lu;
                     w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(kb)));
                 } else if (corr) {
                     write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
@@ -1789,6 +1903,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     if (lane == 0) {
         count_add(w.evals, 0, evals);
         count_add(w.evals, 1, tests);
+        if (SC) count_add(w.evals, 7, sc_hits);
     }
 }
 
@@ -2419,7 +2534,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
     const bool cache = w.nn_lu != nullptr;
     if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t ||
-                  !w.defer_xform))
+                  !w.nn_xs || !w.defer_xform))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
     hipError_t e;
@@ -2433,10 +2548,12 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
                        (first || !cache) ? 1 : 0, ncu);
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
     if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
-    if (cache)
-        hipLaunchKernelGGL(nn_lds_kernel<true>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    if (cache && w.second_chance)
+        hipLaunchKernelGGL((nn_lds_kernel<true, true>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    else if (cache)
+        hipLaunchKernelGGL((nn_lds_kernel<true, false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     else
-        hipLaunchKernelGGL(nn_lds_kernel<false>, dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+        hipLaunchKernelGGL((nn_lds_kernel<false, false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     if (cache && !first && w.ilist)
         hipLaunchKernelGGL(nn_light_kernel, dim3(ncu * 8), dim3(kLightWG), 0, st, a, w);
     if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;

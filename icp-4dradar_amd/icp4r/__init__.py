@@ -325,7 +325,7 @@ class Context:
         v = (C.c_uint64 * 8)()
         _check(self._lib.icp4r_nn_stats(self._h, C.byref(v)), "icp4r_nn_stats")
         keys = ("evaluations", "box_tests", "cache_hits", "cache_tested", "records_written_by_test",
-                "tested_in_update", "hits_in_update")
+                "tested_in_update", "hits_in_update", "second_chance_hits")
         return {k: int(v[i]) for i, k in enumerate(keys)}
 
     def nn_cache_hits(self) -> int:

@@ -202,7 +202,8 @@ typedef struct icp4r_nn_stats_t {
     uint64_t records_written_by_test; /* correspondence records the test kernel wrote (32 B)    */
     uint64_t tested_in_update;        /* of cache_tested: tested in the update kernel's tail    */
     uint64_t hits_in_update;          /* of cache_hits: resolved there                          */
-    uint64_t reserved[1];
+    uint64_t second_chance_hits;      /* search-list queries resolved inside the cached NN's kd
+                                         leaf (nn_lds_kernel, before any traversal)           */
 } icp4r_nn_stats_t;
 int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out);
 

@@ -289,6 +289,47 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
         assert out["1"][k]["iterations"] == o["iterations"]
 
 
+@pytest.mark.parametrize("early", [False, True])
+def test_second_chance_identical(gpu_ctx, oracle_mod, early, monkeypatch):
+    """The second chance (nn_lds_kernel<true, true>: searches keep Lo, the distance to the nearest
+    target outside the NN's kd leaf; a later miss whose leaf still provably holds the NN is settled
+    without a traversal): bit-identical batches with it off, with the light per-query search taking
+    the small pairs (it resets Lo), over ragged shapes, lattice ties and duplicate targets; the oracle
+    on sampled pairs; and it settles a good share of the misses."""
+    import icp4r
+
+    rng = np.random.default_rng(11)
+    lat = _lattice(rng, 14)
+    ls = lat.copy()
+    ls[:, :3] += np.float32(0.25)
+    dup = _pair(1499, 4096)
+    dup = (dup[0], np.concatenate([dup[1], dup[1][::3]]))  # exact duplicate targets
+    shapes = [(8192, 8192)] * 240 + [(8000, 8100), (4096, 8192), (2048, 600), (1000, 1200), (37, 4000)] * 3
+    pairs = [_pair(1400 + k, n, m) for k, (n, m) in enumerate(shapes)] + [(ls, lat), dup]
+    args = _batch(pairs)
+    assert icp4r.plan(len(pairs), 8192, 8192)["lds"] and icp4r.plan(len(pairs), 8192, 8192)["cache"]
+    kw = {} if early else dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    p = icp4r.default_params(max_iterations=20, **kw)
+    out = {}
+    for sc, light in (("0", "0"), ("1", "0"), ("1", "200")):
+        monkeypatch.setenv("ICP4R_SECOND_CHANCE", sc)
+        monkeypatch.setenv("ICP4R_LIGHT_MAX", light)
+        gpu_ctx.reset_timers()
+        out[sc + light] = gpu_ctx.align_batch_host(*args, params=p)
+        st = gpu_ctx.nn_stats()
+        if sc == "1" and light == "0":
+            assert st["second_chance_hits"] > 0.2 * (st["cache_tested"] - st["cache_hits"])
+        if sc == "0":
+            assert st["second_chance_hits"] == 0
+    assert out["10"].tobytes() == out["00"].tobytes()
+    assert out["1200"].tobytes() == out["00"].tobytes()
+    assert (out["10"]["status"] == 0).all()
+    for k in (0, 239, 243, 244, len(pairs) - 2, len(pairs) - 1):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20, **kw)
+        assert (out["10"][k]["T"].reshape(4, 4).T == o["T"]).all() and out["10"][k]["fitness"] == o["fitness"]
+        assert out["10"][k]["iterations"] == o["iterations"]
+
+
 def test_light_search_identical(gpu_ctx, oracle_mod, monkeypatch):
     """nn_light_kernel (per-query 16-lane search from the index in HBM, for pairs with few cache
     misses) returns exactly what the LDS work-list search returns: the batch is bit-identical with
