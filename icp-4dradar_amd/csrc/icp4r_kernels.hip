@@ -178,31 +178,52 @@ __device__ __forceinline__ void write_corr(const WorkArgs& w, const PairArgs& a,
 constexpr int kInitWG = 256;
 __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     __shared__ float Tg[16];
-    __shared__ int ident, invalid;
+    __shared__ int ident;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     const int tid = threadIdx.x;
     const int n = a.src_n[p], m = a.tgt_n[p];
     const float4* src = a.src + a.src_off[p];
     const float4* tgt = a.tgt + a.tgt_off[p];
     PairState& st = w.state[p];
-    int bad = 0;
-    for (int i = tid; i < m; i += kInitWG) {
-        const float4 t = tgt[i];
-        bad |= !(isfinite(t.x) && isfinite(t.y) && isfinite(t.z));
+    if (tid < 16) Tg[tid] = a.guess ? a.guess[(int64_t)p * 16 + tid] : ((tid % 5 == 0) ? 1.0f : 0.0f);
+    __syncthreads();
+    if (tid == 0) {
+        bool id = true;
+        for (int k = 0; k < 16; ++k) id = id && (Tg[k] == ((k % 5 == 0) ? 1.0f : 0.0f));
+        ident = id ? 1 : 0;
     }
-    for (int i = tid; i < n; i += kInitWG) {
-        const float4 s = src[i];
-        bad |= !(isfinite(s.x) && isfinite(s.y) && isfinite(s.z));
+    __syncthreads();
+    // One pass over the source: validated and written transformed (transformCloud(input, guess)) in
+    // the same read — X of a pair found invalid below is never read.  Counts above the workspace
+    // stride are not copied (too_big below marks the pair invalid).  kInitPer points per thread in
+    // flight, every load of a round before its stores.
+    constexpr int kInitPer = 4;
+    float4* X = w.X + (int64_t)p * w.x_stride;
+    const bool id = ident != 0;
+    const int nc = min(n, (int)w.x_stride);
+    int bad = 0;
+    for (int i0 = 0; i0 < m; i0 += kInitWG * kInitPer) {
+        float4 t[kInitPer];
+#pragma unroll
+        for (int e = 0; e < kInitPer; ++e) t[e] = tgt[min(i0 + e * kInitWG + tid, m - 1)];
+#pragma unroll
+        for (int e = 0; e < kInitPer; ++e) bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
+    }
+    for (int i0 = 0; i0 < n; i0 += kInitWG * kInitPer) {
+        float4 v[kInitPer];
+#pragma unroll
+        for (int e = 0; e < kInitPer; ++e) v[e] = src[min(i0 + e * kInitWG + tid, n - 1)];
+#pragma unroll
+        for (int e = 0; e < kInitPer; ++e) {
+            const int i = i0 + e * kInitWG + tid;
+            bad |= !(isfinite(v[e].x) && isfinite(v[e].y) && isfinite(v[e].z));
+            float4 o = v[e];
+            if (!id) xform_pt(Tg, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            if (i < nc) X[i] = o;
+        }
     }
     bad = __syncthreads_or(bad);
     if (tid == 0) {
-        bool id = true;
-        for (int k = 0; k < 16; ++k) {
-            const float g = a.guess ? a.guess[(int64_t)p * 16 + k] : ((k % 5 == 0) ? 1.0f : 0.0f);
-            Tg[k] = g;
-            id = id && (g == ((k % 5 == 0) ? 1.0f : 0.0f));
-        }
-        ident = id ? 1 : 0;
         mat4_identity(st.T_inc);
         st.prev_mse = DBL_MAX;
         st.similar = 0;
@@ -216,23 +237,11 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
             mat4_identity(st.final_T);
             st.phase = kPhaseInvalid;
             st.status = too_big ? kStatusInvalid : m <= 0 ? kStatusEmpty : kStatusNonFinite;
-            invalid = 1;
         } else {
             for (int k = 0; k < 16; ++k) st.final_T[k] = Tg[k];  // final_transformation_ = guess
             st.phase = kPhaseActive;
             st.status = 0;
-            invalid = 0;
         }
-    }
-    __syncthreads();
-    if (invalid) return;
-    float4* X = w.X + (int64_t)p * w.x_stride;
-    const bool id = ident != 0;
-    for (int i = tid; i < n; i += kInitWG) {
-        const float4 s = src[i];
-        float4 o = s;
-        if (!id) xform_pt(Tg, s.x, s.y, s.z, o.x, o.y, o.z);  // transformCloud(input, guess)
-        X[i] = o;
     }
 }
 
