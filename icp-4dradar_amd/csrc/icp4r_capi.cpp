@@ -232,6 +232,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.tbox = static_cast<float4*>(ctx->tbox.p);
         w.sbox = static_cast<float4*>(ctx->sbox.p);
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
+        HIP_TRY(ctx->kdn.ensure((size_t)npairs * kKdnStride * sizeof(uint32_t)));
+        w.kdn = static_cast<uint32_t*>(ctx->kdn.p);
         if (pl.lds) {
             HIP_TRY(ctx->plist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
             HIP_TRY(ctx->plist_n.ensure(4 * kMaxGroups * sizeof(int32_t)));  // per group: items, queue, part size
@@ -329,6 +331,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.tbox += (int64_t)p0 * 2 * w.b_stride;
         wg.sbox += (int64_t)p0 * 2 * w.sb_stride;
         wg.sperm += xs;
+        if (wg.kdn) wg.kdn += (int64_t)p0 * kKdnStride;
     }
     if (wg.nn_lu) {
         wg.nn_lu += xs;
@@ -364,6 +367,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     int rc;
     const bool pcl = a.kp.numerics == kNumericsPCL;
     if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl, st, w))) return rc;
+    w.src_by_tgt = pl.pruned ? (env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0) : 0;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
@@ -553,7 +557,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     }
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->nn_xs, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->nn_xs, &ctx->kdn, &ctx->sinv, &ctx->qlist, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ilist, &ctx->ilist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})

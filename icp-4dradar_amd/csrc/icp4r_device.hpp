@@ -54,6 +54,12 @@ __device__ __forceinline__ NNKey make_key(float d2, uint32_t idx) {
     return ((NNKey)__float_as_uint(d2) << 32) | idx;
 }
 
+// A first-pass seed key (src_order_kernel): d² = +inf and an index inside the target (anything else
+// in nn_key before the first pass is stale and ignored).
+__device__ __forceinline__ bool seed_key(NNKey k, int m) {
+    return (uint32_t)(k >> 32) == 0x7f800000u && (uint32_t)k < (uint32_t)m;
+}
+
 // Box pruning is conservative in float: a box lower bound is shrunk by 2^-16 before its `<=` test
 // against a d², which covers the few-ulp rounding of both the bound and l2_simple.
 constexpr float kLbShrink = 1.0f - 1.0f / 65536.0f;

@@ -26,6 +26,8 @@ constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest targe
 constexpr int kCacheMaxN = 16384; // cached-neighbour test (nn_lds_kernel<true>): max source points per pair
 // Work counters: one 128-B slot per wave (mod kCountSlots).  A single counter word hit by every wave
 // of a launch serialises the atomics at one L2 channel (~10 ns each: 30k waves = 0.3 ms per launch).
+constexpr int kKdNodes = 2048;                 // kd tree nodes kept per target (heap ids < this)
+constexpr int kKdnStride = 8 + kKdNodes;
 constexpr int kCountSlots = 2048;
 constexpr int kCountStride = 16;
 
@@ -107,6 +109,11 @@ struct WorkArgs {
     int32_t leaf;       // pruned: targets per block (16 or 32); 0 = brute force
     int32_t kd_index;   // clouds of <= 8192 points get the balanced kd order (index_kernel), else Morton;
                         // bit 0: targets, bit 1: sources
+    int32_t src_by_tgt; // 1: a source whose target gets the kd order is ordered by descending the target's
+                        // kd tree (src_order_kernel) instead of by its own tree: queries sorted by the
+                        // target leaf they fall in, and that leaf seeds their first search
+    uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,
+                        // [8 + node] internal node (heap order) = 1 << 31 | mid << 13 | axis << 11 | key
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):
     float4* tsort;      // [npairs * t_stride] targets in index order (kd / Morton), .w = original index bits;
                         // positions [m, t_stride): +inf coordinates (never a match)

@@ -381,8 +381,12 @@ __device__ __forceinline__ int kd_split(int S, int leaf) {
 // counting sorts of the coordinate quantised to kKdBins levels over the cloud's extent; the order
 // of equal keys (LDS atomics) is arbitrary, which only moves points between the two sides of a
 // split among equals — the search is exact for any order.
+// kdn (nullable): the tree is also written out for src_order_kernel — the quantisation (lo, scale
+// bits at [0, 6)) and every internal node at [8 + heap id] (root 1, children 2i / 2i + 1) as
+// 1 << 31 | mid << 13 | axis << 11 | key of the first point right of the split (on its axis); the
+// caller zeroes the node slots (0: leaf).
 template <typename Get>  // Get: int -> float4, point i of the cloud
-__device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
+__device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, uint32_t* kdn = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
     // 1. bounding box -> quantisation
@@ -414,6 +418,10 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
         }
         sh.lo[tid] = l;
         sh.sc[tid] = h > l ? (float)kKdBins / (h - l) : 0.0f;
+        if (kdn) {
+            kdn[tid] = __float_as_uint(l);
+            kdn[3 + tid] = __float_as_uint(sh.sc[tid]);
+        }
     }
     __syncthreads();
     const float lo[3] = {sh.lo[0], sh.lo[1], sh.lo[2]}, sc[3] = {sh.sc[0], sh.sc[1], sh.sc[2]};
@@ -472,7 +480,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
     // multiples of 16 >= kKdPer, so a thread's positions [p0, p0 + kKdPer) share one segment [s, e),
     // tracked per thread; the thread owning a segment's first position decides its split.
     const int p0 = tid * kKdPer;
-    int s = 0, e = n;
+    int s = 0, e = n, node = 1;  // this thread's segment and its heap id
     for (;;) {
         bool any = false;
         if (p0 == s && p0 < n) {
@@ -484,6 +492,9 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
                 for (int a = 0; a < 3; ++a) ext[a] = (float)(sh.q[a][sh.L[a][e - 1]] - sh.q[a][sh.L[a][s]]) / sc[a];
                 ax = ext[0] >= ext[1] && ext[0] >= ext[2] ? 0 : (ext[1] >= ext[2] ? 1 : 2);
                 any = true;
+                if (kdn && node < kKdNodes)
+                    kdn[8 + node] = 0x80000000u | ((uint32_t)(s + h) << 13) | ((uint32_t)ax << 11) |
+                                    (uint32_t)sh.q[ax][sh.L[ax][s + h]];
             }
             sh.seg_mid[tid] = (uint16_t)(s + h);
             sh.seg_ax[tid] = ax;
@@ -567,8 +578,13 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk) {
                     sh.L[a][np] = v[a][k];
                 }
             }
-            if (p0 < mid) e = mid;
-            else s = mid;
+            if (p0 < mid) {
+                e = mid;
+                node = 2 * node;
+            } else {
+                s = mid;
+                node = 2 * node + 1;
+            }
         }
         __syncthreads();
     }
@@ -613,6 +629,12 @@ __device__ void index_boxes(const WorkArgs& w, int p, int n) {
     }
 }
 
+// The source of pair p is ordered by its target's kd tree (src_order_kernel) rather than its own.
+__device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArgs& w, int p) {
+    const int m = a.tgt_n[p];
+    return w.src_by_tgt && w.kdn && (w.kd_index & 1) && m > 0 && m <= kKdMaxN && w.t_stride <= kKdMaxN;
+}
+
 __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     __shared__ IndexShared shu;
     const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * 2);
@@ -623,9 +645,13 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
     if (n <= 0) return;
     const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
+    if (!is_tgt && src_by_tgt_tree(a, w, p)) return;  // src_order_kernel orders it
     if ((w.kd_index & (is_tgt ? 1 : 2)) && n <= kKdMaxN && (!is_tgt || w.t_stride <= kKdMaxN)) {
         uint64_t* tk = (w.ticks && p == 0 && is_tgt && tid == 0) ? w.ticks + 12 : nullptr;
-        kd_order(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk);
+        uint32_t* kdn = (is_tgt && w.kdn && w.src_by_tgt) ? w.kdn + (int64_t)p * kKdnStride : nullptr;
+        if (kdn)
+            for (int k = tid; k < kKdnStride; k += kIdxWG) kdn[k] = 0u;  // (kd_order syncs before writing)
+        kd_order(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
         const uint16_t* ord = shu.kd.L[0];
         if (is_tgt) {
             // sorted targets, padding (+inf coordinates, .w = the last target's index: never a match,
@@ -772,6 +798,88 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             sp[pos] = i;
             if (si) si[i] = (int32_t)pos;
         }
+    }
+}
+
+// src_order_kernel: one workgroup per pair whose target has the kd order (src_by_tgt_tree).  Every
+// source point descends the target's kd tree (the quantised key of the node's axis against the key of
+// the first point right of the split; equal keys sit on both sides, so they may go either way — the
+// order only decides how well the search prunes), and a counting sort by the leaf reached gives the
+// source order (sperm / sinv): consecutive queries fall in the same or neighbouring target leaves, so
+// query runs stay compact, and the leaf's first target seeds the query's first search (nn_key with
+// d² = +inf, read by the first pass).  It replaces the source's own kd build (index_kernel).
+constexpr int kSoWG = 256;
+
+__global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w) {
+    __shared__ uint32_t nodes[kKdNodes];
+    __shared__ uint32_t bins[kKdMaxN / 16];
+    __shared__ uint32_t wsum[kSoWG / 64];
+    __shared__ float qz[6];
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    if (w.state[p].phase == kPhaseInvalid || !src_by_tgt_tree(a, w, p)) return;
+    const int n = a.src_n[p], m = a.tgt_n[p];
+    if (n <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int B = w.leaf;
+    const int nb = (m + B - 1) / B;  // <= kKdMaxN / 16
+    const uint32_t* kd = w.kdn + (int64_t)p * kKdnStride;
+    for (int k = tid; k < kKdNodes; k += kSoWG) nodes[k] = kd[8 + k];
+    if (tid < 6) qz[tid] = __uint_as_float(kd[tid]);
+    for (int b = tid; b < kKdMaxN / 16; b += kSoWG) bins[b] = 0u;
+    __syncthreads();
+    const float lo[3] = {qz[0], qz[1], qz[2]}, sc[3] = {qz[3], qz[4], qz[5]};
+    const float4* src = a.src + a.src_off[p];
+    auto leaf_of = [&](const float4 v) {
+        const int k0 = min(kKdBins - 1, max(0, (int)((v.x - lo[0]) * sc[0])));
+        const int k1 = min(kKdBins - 1, max(0, (int)((v.y - lo[1]) * sc[1])));
+        const int k2 = min(kKdBins - 1, max(0, (int)((v.z - lo[2]) * sc[2])));
+        int node = 1, s = 0;
+        while (node < kKdNodes) {
+            const uint32_t nd = nodes[node];
+            if (!(nd >> 31)) break;
+            const int ax = (int)((nd >> 11) & 3u), thr = (int)(nd & 2047u);
+            const int k = ax == 0 ? k0 : (ax == 1 ? k1 : k2);
+            const bool right = k >= thr;
+            s = right ? (int)((nd >> 13) & 0x3fffu) : s;
+            node = 2 * node + (right ? 1 : 0);
+        }
+        return min(s / B, nb - 1);
+    };
+    for (int i = tid; i < n; i += kSoWG) atomicAdd(&bins[leaf_of(src[i])], 1u);
+    __syncthreads();
+    {  // exclusive scan of the nb bins: thread t owns bins [2t, 2t + 2)
+        constexpr int per = kKdMaxN / 16 / kSoWG;
+        uint32_t loc[per], run = 0;
+#pragma unroll
+        for (int k = 0; k < per; ++k) {
+            loc[k] = run;
+            run += bins[tid * per + k];
+        }
+        uint32_t incl = run;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int v = 0; v < wave; ++v) base += wsum[v];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < per; ++k) bins[tid * per + k] = base + incl - run + loc[k];
+    }
+    __syncthreads();
+    int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
+    int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const float4* ts = w.tsort + (int64_t)p * w.t_stride;
+    for (int i = tid; i < n; i += kSoWG) {
+        const int b = leaf_of(src[i]);
+        const uint32_t pos = atomicAdd(&bins[b], 1u);
+        sp[pos] = i;
+        if (si) si[i] = (int32_t)pos;
+        key[i] = make_key(INFINITY, __float_as_uint(ts[b * B].w));  // first-pass seed: the leaf's first target
     }
 }
 
@@ -931,7 +1039,9 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
         x[q] = v.x;
         y[q] = v.y;
         z[q] = v.z;
-        const uint32_t j = first ? __float_as_uint(tsg[((int64_t)s * m) / n].w) : (uint32_t)key_idx(key[o]);
+        const NNKey k0 = key[o];  // first pass: src_order_kernel's seed key (d² = +inf) or stale
+        const uint32_t j = (first && !seed_key(k0, m)) ? __float_as_uint(tsg[((int64_t)s * m) / n].w)
+                                                       : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
         const float4 t = tgt[j];
         best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
     }
@@ -1672,12 +1782,14 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) {
                 orig[q] = base + lane + q * 64 < cend ? o_[q] : -1;
                 v[q] = X[o_[q]];
-                pk[q] = first ? 0ull : key[o_[q]];
+                pk[q] = key[o_[q]];  // first pass: src_order_kernel's seed key (d² = +inf) or stale
                 uu[q] = (CACHE && !first) ? w.nn_lu[(int64_t)p * w.x_stride + o_[q]].y : 0.0f;
             }
             int pj[Q];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) pj[q] = first ? (int)(((int64_t)sidx[q] * m) / n) : tinv[key_idx(pk[q])];
+            for (int q = 0; q < Q; ++q)
+                pj[q] = (first && !seed_key(pk[q], m)) ? (int)(((int64_t)sidx[q] * m) / n)
+                                                       : tinv[min((uint32_t)key_idx(pk[q]), (uint32_t)(m - 1))];
             const int seed_pos0 = pj[0];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
@@ -2532,6 +2644,8 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     hipLaunchKernelGGL(index_kernel, dim3(npairs, 2), dim3(kIdxWG), 0, st, a, w);
+    if (w.src_by_tgt && w.kdn)
+        hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);
     if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))
         hipLaunchKernelGGL(index_refine_kernel, dim3((unsigned)((w.t_stride + kKdMaxN - 1) / kKdMaxN), npairs),
                            dim3(kIdxWG), 0, st, a, w);

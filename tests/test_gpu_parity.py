@@ -289,6 +289,34 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
         assert out["1"][k]["iterations"] == o["iterations"]
 
 
+@pytest.mark.parametrize("npairs", [1, 300])
+def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
+    """Sources ordered by descending their target's kd tree (src_order_kernel, default) or by their
+    own kd tree (ICP4R_SRC_ORDER=0): the order and the first-pass seeds change, the registrations do
+    not — bit-identical on the single-pair pruned kernel and the batched LDS search, ragged shapes,
+    a lattice (ties) and targets over 8192 points (their sources keep the own-tree path)."""
+    import icp4r
+
+    rng = np.random.default_rng(5)
+    lat = _lattice(rng, 13)
+    ls = lat.copy()
+    ls[:, :3] += np.float32(0.25)
+    if npairs == 1:
+        pairs = [_pair(1600, 8192)]
+    else:
+        shapes = [(8192, 8192)] * (npairs - 8) + [(8000, 8100), (4096, 8192), (2048, 600), (1000, 1200),
+                                                   (37, 4000), (3, 700), (8192, 9000)]
+        pairs = [_pair(1600 + k, n, m) for k, (n, m) in enumerate(shapes)] + [(ls, lat)]
+    args = _batch(pairs)
+    p = icp4r.default_params(max_iterations=15)
+    out = {}
+    for so in ("0", "1"):
+        monkeypatch.setenv("ICP4R_SRC_ORDER", so)
+        out[so] = gpu_ctx.align_batch_host(*args, params=p)
+    assert out["0"].tobytes() == out["1"].tobytes()
+    assert (out["1"]["status"] == 0).all()
+
+
 @pytest.mark.parametrize("early", [False, True])
 def test_second_chance_identical(gpu_ctx, oracle_mod, early, monkeypatch):
     """The second chance (nn_lds_kernel<true, true>: searches keep Lo, the distance to the nearest
