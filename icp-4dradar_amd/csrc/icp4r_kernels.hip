@@ -2202,6 +2202,9 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 //          a plain sum — IEEE addition is commutative, so p + acc == a*b + acc bit for bit.
 // Rejected correspondences contribute the fold's identity (-0.0f / +0), i.e. nothing.
 constexpr int kFoldWG = 256;
+#ifndef ICP4R_TAIL_PER
+#define ICP4R_TAIL_PER 4  // fused test: points per thread per pipelined group
+#endif
 constexpr int kFoldWaves = kFoldWG / 64;
 constexpr int kFoldChunkP = 512;
 
@@ -2393,32 +2396,43 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
         float2* lu = w.nn_lu + (int64_t)p * xs;
         const float4* nt = w.nn_t + (int64_t)p * xs;
         const int32_t* sinv = w.sinv + (int64_t)p * xs;
-        constexpr int kPer = 4;  // points per thread in flight (8 pushed the kernel past 128 VGPRs: 3 workgroups per CU)
+        // kPer points per thread per group, software-pipelined: the next group's loads are issued
+        // before this group's stores, so the stores drain while the loads are in flight (a load
+        // issued after a store would wait behind it on vmcnt)
+        constexpr int kPer = ICP4R_TAIL_PER;
+        constexpr int kStep = kFoldWG * kPer;
         int hits = 0, misses = 0;
-        for (int i0 = 0; i0 < n; i0 += kFoldWG * kPer) {
-            float4 v[kPer], t[kPer];
-            float2 L[kPer];
-            int32_t sp[kPer];
+        float4 v[kPer], t[kPer];
+        float2 L[kPer];
+        int32_t sp[kPer];
+        auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float2 (&LL)[kPer], int32_t (&ss)[kPer]) {
 #pragma unroll
-            for (int e = 0; e < kPer; ++e) {  // every load before the first store
+            for (int e = 0; e < kPer; ++e) {
                 const int i = min(i0 + e * kFoldWG + tid, n - 1);
-                v[e] = X[i];
-                t[e] = nt[i];
-                L[e] = lu[i];
-                sp[e] = sinv[i];
+                vv[e] = X[i];
+                tt[e] = nt[i];
+                LL[e] = lu[i];
+                ss[e] = sinv[i];
             }
+        };
+        load(0, v, t, L, sp);
+        for (int i0 = 0; i0 < n; i0 += kStep) {
+            float4 vn[kPer], tn[kPer];
+            float2 Ln[kPer];
+            int32_t spn[kPer];
+            if (i0 + kStep < n) load(i0 + kStep, vn, tn, Ln, spn);
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
                 const int i = i0 + e * kFoldWG + tid;
                 const bool valid = i < n;
                 float4 o = v[e];
                 xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
-                const float2 Ln = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+                const float2 Lm = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
                 const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
-                const bool hit = valid & cache_hit(Ln.x, d2);
+                const bool hit = valid & cache_hit(Lm.x, d2);
                 if (valid) {
                     X[i] = o;
-                    lu[i] = Ln;
+                    lu[i] = Lm;
                 }
                 if (hit) {
                     key[i] = make_key(d2, __float_as_uint(t[e].w));
@@ -2427,6 +2441,13 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
                     atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
                     ++misses;
                 }
+            }
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                v[e] = vn[e];
+                t[e] = tn[e];
+                L[e] = Ln[e];
+                sp[e] = spn[e];
             }
         }
         hits = wave_sum(hits);
