@@ -2208,8 +2208,17 @@ constexpr int kFoldWG = 256;
 constexpr int kFoldWaves = kFoldWG / 64;
 constexpr int kFoldChunkP = 512;
 
+// Each fold chain's row is padded by kFoldPad floats: unpadded, rows 2 KB apart start on the same
+// LDS bank, and the 7-9 fold lanes' ds_read_b128 of one column were a 7-9-way bank conflict on every
+// read.  Padded by 16 B they take distinct banks.
+#ifndef ICP4R_FOLD_PAD
+#define ICP4R_FOLD_PAD 4
+#endif
+constexpr int kFoldPad = ICP4R_FOLD_PAD;
+constexpr int kFoldRow = kFoldChunkP + kFoldPad;
+
 struct FoldShared {
-    float buf[2][9][kFoldChunkP];
+    float buf[2][9][kFoldRow];
     float res[8];
     int32_t cnt[kFoldWaves];
     SolveShared s;
@@ -2262,7 +2271,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     // chunk costs one global round trip, not one per element.
     constexpr int kPerA = (kFoldChunkP + (kFoldWG - 128) - 1) / (kFoldWG - 128);
     auto fill_a = [&](int c) {  // waves 2, 3 (and 1 without the MSE chain)
-        float(*b)[kFoldChunkP] = sh.buf[c & 1];
+        float(*b)[kFoldRow] = sh.buf[c & 1];
         const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
         float4 r[kPerA][2];
 #pragma unroll
@@ -2331,7 +2340,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     const float md[3] = {sh.s.mean[3], sh.s.mean[4], sh.s.mean[5]};
     constexpr int kFillB = kFoldWG - 64, kPerB = (kFoldChunkP + kFillB - 1) / kFillB;
     auto fill_b = [&](int c) {  // waves 1..3
-        float(*b)[kFoldChunkP] = sh.buf[c & 1];
+        float(*b)[kFoldRow] = sh.buf[c & 1];
         const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
         float4 r[kPerB][2];
 #pragma unroll
