@@ -1,11 +1,18 @@
-import os, sys, numpy as np
-sys.path.insert(0, "/root/repo/icp-4dradar_amd"); sys.path.insert(0, "/root/repo/tests")
+"""NN work counters of a 256-pair 8k batch with the second chance off and on (diagnostic).
+
+    python tools/sc_stats.py
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import icp4r
 from icp4r import synth
 pairs = [synth.make_pair(1000 + k, 8192) for k in range(256)]
-src = np.concatenate([p.src_xyzi() for p in pairs]).astype(np.float32)
-tgt = np.concatenate([p.tgt_xyzi() for p in pairs]).astype(np.float32)
-sn = np.full(256, 8192, np.int32)
 ctx = icp4r.Context(0)
 p = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
 from test_gpu_parity import _batch
