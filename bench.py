@@ -3,21 +3,39 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+With ``--gpus N > 1`` and no ``WORLD_SIZE`` in the environment, bench.py starts
+``torch.distributed.run`` with N ranks as a CHILD process (before anything here touches the GPU) and
+exits with its status; the driver's own ``torch.distributed.run`` launch lands directly in the rank
+code.
+
 Workload (BASELINE.json configs[2]/[3]): every rank registers its own batch of
 1024 independent synthetic radar scan pairs (8192 source / 8192 target points, pair i seeded
 1000 + i, rank r owns pairs [1024 r, 1024 (r + 1))), 20 ICP iterations exactly (PCL defaults
 otherwise; the |ΔMSE| early stop disabled so every pair does the same work) plus the fitness pass.
 A step = one device-resident batch registration + the all-gather of the 96-B result structs over
 RCCL.  Inputs are resident in HBM before timing.  value = pairs registered by all ranks / max-over-
-ranks wall time.  "roofline" prices the dominant kernel (the NN sweep) from the library's HIP events
-on the launch stream; "cpu_baseline" times the oracle (the C restatement of the reference CPU path)
-single-threaded on a bounded sample of the same pairs.
+ranks wall time.  The results checked (status, iterations, pairs of every rank and both pair groups
+against the oracle) are the TIMED run's, copied before any diagnostic rerun.
+
+Beside the headline: ``incl_upload`` (the same steps with each batch's H2D upload from pinned host
+memory inside the timed region, overlapped with the previous batch on a copy stream), ``gather``
+(the all-gather timed alone), ``roofline`` (the dominant kernel, the batched search, from the
+library's HIP events on its launch stream), ``c5`` (the scan-to-map config, priced against HBM) and
+``cpu_baseline`` (the oracle — the C restatement of the reference CPU path — on one pinned core,
+with median / p90 per pair, and on all the process's cores, both running the node's two fitness
+passes, ``iterative_closest_point.cpp:516,:520``).
+
+``--dry-run`` exercises the launcher, the sharding and the gather on CPU (gloo, no GPU, no
+registration): every rank fills its result rows with their global pair index, and rank 0 checks the
+gathered order (tests/test_bench_launcher.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,7 +50,7 @@ FLOP_PER_PAIR_EVAL = 8     # 3 sub + 3 mul + 2 add (FLANN L2_Simple); compare/se
 FLOP_PER_BOX_TEST = 11     # 6 sub + 3 mul + 2 add (point-to-box lower bound); max/compare not counted
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -40,12 +58,76 @@ def parse():
     ap.add_argument("--pairs", type=int, default=1024, help="pairs per GPU")
     ap.add_argument("--points", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline time budget (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="single-core CPU-baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-all-seconds", type=float, default=8.0, help="all-cores CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--check", type=int, default=2, help="pairs checked against the oracle after timing")
-    return ap.parse_args()
+    ap.add_argument("--no-upload", action="store_true", help="skip the incl-upload figure")
+    ap.add_argument("--no-c5", action="store_true", help="skip the scan-to-map (C5) figure")
+    ap.add_argument("--check", type=int, default=8, help="pairs of the timed run checked against the oracle "
+                                                         "(N=1; with N>1 two per rank)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher/shard/gather only, gloo on CPU (tests)")
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    """N ranks through torch.distributed.run, as a child process (never exec from here)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def _env_rank():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def _metric():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        return json.load(f)["metric"]
+
+
+# ------------------------------------------------------------------------------------------ dry run
+def run_dry(args) -> int:
+    import torch
+    import torch.distributed as dist
+
+    from icp4r import RESULT_DTYPE
+    from icp4r import dist as idist
+
+    world, rank, _ = _env_rank()
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    P = args.pairs
+    mine = idist.shard(rank, world, P)
+    rows = np.zeros(P, RESULT_DTYPE)
+    rows["reserved"] = np.arange(mine.start, mine.stop, dtype=np.int32)
+    rows["iterations"] = args.iters
+    local = torch.from_numpy(rows.view(np.uint8).reshape(P, 96).copy())
+    t0 = time.perf_counter()
+    allr = idist.gather_results(local, world)
+    elapsed = time.perf_counter() - t0
+    res = np.frombuffer(allr.numpy().tobytes(), dtype=RESULT_DTYPE)
+    order_ok = bool(len(res) == world * P and (res["reserved"] == np.arange(world * P)).all())
+    if rank == 0:
+        print(json.dumps({"metric": _metric(), "dry_run": True, "n_gpus": world, "pairs_per_gpu": P,
+                          "gathered_pairs": int(len(res)), "gather_order_ok": order_ok,
+                          "gather_ms": elapsed * 1e3}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if order_ok else 1
+
+
+# ------------------------------------------------------------------------------------------ inputs
 def make_shard(first: int, count: int, n: int):
     from icp4r import synth
 
@@ -58,42 +140,133 @@ def make_shard(first: int, count: int, n: int):
     return src, tgt
 
 
-def cpu_baseline(src, tgt, iters: int, budget_s: float) -> dict:
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # checker / CPU baseline only
+def _pose_err(T, To):
+    T = np.asarray(T, np.float64)
+    To = np.asarray(To, np.float64)
+    M = T[:3, :3].T @ To[:3, :3]
+    dr = float(np.arctan2(np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2,
+                          (np.trace(M) - 1) / 2))
+    return float(np.abs(T[:3, 3] - To[:3, 3]).max()), dr
 
-    done, t0 = 0, time.perf_counter()
-    while done < len(src) and (time.perf_counter() - t0) < budget_s:
-        oracle.align(src[done], tgt[done], numerics=oracle.NUM_F32, max_iterations=iters, mse_threshold_absolute=-1.0,
-                     transformation_epsilon=-1.0)
-        done += 1
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
+
+def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": done / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"{done} pairs of the benchmark workload ({src.shape[1]}/{tgt.shape[1]} pts, {iters} iters "
-                      f"+ fitness), oracle/icp_oracle.c: FLANN-style kd-tree NN + float Umeyama, -O2, 1 thread, "
-                      f"{dt:.1f} s on {cpu} (nproc={os.cpu_count()})"}
+    return "unknown"
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------------------------------ CPU baseline
+def cpu_baseline(src, tgt, iters: int, budget_s: float, all_budget_s: float) -> dict:
+    """The oracle (C restatement of PCL 1.8.1 ICP, -O2) per pair as the node calls it: align, then
+    getFitnessScore twice (`iterative_closest_point.cpp:514,:516,:520`; the oracle's align computes
+    the first).  Single core (the calling thread pinned to one CPU) with per-pair median / p90, and
+    all the process's cores (a thread pool; the oracle's ctypes calls release the GIL)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from concurrent.futures import ThreadPoolExecutor
+
+    import oracle  # checker / CPU baseline only
+
+    kw = dict(numerics=oracle.NUM_F32, max_iterations=iters, mse_threshold_absolute=-1.0,
+              transformation_epsilon=-1.0)
+
+    def one(k):
+        t0 = time.perf_counter()
+        o = oracle.align(src[k], tgt[k], **kw)
+        oracle.fitness(src[k], tgt[k], o["T"])  # the node's second getFitnessScore (:520)
+        return time.perf_counter() - t0
+
+    allowed = sorted(os.sched_getaffinity(0))
+    # the box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there); never more than allowed
+    threads = max(1, min(len(allowed), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    # all cores first: pool threads inherit the (full) affinity of the thread that creates them
+    n_all, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while (time.perf_counter() - t0) < all_budget_s and n_all < len(src):
+            chunk = list(range(n_all, min(len(src), n_all + threads)))
+            list(ex.map(one, chunk))
+            n_all += len(chunk)
+    dt_all = time.perf_counter() - t0
+    # one pinned core
+    core = allowed[0]
+    os.sched_setaffinity(0, {core})
+    try:
+        one(0)  # warm-up
+        per, t0 = [], time.perf_counter()
+        while len(per) < len(src) and (time.perf_counter() - t0) < budget_s:
+            per.append(one(len(per)))
+        dt = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, set(allowed))
+    per_ms = np.array(per) * 1e3
+    cpu = _cpu_model()
+    return {"value": len(per) / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "per_pair_ms_median": float(np.median(per_ms)), "per_pair_ms_p90": float(np.percentile(per_ms, 90)),
+            "fitness_passes": 2,
+            "sample": f"{len(per)} pairs of the benchmark workload ({src.shape[1]}/{tgt.shape[1]} pts, {iters} iters "
+                      f"+ 2 getFitnessScore passes as the node calls them), oracle/icp_oracle.c: FLANN-style kd-tree "
+                      f"NN + float Umeyama, -O2, 1 thread pinned to CPU {core}, {dt:.1f} s on {cpu} "
+                      f"(nproc={os.cpu_count()}, {len(allowed)} CPUs allowed)",
+            "all_cores": {"value": n_all / dt_all, "unit": "pairs/s", "cores": threads,
+                          "sample": f"{n_all} pairs on a {threads}-thread pool over {dt_all:.1f} s (the box's CPU "
+                                    f"share for one GPU)"}}
+
+
+# ------------------------------------------------------------------------------------------ C5
+def c5_measure(ctx, dev, iters: int = 20, reps: int = 10) -> dict:
+    """C5: 8,192-point scan vs a 65,540-point map (10 accumulated scans), 20 iterations,
+    one GPU.  The NN pass is priced against HBM with §8(d)'s formula on the work the device counts:
+    per launch N x (16 B query in + 8 B key out) + 16 B per examined target (sum_q K_q) + 24 B per
+    box test (lo/hi xyz) — every examination priced as a fresh read, never the re-reads beyond that
+    (DESIGN.md §6e)."""
+    import icp4r
+    from icp4r import synth
+
+    mp = synth.make_map_pair(0)
+    src, tgt = mp.src_xyzi(), mp.tgt_xyzi()
+    n, m = len(src), len(tgt)
+    p = icp4r.default_params(max_iterations=iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    r, _ = ctx.align(src, tgt, p)  # warm-up + result
+    ctx.reset_timers()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.align(src, tgt, p)
+    wall_ms = (time.perf_counter() - t0) / reps * 1e3
+    batch_ms, _ = ctx.batch_time_ms()
+    nn_ms, nn_launches = ctx.kernel_time_ms()
+    st = ctx.nn_stats()
+    evals = st["evaluations"] / max(nn_launches, 1)
+    tests = st["box_tests"] / max(nn_launches, 1)
+    # algorithmic bytes per NN launch: queries in (16 B) + key out (8 B) + every examined target read
+    # once per examination (16 B, sum_q K_q) + the boxes tested (24 B: lo/hi xyz)
+    bytes_per_launch = n * (16 + 8) + 16 * evals + 24 * tests
+    achieved = bytes_per_launch / (nn_ms * 1e-3) / 1e9 if nn_ms > 0 else 0.0
+    return {"workload": f"C5: {n}-pt scan vs {m}-pt map (10 scans), {iters} iterations fixed + fitness, 1 GPU",
+            "registration_device_ms": batch_ms, "registration_wall_ms_incl_pcie": wall_ms,
+            "pairs_per_s": 1e3 / batch_ms if batch_ms > 0 else None,
+            "status": int(r.status), "iterations": int(r.iterations),
+            "roofline": {"bound": "hbm", "kernel": "nn (scan-to-map pass)", "avg_launch_ms": nn_ms,
+                         "launches_per_registration": nn_launches / reps, "examined_targets_per_launch": evals,
+                         "box_tests_per_launch": tests, "bytes_per_launch": bytes_per_launch,
+                         "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS},
+            "_src": src, "_tgt": tgt, "_T": r.matrix(), "_params": dict(max_iterations=iters)}
+
+
+# ------------------------------------------------------------------------------------------ GPU run
+def run_gpu(args) -> int:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = _env_rank()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -115,35 +288,111 @@ def main():
     ctx = icp4r.Context(dev.index)
     # fixed work: 20 iterations for every pair (the |ΔMSE| and exact-identity stops disabled)
     params = icp4r.default_params(max_iterations=args.iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-    batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
-                        tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
-                        max_src_n=n, max_tgt_n=n)
+
+    def mk_batch(s, t):
+        return icp4r.Batch(src=s.data_ptr(), tgt=t.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
+                           tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
+                           max_src_n=n, max_tgt_n=n)
+
+    batch = mk_batch(src, tgt)
     stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def gather():
+        if world > 1:
+            idist.gather_results(results, world, out=gathered)
 
     def step():
         ctx.align_batch_device(batch, params, results.data_ptr(), stream)
+        gather()
+
+    def barrier_sync():
+        torch.cuda.synchronize(dev)
         if world > 1:
-            idist.gather_results(results, world, out=gathered)
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     ctx.reset_timers()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    barrier_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     batch_ms, _ = ctx.batch_time_ms()
+    # the TIMED run's results (every step writes the same rows; copied before any rerun below)
+    timed = (gathered if world > 1 else results).cpu().numpy().copy()
+
+    # the all-gather alone
+    gather_ms = None
+    if world > 1:
+        barrier_sync()
+        tg = time.perf_counter()
+        for _ in range(10):
+            gather()
+        barrier_sync()
+        gather_ms = max_over_ranks((time.perf_counter() - tg) / 10 * 1e3)
+
+    # incl-upload: the same steps with each batch uploaded from pinned host memory inside the timed
+    # region; batch k+1's upload (copy stream) overlaps batch k's registration (compute stream)
+    upload = None
+    if not args.no_upload:
+        src_pin = torch.from_numpy(src_h.reshape(-1, 4)).pin_memory()
+        tgt_pin = torch.from_numpy(tgt_h.reshape(-1, 4)).pin_memory()
+        slots = [(torch.empty_like(src), torch.empty_like(tgt)) for _ in range(2)]
+        slot_batches = [mk_batch(s, t) for s, t in slots]
+        copy_stream = torch.cuda.Stream(dev)
+        comp = torch.cuda.current_stream(dev)
+        uploaded = [torch.cuda.Event() for _ in range(2)]
+        freed = [torch.cuda.Event() for _ in range(2)]
+        for e in freed:
+            e.record(comp)
+        barrier_sync()
+        tu = time.perf_counter()
+        for k in range(args.steps):
+            sl = k % 2
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(freed[sl])
+                slots[sl][0].copy_(src_pin, non_blocking=True)
+                slots[sl][1].copy_(tgt_pin, non_blocking=True)
+                uploaded[sl].record(copy_stream)
+            comp.wait_event(uploaded[sl])
+            ctx.align_batch_device(slot_batches[sl], params, results.data_ptr(), stream)
+            gather()
+            freed[sl].record(comp)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        up_elapsed = max_over_ranks(time.perf_counter() - tu)
+        # the upload alone (H2D rate)
+        torch.cuda.synchronize(dev)
+        th = time.perf_counter()
+        for _ in range(3):
+            slots[0][0].copy_(src_pin, non_blocking=True)
+            slots[0][1].copy_(tgt_pin, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        h2d_s = (time.perf_counter() - th) / 3
+        nbytes = src_pin.numel() * 4 + tgt_pin.numel() * 4
+        same = bool((results.cpu().numpy() == timed[rank * P:(rank + 1) * P] if world > 1 else
+                     results.cpu().numpy() == timed).all())
+        upload = {"value": world * P * args.steps / up_elapsed, "unit": "pairs/s",
+                  "ms_per_step": up_elapsed / args.steps * 1e3, "h2d_bytes_per_step": nbytes,
+                  "h2d_ms_alone": h2d_s * 1e3, "h2d_gbs": nbytes / h2d_s / 1e9, "results_equal_resident": same,
+                  "note": "H2D of each batch's clouds (pinned host -> HBM) inside the timed region, double-buffered: "
+                          "batch k+1 uploads on a copy stream while batch k registers"}
+        del slots, slot_batches, src_pin, tgt_pin
+
     # Kernel-level measurements (roofline, test and update kernels): the timed steps run the batch as
     # pair groups on several streams (icp4r run_pairs, ICP4R_GROUPS), where one group's kernels
     # overlap another's and a launch time is not one kernel's; so the same steps are repeated once
@@ -162,6 +411,7 @@ def main():
             del os.environ["ICP4R_GROUPS"]
         else:
             os.environ["ICP4R_GROUPS"] = groups_env
+    single_group_equal = bool((results.cpu().numpy() == (timed[rank * P:(rank + 1) * P] if world > 1 else timed)).all())
     nn_ms, nn_launches = ctx.kernel_time_ms()  # the dominant kernel: the batched search
     test_ms, test_launches = ctx.stage_time_ms(icp4r.STAGE_NN_TEST)
     upd_ms, upd_launches = ctx.stage_time_ms(icp4r.STAGE_UPDATE)
@@ -170,29 +420,47 @@ def main():
     plan = icp4r.plan(P, n, n)
     kernel = "nn_lds_kernel" if plan["lds"] else "nn_pruned_kernel" if plan["pruned"] else "nn_kernel"
 
-    # result check (outside the timed region): statuses, iteration counts, and pairs vs the oracle
-    res = np.frombuffer(results.cpu().numpy().tobytes(), dtype=icp4r.RESULT_DTYPE)
+    # C5 (rank 0 only; one GPU)
+    c5 = None
+    if rank == 0 and not args.no_c5:
+        c5 = c5_measure(ctx, dev)
+
+    # checks on the TIMED results: statuses, iteration counts, and pairs of every rank / both pair
+    # groups against the oracle (rank 0 regenerates those pairs' inputs from their seeds)
+    res = np.frombuffer(timed.tobytes(), dtype=icp4r.RESULT_DTYPE)
     status_ok = bool((res["status"] == 0).all())
     iters_ok = bool((res["iterations"] == args.iters).all())
     diag = {"status_nonzero": int((res["status"] != 0).sum()), "iter_min": int(res["iterations"].min()),
-            "iter_max": int(res["iterations"].max()), "conv_states": sorted(set(int(v) for v in res["convergence_state"]))}
-    ok = status_ok and iters_ok
+            "iter_max": int(res["iterations"].max()), "conv_states": sorted(set(int(v) for v in res["convergence_state"])),
+            "single_group_rerun_equal": single_group_equal}
+    ok = status_ok and iters_ok and single_group_equal
     check = []
     if rank == 0 and args.check > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
+        from icp4r import synth
 
-        for k in range(min(args.check, P)):
-            o = oracle.align(src_h[k], tgt_h[k], numerics=oracle.NUM_F32, max_iterations=args.iters,
+        if world == 1:
+            k = min(args.check, P)
+            picks = sorted(set(np.linspace(0, P - 1, k).round().astype(int).tolist()) | {P // 2 - 1, P // 2} & set(range(P)))
+        else:
+            picks = sorted({r * P + j for r in range(world) for j in (0, P - 1)})
+        for g in picks:
+            p = synth.make_pair(g, n)
+            o = oracle.align(p.src_xyzi(), p.tgt_xyzi(), numerics=oracle.NUM_F32, max_iterations=args.iters,
                              mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-            T = res[k]["T"].reshape(4, 4).T.astype(np.float64)
-            To = o["T"].astype(np.float64)
-            M = T[:3, :3].T @ To[:3, :3]
-            dr = float(np.arctan2(np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2,
-                                  (np.trace(M) - 1) / 2))
-            check.append({"pair": k, "dt_m": float(np.abs(T[:3, 3] - To[:3, 3]).max()), "dr_rad": dr,
-                          "bit_exact": bool((res[k]["T"].reshape(4, 4).T == o["T"]).all())})
+            T = res[g]["T"].reshape(4, 4).T
+            dt, dr = _pose_err(T, o["T"])
+            check.append({"pair": int(g), "rank": int(g // P), "group": int((g % P) >= P // 2), "dt_m": dt, "dr_rad": dr,
+                          "bit_exact": bool((T == o["T"]).all() and res[g]["fitness"] == o["fitness"])})
         ok = ok and all(c["dt_m"] <= 1e-4 and c["dr_rad"] <= 1e-4 for c in check)
+        if c5 is not None:
+            o = oracle.align(c5["_src"], c5["_tgt"], numerics=oracle.NUM_F32, mse_threshold_absolute=-1.0,
+                             transformation_epsilon=-1.0, **c5["_params"])
+            c5["bit_exact_vs_oracle"] = bool((c5["_T"] == o["T"]).all())
+    if c5 is not None:
+        for k in ("_src", "_tgt", "_T", "_params"):
+            c5.pop(k)
 
     total_pairs = world * P * args.steps
     value = total_pairs / elapsed
@@ -213,12 +481,9 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    # cached-neighbour test kernel (HBM-bound): algorithmic bytes = per tested query X (16) + nn_t
-    # (16) + L (4) + sinv (4) read; per hit its key (8) written, + its correspondence record (32)
-    # in the iteration passes
-    # The iteration passes' tests run in the tail of fold_update_kernel (ICP4R_FUSE_TEST, default):
-    # their counts are tested_in_update / hits_in_update; the rest is the standalone kernel's (the
-    # fitness pass, or every pass with the fusion off).
+    # cached-neighbour test kernel (HBM-bound): per tested query X (16) + nn_t (16) + L (4) + sinv (4)
+    # read; per hit its key (8) written.  The iteration passes' tests run in the tail of
+    # fold_update_kernel (ICP4R_FUSE_TEST, default); the rest (the fitness pass) is this kernel's.
     cache_test = None
     t_own = st["cache_tested"] - st["tested_in_update"]
     h_own = st["cache_hits"] - st["hits_in_update"]
@@ -230,22 +495,24 @@ def main():
                       "frac": tb / (test_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                       "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1),
                       "tests_fused_into_update": st["tested_in_update"]}
-    # fold_update_kernel (HBM): two passes over X + nn_t (32 B per point each), and, fused, the next
-    # pass's test: X, nn_t, L/U, sinv read (44 B), X and L/U written (24 B), a key per hit (8 B)
+    # fold_update_kernel (HBM), one-read algorithmic bytes (never count re-reads): X and
+    # nn_t read once per point (32 B) for the two fold passes; fused, the next pass's test adds L/U and
+    # sinv (12 B) read, X and L/U written (24 B), a key per hit (8 B).  The kernel actually reads X and
+    # nn_t twice more (pass B, the test tail): `bytes_with_rereads` prices those too.
     update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches}
     if upd_launches and upd_ms > 0:
-        ub = (P * n * 64 * upd_launches + st["tested_in_update"] * 68 + st["hits_in_update"] * 8) / upd_launches
+        ub = (P * n * 32 * upd_launches + st["tested_in_update"] * 36 + st["hits_in_update"] * 8) / upd_launches
+        ub_re = (P * n * 64 * upd_launches + st["tested_in_update"] * 68 + st["hits_in_update"] * 8) / upd_launches
         update.update({"bound": "hbm", "bytes_per_launch": ub, "achieved": ub / (upd_ms * 1e-3) / 1e9,
-                       "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS})
+                       "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                       "bytes_with_rereads": ub_re, "frac_with_rereads": ub_re / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS})
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(src_h, tgt_h, args.iters, args.cpu_seconds)
-        with open(os.path.join(ROOT, "BASELINE.json")) as f:
-            metric = json.load(f)["metric"]
+            cpu = cpu_baseline(src_h, tgt_h, args.iters, args.cpu_seconds, args.cpu_all_seconds)
         line = {
-            "metric": metric,
+            "metric": _metric(),
             "value": value,
             "unit": "pairs/s",
             "n_gpus": world,
@@ -259,7 +526,7 @@ def main():
             "data": "synthetic (seeded 4D-radar scan pairs, SURVEY.md App. B)",
             "config": {
                 "workload": f"C3/C4: {P} independent pairs per GPU, {n}/{n}-pt scans, {args.iters} ICP iterations "
-                            f"(fixed) + fitness pass, exact NN ({'Morton-block pruned' if plan['pruned'] else 'brute force'}), "
+                            f"(fixed) + fitness pass, exact NN ({'kd-block pruned' if plan['pruned'] else 'brute force'}), "
                             f"PCL numerics (bit-exact float restatement)",
                 "nn_plan": plan,
                 "pairs_per_gpu": P, "points": n, "iterations": args.iters,
@@ -286,11 +553,13 @@ def main():
                         "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add); "
                         "compare/select/ballot/LDS not counted. achieved = that / avg launch time (HIP events on "
                         "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). brute_force_equivalent_"
-                        "tflops = n*m*8 per NN pass / search time. The search is latency-bound (4 waves/SIMD, "
-                        "LDS-limited), see DESIGN.md",
+                        "tflops = n*m*8 per NN pass / search time. See DESIGN.md §5",
             },
+            "incl_upload": upload,
+            "gather": {"ms": gather_ms, "bytes": world * P * 96} if world > 1 else None,
             "cache_test_kernel": cache_test,
             "update_kernel": update,
+            "c5": c5,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
             "batch_device_ms": batch_ms,
@@ -302,7 +571,18 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        return launch(args, argv)  # nothing above has touched the GPU
+    if args.dry_run:
+        return run_dry(args)
+    return run_gpu(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

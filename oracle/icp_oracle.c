@@ -235,7 +235,7 @@ static void kd_free(kd_tree* t) {
     memset(t, 0, sizeof(*t));
 }
 
-static int64_t g_leaf_visits;
+static _Thread_local int64_t g_leaf_visits; /* per thread: the CPU baseline runs pairs on a thread pool */
 int64_t oracle_kdtree_leaf_visits(void) { return g_leaf_visits; }
 
 typedef struct { float best; int32_t idx; } kd_result;

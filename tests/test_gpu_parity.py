@@ -535,3 +535,53 @@ def test_kd_index_degenerate_clouds(gpu_ctx, shape, m):
     bi, bd = _brute_nn(src, tgt)
     assert (gd.view(np.uint32) == bd.view(np.uint32)).all()
     assert (gi == bi).all()
+
+
+def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, monkeypatch):
+    """BASELINE.json configs[2] at its own size, exactly as bench.py runs it: 1024 pairs of 8192/8192
+    points (pair i seeded 1000 + i), 20 fixed iterations + the fitness pass, device-resident, the
+    default plan (two pair groups on two streams, cached-neighbour test fused into the update).
+    All 1024 result rows must be bit-identical to the same batch on one group without the
+    cached-neighbour test, and 16 pairs spread over both groups bit-equal to the oracle."""
+    import torch
+
+    import icp4r
+
+    P, n, iters = 1024, 8192, 20
+    src_h = np.empty((P, n, 4), np.float32)
+    tgt_h = np.empty((P, n, 4), np.float32)
+    for k in range(P):
+        src_h[k], tgt_h[k] = _pair(1000 + k, n)
+    dev = torch.device("cuda", 0)
+    src = torch.from_numpy(src_h.reshape(-1, 4)).to(dev)
+    tgt = torch.from_numpy(tgt_h.reshape(-1, 4)).to(dev)
+    off = torch.arange(P, dtype=torch.int64, device=dev) * n
+    cnt = torch.full((P,), n, dtype=torch.int32, device=dev)
+    batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
+                        tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
+                        max_src_n=n, max_tgt_n=n)
+    params = icp4r.default_params(max_iterations=iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    plan = icp4r.plan(P, n, n)
+    assert plan["lds"] and plan["cache"]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        out = torch.zeros((P, 96), dtype=torch.uint8, device=dev)
+        gpu_ctx.align_batch_device(batch, params, out.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        return np.frombuffer(out.cpu().numpy().tobytes(), dtype=icp4r.RESULT_DTYPE)
+
+    for k in ("ICP4R_GROUPS", "ICP4R_NN_CACHE", "ICP4R_FUSE_TEST", "ICP4R_NN_LDS"):
+        monkeypatch.delenv(k, raising=False)
+    default = run()
+    assert (default["status"] == 0).all() and (default["iterations"] == iters).all()
+    monkeypatch.setenv("ICP4R_GROUPS", "1")
+    monkeypatch.setenv("ICP4R_NN_CACHE", "0")
+    plain = run()
+    assert default.tobytes() == plain.tobytes()
+    picks = [0, 1, 100, 255, 384, 510, 511, 512, 513, 640, 777, 900, 1000, 1021, 1022, 1023]
+    for k in picks:
+        o = oracle_mod.align(src_h[k], tgt_h[k], numerics=oracle_mod.NUM_F32, max_iterations=iters,
+                             mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+        assert (default[k]["T"].reshape(4, 4).T == o["T"]).all(), k
+        assert default[k]["fitness"] == o["fitness"], k

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 # kernel-level profiles of the single-stream configuration (bench.py prices its kernels on the same)
 export ICP4R_GROUPS=1
 mkdir -p gpurun_out
-ARGS="--steps 5 --warmup 1 --no-cpu --check 0"
+ARGS="--steps 5 --warmup 1 --no-cpu --check 0 --no-upload --no-c5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats -o run --output-format csv -- \
     python3 bench.py $ARGS > gpurun_out/prof_stats.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/prof_fetch -o run --output-format csv -- \
