@@ -38,16 +38,16 @@ class FastGICPSingleThread {
   public:
     using PointCloudSource = pcl::PointCloud<PointSource>;
     using PointCloudTarget = pcl::PointCloud<PointTarget>;
+    using PointCloudSourceConstPtr = typename PointCloudSource::ConstPtr;  // boost::shared_ptr in PCL 1.8
+    using PointCloudTargetConstPtr = typename PointCloudTarget::ConstPtr;
     using Matrix4 = Eigen::Matrix<float, 4, 4>;
 
     FastGICPSingleThread() { icp4r_gicp_params_default(&params_); }
 
     void clearSource() { src_.reset(); }
     void clearTarget() { tgt_.reset(); }
-    template <typename CloudPtr>
-    void setInputSource(const CloudPtr& cloud) { src_ = cloud; }
-    template <typename CloudPtr>
-    void setInputTarget(const CloudPtr& cloud) { tgt_ = cloud; }
+    void setInputSource(const PointCloudSourceConstPtr& cloud) { src_ = cloud; }
+    void setInputTarget(const PointCloudTargetConstPtr& cloud) { tgt_ = cloud; }
 
     void setCorrespondenceRandomness(int k) { params_.k_correspondences = k; }
     void setRegularizationMethod(RegularizationMethod m) { params_.regularization = (int32_t)m; }
@@ -112,8 +112,8 @@ class FastGICPSingleThread {
         }
     }
 
-    std::shared_ptr<const PointCloudSource> src_;
-    std::shared_ptr<const PointCloudTarget> tgt_;
+    PointCloudSourceConstPtr src_;
+    PointCloudTargetConstPtr tgt_;
     icp4r_gicp_params params_;
     icp4r_result result_{};
     Matrix4 final_ = Matrix4::Identity();

@@ -9,6 +9,8 @@
 //
 // With real PCL and Eigen on the include path their PointCloud / Matrix4f types are used; this image
 // has neither, so minimal stand-ins with the same member names are provided (ICP4R_STANDALONE).
+// The ICP4R_HAVE_PCL branch stores PCL's own PointCloud<T>::ConstPtr (boost::shared_ptr in PCL 1.8);
+// tests/test_facades_pcl18.py compiles it against a PCL-1.8-shaped include tree (tests/cpp/pcl18).
 // Define ICP4R_NO_PCL_ALIAS to get icp4r::IterativeClosestPoint without the pcl:: alias.
 #pragma once
 
@@ -130,16 +132,19 @@ class IterativeClosestPoint {
   public:
     using PointCloudSource = pcl::PointCloud<PointSource>;
     using PointCloudTarget = pcl::PointCloud<PointTarget>;
-    using PointCloudSourceConstPtr = std::shared_ptr<const PointCloudSource>;
-    using PointCloudTargetConstPtr = std::shared_ptr<const PointCloudTarget>;
+    // PCL's own pointer types: boost::shared_ptr in PCL 1.8 (the node's ROS melodic), std::shared_ptr
+    // from PCL 1.11 and in the stand-ins above — the caller's Ptr converts to ConstPtr either way
+    using PointCloudSourceConstPtr = typename PointCloudSource::ConstPtr;
+    using PointCloudTargetConstPtr = typename PointCloudTarget::ConstPtr;
     using Matrix4 = Eigen::Matrix<Scalar, 4, 4>;
 
     IterativeClosestPoint() { icp4r_params_default(&params_); }
 
-    template <typename CloudPtr>
-    void setInputSource(const CloudPtr& cloud) { src_ = cloud; }
-    template <typename CloudPtr>
-    void setInputTarget(const CloudPtr& cloud) { tgt_ = cloud; }
+    // Registration::setInputSource / setInputTarget (const PointCloud::ConstPtr&), no copy
+    void setInputSource(const PointCloudSourceConstPtr& cloud) { src_ = cloud; }
+    void setInputTarget(const PointCloudTargetConstPtr& cloud) { tgt_ = cloud; }
+    PointCloudSourceConstPtr const getInputSource() { return src_; }
+    PointCloudTargetConstPtr const getInputTarget() { return tgt_; }
 
     void setMaximumIterations(int nr_iterations) { params_.max_iterations = nr_iterations; }
     int getMaximumIterations() const { return params_.max_iterations; }
@@ -207,8 +212,8 @@ class IterativeClosestPoint {
         }
     }
 
-    std::shared_ptr<const PointCloudSource> src_;
-    std::shared_ptr<const PointCloudTarget> tgt_;
+    PointCloudSourceConstPtr src_;
+    PointCloudTargetConstPtr tgt_;
     icp4r_params params_;
     icp4r_result result_{};
     Matrix4 final_ = Matrix4::Identity();

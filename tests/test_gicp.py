@@ -258,7 +258,8 @@ def test_gpu_fast_gicp_facade(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_fast_gicp_cpp_callsite(gpu_ctx, oracle_mod, tmp_path):
+@pytest.mark.parametrize("exe_name", ["gicp_callsite", "pcl18_gicp_callsite"])
+def test_gpu_fast_gicp_cpp_callsite(gpu_ctx, oracle_mod, tmp_path, exe_name):
     """tests/cpp/gicp_callsite.cpp: radar_odometry's GICP block (radar_odometry.cpp:398-411) through
     include/icp4r/fast_gicp_compat.hpp — the same bits as the Python facade on the same inputs, and the
     oracle's pose within the GICP bar."""
@@ -272,7 +273,7 @@ def test_gpu_fast_gicp_cpp_callsite(gpu_ctx, oracle_mod, tmp_path):
     synth.write_bin(a, rec(src))
     synth.write_bin(b, rec(tgt))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = os.path.join(root, "tests", "cpp", "_build", "gicp_callsite")
+    exe = os.path.join(root, "tests", "cpp", "_build", exe_name)  # stand-in types / PCL-1.8-shaped tree
     r = subprocess.run([exe, str(a), str(b)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     head, tl = r.stdout.strip().split("\n")[:2]

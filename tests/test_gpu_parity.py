@@ -459,12 +459,14 @@ def test_fitness_entry_point(gpu_ctx, oracle_mod):
 
 
 # ---------------------------------------------------------------------------------------------- facade
-def test_pcl_facade_callsite(oracle_mod, golden):
-    """The node's call sequence compiled against pcl_compat.hpp, on the golden C1 scans."""
+@pytest.mark.parametrize("exe_name", ["callsite", "pcl18_callsite"])
+def test_pcl_facade_callsite(oracle_mod, golden, exe_name):
+    """The node's call sequence compiled against pcl_compat.hpp, on the golden C1 scans — with the
+    facade's stand-in types, and against the PCL-1.8-shaped include tree (boost::shared_ptr clouds)."""
     r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     case = golden["cases"][0]
-    exe = os.path.join(ROOT, "tests", "cpp", "_build", "callsite")
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", exe_name)
     out = subprocess.run([exe, os.path.join(GOLDEN_DIR, case["src_bin"]), os.path.join(GOLDEN_DIR, case["tgt_bin"])],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr

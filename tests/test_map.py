@@ -197,7 +197,8 @@ def test_scan_to_map_registration_device_resident(gpu_ctx, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_ikd_facade_callsite(oracle_mod):
+@pytest.mark.parametrize("exe_name", ["map_callsite", "pcl18_map_callsite"])
+def test_ikd_facade_callsite(oracle_mod, exe_name):
     """tests/cpp/map_callsite.cpp: radar_odometry's map calls through include/icp4r/ikd_compat.hpp
     (namespace-scope KD_TREE, Build, set_downsample_param, Add_Points(.., false), Sector_Search) give
     the oracle's submap, intensities included."""
@@ -209,7 +210,7 @@ def test_ikd_facade_callsite(oracle_mod):
     from icp4r import synth
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = os.path.join(root, "tests", "cpp", "_build", "map_callsite")
+    exe = os.path.join(root, "tests", "cpp", "_build", exe_name)  # stand-in types / PCL-1.8-shaped tree
     a, b = (os.path.join(GOLDEN_DIR, f) for f in ("c2_pair1_8k_tgt.bin", "c2_pair1_8k_src.bin"))
     x, y, yaw = 5.0, -3.0, 30.0
     r = subprocess.run([exe, a, b, str(x), str(y), str(yaw)], capture_output=True, text=True, timeout=120)
