@@ -18,6 +18,24 @@
 // previous scan (:465-493) feeds nothing that is written and is skipped.
 //
 //   icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N]
+//                    [--use-icp-result CSV]
+//
+// Empty scans (:505 vs :698-699): the node pushes every frame's points onto cloud_src_in /
+// cloud_tar_in and clears them only inside `if (cloud_tar_in->size() && cloud_src_in->size())`.
+// When either cloud is empty the frame is not registered AND the other cloud keeps its points, so
+// the next frame's points are appended to them: after an empty scan k the next registration is
+// scan k+1 against scan k-1 (the tar cloud carried over), and an empty first scan makes frame 2
+// register scan 1 + scan 2 against scan 1.  Reproduced here (both modes), as is the node's
+// output_time, which advances on registered frames only.
+//
+// --use-icp-result CSV: the node built with USE_ICP_RESULT (:192-206, :523-540) — no ICP; each
+// registered frame takes its transform from the next row of a previous run's output_result.csv.
+// The header line is consumed as `firstline` (19 getline(',') + getline('\n'), atof each field);
+// a row past the end of the file reads as zeros (getline fails, `value` is empty, atof("") = 0).
+// The node fills icp_result(i, j) = data(4*i + j + 1, 1) on a 20x1 vector: column 1 does not exist
+// (Eigen's assertion aborts the node's -g build; without assertions it reads past the vector).
+// Column 0 — csv field 4*i + j + 1, i.e. Rtrans(i, j) as the non-USE_ICP_RESULT run wrote it — is
+// the only defined reading and the one used.  No CSV is written in this mode (:700-707).
 //
 // --batch: every frame's ICP is independent of the poses (identity guess), so all frames are
 // registered in ONE device batch (icp4r_align_batch_host) and composed afterwards — identical output
@@ -105,7 +123,8 @@ struct FrameOut {
 };
 
 int usage() {
-    std::fprintf(stderr, "usage: icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N]\n");
+    std::fprintf(stderr, "usage: icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N] "
+                         "[--use-icp-result CSV]\n");
     return 2;
 }
 
@@ -120,13 +139,16 @@ int main(int argc, char** argv) {
     icp4r_ego_params ep;
     icp4r_ego_params_default(&ep);
     int max_iterations = -1;  // PCL default (10) unless given
+    std::string icp_result_csv;
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--csv") && i + 1 < argc) csv = argv[++i];
         else if (!std::strcmp(argv[i], "--batch")) batch = true;
         else if (!std::strcmp(argv[i], "--seed") && i + 1 < argc) ep.seed = std::strtoull(argv[++i], nullptr, 0);
         else if (!std::strcmp(argv[i], "--max-iterations") && i + 1 < argc) max_iterations = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--use-icp-result") && i + 1 < argc) icp_result_csv = argv[++i];
         else return usage();
     }
+    const bool use_icp_result = !icp_result_csv.empty();
     const std::string out_dir = dataset_folder + "radar";
     if (!exists(out_dir) && mkdir(out_dir.c_str(), 0755) != 0) {  // the node shells out to `sudo mkdir` (:151-156)
         std::perror("mkdir");
@@ -145,11 +167,12 @@ int main(int argc, char** argv) {
     std::ofstream pcl_info(out_dir + "/pcl_info.txt", std::ios::trunc);
     pcl_info.setf(std::ios::dec, std::ios::floatfield);
     using Cloud = pcl::PointCloud<pcl::PointXYZI>;
-    auto to_cloud = [](const std::vector<float>& rec) {
-        auto c = std::make_shared<Cloud>();
-        const size_t n = rec.size() / 5;  // (int)(size() / 5.0) records
+    auto to_cloud = [](const std::vector<float>& xyzi) {
+        Cloud::Ptr c(new Cloud);
+        const size_t n = xyzi.size() / 4;
         c->points.reserve(n);
-        for (size_t i = 0; i < n; ++i) c->push_back(pcl::PointXYZI(rec[5 * i], rec[5 * i + 1], rec[5 * i + 2], rec[5 * i + 3]));
+        for (size_t i = 0; i < n; ++i)
+            c->push_back(pcl::PointXYZI(xyzi[4 * i], xyzi[4 * i + 1], xyzi[4 * i + 2], xyzi[4 * i + 3]));
         return c;
     };
     icp4r_params ip;
@@ -164,6 +187,10 @@ int main(int argc, char** argv) {
         pk.seed = ep.seed + ((uint64_t)k << 32);
         icp4r_ego_result er;
         const int n = (int)(curr.size() / 5);
+        if (n == 0) {  // A_src = b_src = 0; Vxyz = (KᵀK)⁻¹ Kᵀ Vr over 0 rows: Eigen's empty products give 0
+            out[k].A = out[k].b = 0.0;
+            continue;
+        }
         int rc = icp4r_ego_velocity(ctx, curr.data(), n, &pk, &er, nullptr, nullptr);
         if (rc != ICP4R_OK && rc != ICP4R_E_EMPTY) {
             std::fprintf(stderr, "icp4r_ego_velocity: %s\n", icp4r_last_error());
@@ -174,46 +201,89 @@ int main(int argc, char** argv) {
         for (int c = 0; c < 3; ++c) out[k].V[c] = er.v[c];
     }
 
-    if (batch) {
-        // every registration in one device batch: pair k = (scan k, scan max(k-1, 0))
+    // ---- which frames register, and on which clouds (:505, :698-699): the points of every frame are
+    // appended to the running clouds, which are cleared only after a registration.  Registered pair
+    // q = (src records, tgt records) in frame order; the list depends on the scan sizes only.
+    struct PairIn {
+        size_t frame;
+        std::vector<float> src, tgt;  // float4 x, y, z, intensity
+    };
+    std::vector<PairIn> pairs;
+    {
+        std::vector<float> acc_src, acc_tgt;
+        auto push = [](std::vector<float>& acc, const std::vector<float>& rec) {
+            const size_t n = rec.size() / 5;
+            for (size_t i = 0; i < n; ++i) acc.insert(acc.end(), &rec[5 * i], &rec[5 * i] + 4);
+        };
+        for (size_t k = 0; k < nframes; ++k) {
+            push(acc_src, scans[k]);
+            push(acc_tgt, scans[k ? k - 1 : 0]);
+            if (acc_src.empty() || acc_tgt.empty()) continue;  // not registered, not cleared
+            pairs.push_back({k, std::move(acc_src), std::move(acc_tgt)});
+            acc_src.clear();
+            acc_tgt.clear();
+        }
+    }
+
+    if (use_icp_result) {
+        // USE_ICP_RESULT (:192-206, :523-540): transforms from a previous run's CSV, no ICP
+        std::ifstream file(icp_result_csv.c_str());
+        if (!file) {
+            std::fprintf(stderr, "cannot open %s\n", icp_result_csv.c_str());
+            return 1;
+        }
+        std::string value;
+        double data[20];
+        auto read_row = [&]() {
+            for (int i = 0; i < 19; i++) {
+                std::getline(file, value, ',');
+                data[i] = std::atof(value.c_str());
+            }
+            std::getline(file, value, '\n');
+            data[19] = std::atof(value.c_str());
+        };
+        read_row();  // firstline: the header
+        for (const PairIn& q : pairs) {
+            read_row();
+            FrameOut& f = out[q.frame];
+            f.registered = true;
+            for (int i = 0; i < 4; i++)
+                for (int j = 0; j < 4; j++) f.T[4 * i + j] = data[4 * i + j + 1];  // data(4*i+j+1, 1): see header
+            f.score = 0.0;
+        }
+    } else if (batch) {
+        // every registration in one device batch
         std::vector<float> src, tgt;
         std::vector<int64_t> so, to;
         std::vector<int32_t> sn, tn;
-        std::vector<size_t> frame_of;
-        for (size_t k = 0; k < nframes; ++k) {
-            const std::vector<float>& c = scans[k];
-            const std::vector<float>& l = scans[k ? k - 1 : 0];
-            const int32_t n = (int32_t)(c.size() / 5), m = (int32_t)(l.size() / 5);
-            if (!n || !m) continue;  // `if (cloud_tar_in->size() && cloud_src_in->size())` (:505)
+        for (const PairIn& q : pairs) {
             so.push_back((int64_t)src.size() / 4);
             to.push_back((int64_t)tgt.size() / 4);
-            sn.push_back(n);
-            tn.push_back(m);
-            for (int32_t i = 0; i < n; ++i) src.insert(src.end(), &c[5 * (size_t)i], &c[5 * (size_t)i] + 4);
-            for (int32_t i = 0; i < m; ++i) tgt.insert(tgt.end(), &l[5 * (size_t)i], &l[5 * (size_t)i] + 4);
-            frame_of.push_back(k);
+            sn.push_back((int32_t)(q.src.size() / 4));
+            tn.push_back((int32_t)(q.tgt.size() / 4));
+            src.insert(src.end(), q.src.begin(), q.src.end());
+            tgt.insert(tgt.end(), q.tgt.begin(), q.tgt.end());
         }
-        std::vector<icp4r_result> res(frame_of.size());
-        if (!frame_of.empty()) {
+        std::vector<icp4r_result> res(pairs.size());
+        if (!pairs.empty()) {
             int rc = icp4r_align_batch_host(ctx, src.data(), so.data(), sn.data(), tgt.data(), to.data(), tn.data(),
-                                            (int32_t)frame_of.size(), nullptr, &ip, res.data());
+                                            (int32_t)pairs.size(), nullptr, &ip, res.data());
             if (rc != ICP4R_OK) {
                 std::fprintf(stderr, "icp4r_align_batch_host: %s\n", icp4r_last_error());
                 return 1;
             }
         }
-        for (size_t q = 0; q < frame_of.size(); ++q) {
-            FrameOut& f = out[frame_of[q]];
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            FrameOut& f = out[pairs[q].frame];
             f.registered = true;
             for (int r = 0; r < 4; ++r)
                 for (int c = 0; c < 4; ++c) f.T[4 * r + c] = (double)res[q].T[4 * c + r];  // column-major float
             f.score = res[q].fitness;
         }
     } else {
-        for (size_t k = 0; k < nframes; ++k) {
-            auto cloud_src_in = to_cloud(scans[k]);
-            auto cloud_tar_in = to_cloud(scans[k ? k - 1 : 0]);
-            if (!(cloud_tar_in->size() && cloud_src_in->size())) continue;  // :505
+        for (const PairIn& q : pairs) {
+            auto cloud_src_in = to_cloud(q.src);
+            auto cloud_tar_in = to_cloud(q.tgt);
             Cloud Final;
             pcl::IterativeClosestPoint<pcl::PointXYZI, pcl::PointXYZI> icp;  // :510-521
             icp.setInputSource(cloud_src_in);
@@ -222,7 +292,7 @@ int main(int argc, char** argv) {
             icp.align(Final);
             const double score = icp.getFitnessScore();
             const Eigen::Matrix4d icp_result = icp.getFinalTransformation().cast<double>();
-            FrameOut& f = out[k];
+            FrameOut& f = out[q.frame];
             f.registered = true;
             for (int r = 0; r < 4; ++r)
                 for (int c = 0; c < 4; ++c) f.T[4 * r + c] = icp_result(r, c);
@@ -231,12 +301,12 @@ int main(int argc, char** argv) {
     }
 
     // ---- pose composition and the per-frame CSV (:541-558, :701-708)
-    FILE* fp = std::fopen(csv.c_str(), "w+");
-    if (!fp) {
+    FILE* fp = use_icp_result ? nullptr : std::fopen(csv.c_str(), "w+");  // #ifndef USE_ICP_RESULT (:187-191)
+    if (!use_icp_result && !fp) {
         std::perror("output_result.csv");
         return 1;
     }
-    std::fprintf(fp, "#time(s),Rtrans00,Rtrans01,Rtrans02,Rtrans03,Rtrans10,Rtrans11,Rtrans12,Rtrans13,Rtrans20,"
+    if (fp) std::fprintf(fp, "#time(s),Rtrans00,Rtrans01,Rtrans02,Rtrans03,Rtrans10,Rtrans11,Rtrans12,Rtrans13,Rtrans20,"
                      "Rtrans21,Rtrans22,Rtrans23,Rtrans00,Rtrans00,Rtrans00,Rtrans00,score,A,b\n");
     M4 currOdom = {{1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}};
     M3 Rtrans = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
@@ -261,12 +331,12 @@ int main(int argc, char** argv) {
             t[r] = t[r] + s;
         }
         Rtrans = mul3(Rtrans, dR);
-        std::fprintf(fp, "%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f\n", output_time, T.a[0], T.a[1],
+        if (fp) std::fprintf(fp, "%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f\n", output_time, T.a[0], T.a[1],
                      T.a[2], T.a[3], T.a[4], T.a[5], T.a[6], T.a[7], T.a[8], T.a[9], T.a[10], T.a[11], T.a[12],
                      T.a[13], T.a[14], T.a[15], f.score, f.A, f.b);
         output_time += 1.0;
     }
-    std::fclose(fp);
+    if (fp) std::fclose(fp);
 
     // ---- the files written after the loop (:757-816)
     std::ofstream velocity_odom(out_dir + "/velocity.txt", std::ios::trunc);
