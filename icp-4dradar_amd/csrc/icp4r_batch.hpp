@@ -19,6 +19,8 @@ struct Plan {
     bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
     bool cache;   // lds: cached-neighbour test + second-nearest search (ICP4R_NN_CACHE=0 disables)
     int leaf;     // pruned: targets per block
+    int chunk_sb; // pruned (streamed): superblocks per target chunk (<= 64)
+    int chunks;   // pruned (streamed): target chunks searched by separate waves (merged by atomicMin)
     int64_t blocks;
 };
 

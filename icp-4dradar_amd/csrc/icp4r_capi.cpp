@@ -104,6 +104,8 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
     pl.cache = false;
     pl.splits = 1;
     pl.leaf = 0;
+    pl.chunk_sb = 64;
+    pl.chunks = 1;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
     pl.q = (qcap == 1 || qcap == 2 || qcap == 4 || qcap == 8 || qcap == 16) ? qcap
                                                                              : (pl.pruned ? kDefaultPrunedQ : kDefaultQ);
@@ -114,6 +116,18 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
         pl.leaf = (leaf == 16 || leaf == 32) ? leaf : kDefaultLeaf;
         while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) * (kNNWG / 64) < 8192) pl.q /= 2;
         pl.blocks = (int64_t)npairs * qblocks(pl.q);
+        // target chunks for the streamed kernel: at most 64 superblocks each (one lane per superblock
+        // of the candidate ballot); small grids (single pairs) cut the target further, down to 16
+        // superblocks per chunk, until the launch has about 1024 waves (ICP4R_CHUNK_SB overrides)
+        const int nsb = (((max_m + pl.leaf - 1) / pl.leaf) + kSuper - 1) / kSuper;
+        const int64_t waves = pl.blocks * (kNNWG / 64);
+        int cs = 64;
+        while (cs > 16 && waves * ((nsb + cs - 1) / cs) < 1024) cs /= 2;
+        const int cs_env = env_int("ICP4R_CHUNK_SB", 0);
+        if (cs_env == 16 || cs_env == 32 || cs_env == 64) cs = cs_env;
+        pl.chunk_sb = cs;
+        pl.chunks = nsb > 0 ? (nsb + cs - 1) / cs : 1;
+        pl.blocks *= pl.chunks;
         // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides)
         const int lds = env_int("ICP4R_NN_LDS", -1);
         const bool fits = pl.leaf == 16 && max_m <= kLdsMaxTargets;
@@ -121,6 +135,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
         if (pl.lds) {
             pl.q = 2;
             pl.blocks = npairs;
+            pl.chunks = 1;
             pl.cache = max_n <= kCacheMaxN && env_int("ICP4R_NN_CACHE", 1) != 0;
         }
         return pl;
@@ -298,7 +313,7 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
     }
     HIP_TRY(hipEventRecord(ne->start, st));
     if (pl.pruned) {
-        HIP_TRY(launch_nn_pruned(pl.q, a, w, npairs, max_n, fitness_pass, first, st));
+        HIP_TRY(launch_nn_pruned(pl.q, pl.chunk_sb, pl.chunks, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));
         HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n, fitness_pass, st));

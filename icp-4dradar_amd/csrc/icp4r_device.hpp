@@ -60,6 +60,34 @@ __device__ __forceinline__ bool seed_key(NNKey k, int m) {
     return (uint32_t)(k >> 32) == 0x7f800000u && (uint32_t)k < (uint32_t)m;
 }
 
+// Wave-wide float min / max through DPP (no LDS round trip: __shfl_xor compiles to ds_bpermute /
+// ds_swizzle, one dependent LDS-unit op per step).  Steps: xor 1 and xor 2 (quad_perm), the 8- and
+// 16-lane mirrors, then row_bcast15 / row_bcast31 fold rows 0-1 and 0-3 into row 3; lane 63 holds
+// the result, broadcast with readlane.  Every lane of the wave must be active.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                                 CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ float wave_minf(float x) {
+    x = fminf(x, dpp_f<0xB1>(x));        // quad_perm [1,0,3,2]
+    x = fminf(x, dpp_f<0x4E>(x));        // quad_perm [2,3,0,1]
+    x = fminf(x, dpp_f<0x141>(x));       // row_half_mirror
+    x = fminf(x, dpp_f<0x140>(x));       // row_mirror
+    x = fminf(x, dpp_f<0x142, 0xa>(x));  // row_bcast15 -> rows 1, 3
+    x = fminf(x, dpp_f<0x143, 0xc>(x));  // row_bcast31 -> rows 2, 3
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+__device__ __forceinline__ float wave_maxf(float x) {
+    x = fmaxf(x, dpp_f<0xB1>(x));
+    x = fmaxf(x, dpp_f<0x4E>(x));
+    x = fmaxf(x, dpp_f<0x141>(x));
+    x = fmaxf(x, dpp_f<0x140>(x));
+    x = fmaxf(x, dpp_f<0x142, 0xa>(x));
+    x = fmaxf(x, dpp_f<0x143, 0xc>(x));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+
 // Box pruning is conservative in float: a box lower bound is shrunk by 2^-16 before its `<=` test
 // against a d², which covers the few-ulp rounding of both the bound and l2_simple.
 constexpr float kLbShrink = 1.0f - 1.0f / 65536.0f;

@@ -966,6 +966,11 @@ __global__ __launch_bounds__(kIdxWG) void index_refine_kernel(PairArgs a, WorkAr
 // increment, so the old match is nearly as close); iteration 0: the target at the same relative
 // Morton position.
 
+// lane l's value of v, wave-uniform (v_readlane; l uniform)
+__device__ __forceinline__ float rdlane(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
 template <int Q>
 __device__ __forceinline__ bool box_needed(const v4f lo, const v4f hi, const float (&x)[Q], const float (&y)[Q],
                                            const float (&z)[Q], const NNKey (&best)[Q]) {
@@ -1011,13 +1016,47 @@ __device__ __forceinline__ void sweep_block(cv4f_ptr blk, const float (&x)[Q], c
     }
 }
 
+// Seed keys for the chunked pruned search (chunks > 1): every query's key := its seed evaluated at
+// the query's current position — the previous match (iterations > 0 / fitness pass) or, in the
+// first pass, the target at the same relative sorted position (as the unchunked kernel seeds
+// inline).  The chunk searches then start from this key and merge into it with a u64 atomicMin:
+// the seed is a real candidate, so min(seed, chunk minima) is the exact (d², index) minimum.
+__global__ __launch_bounds__(256) void nn_seed_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+    const int p = blockIdx.y;
+    const int phase = uload(&w.state[p].phase);
+    if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
+    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= n) return;
+    const int o = w.sperm[(int64_t)p * w.x_stride + s];
+    const float4 v = w.X[(int64_t)p * w.x_stride + o];
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const NNKey k0 = key[o];
+    const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
+    const uint32_t j = (first && !seed_key(k0, m)) ? __float_as_uint(tsg[((int64_t)s * m) / n].w)
+                                                   : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+    const float4 t = a.tgt[uload(a.tgt_off + p) + j];
+    key[o] = make_key(l2_simple(v.x, v.y, v.z, t.x, t.y, t.z), j);
+}
+
+// Streamed pruned search (single pairs, small batches, targets beyond LDS — C1, C2, C5): one wave
+// per 64·Q queries of a pair (Morton/kd-contiguous), blocks streamed through the scalar cache.
+// grid.z = chunks: chunk c searches superblocks [c·cs, (c+1)·cs) only (cs <= 64, one lane per
+// superblock for the wave's candidate mask), so a single pair fills the GPU — C5's 8 Morton chunks of
+// 8192 map points, each a kd tree, or C2's target in quarters — and a wave whose query box cannot
+// reach a chunk leaves after one ballot.  With chunks > 1 the seed is nn_seed_kernel's key and the
+// chunk minima merge by atomicMin (correspondence records: corr_kernel afterwards).
 template <int Q, int B>
-__global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+__global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first, int cs) {
+    const int chunks = gridDim.z, c = blockIdx.z;
     const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
     const int p = g / gridDim.x, qb = g - p * gridDim.x;
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    const int nb = (m + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
+    const int sb_lo = c * cs, sb_n = min(cs, nsb - sb_lo);
+    if (sb_n <= 0) return;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int base = (qb * (kNNWG / 64) + wave) * (64 * Q);
     if (base >= n) return;
@@ -1027,7 +1066,7 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
     const float4* tgt = a.tgt + uload(a.tgt_off + p);
     const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
     float x[Q], y[Q], z[Q];
-    NNKey best[Q];
+    NNKey best[Q], seed[Q];
     int orig[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -1039,11 +1078,16 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
         x[q] = v.x;
         y[q] = v.y;
         z[q] = v.z;
-        const NNKey k0 = key[o];  // first pass: src_order_kernel's seed key (d² = +inf) or stale
-        const uint32_t j = (first && !seed_key(k0, m)) ? __float_as_uint(tsg[((int64_t)s * m) / n].w)
-                                                       : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
-        const float4 t = tgt[j];
-        best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
+        const NNKey k0 = key[o];  // chunked: nn_seed_kernel's key; else the previous key / first-pass seed
+        if (chunks > 1) {
+            best[q] = k0;
+        } else {
+            const uint32_t j = (first && !seed_key(k0, m)) ? __float_as_uint(tsg[((int64_t)s * m) / n].w)
+                                                           : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+            const float4 t = tgt[j];
+            best[q] = make_key(l2_simple(x[q], y[q], z[q], t.x, t.y, t.z), j);
+        }
+        seed[q] = best[q];
     }
     // the wave's query box and its largest seed distance (uniform; best only shrinks from here on)
     float qlo[3], qhi[3], qmax = 0.0f;
@@ -1058,35 +1102,43 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
         qmax = fmaxf(qmax, key_d2(best[q]));
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
-            qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
-        }
-        qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+    for (int k = 0; k < 3; ++k) {  // DPP reductions, wave-uniform results (every lane active here)
+        qlo[k] = wave_minf(qlo[k]);
+        qhi[k] = wave_maxf(qhi[k]);
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
-        qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
+    qmax = wave_maxf(qmax);
+    // the chunk's superblocks: lane l holds superblock sb_lo + l; one ballot gives the candidates
+    v4f isl, ish;
+    {
+        const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+        const int sbl = sb_lo + min(lane, sb_n - 1);
+        isl = sbv[2 * sbl];
+        ish = sbv[2 * sbl + 1];
     }
-    qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
-    const int nb = (m + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
+    const uint64_t cmask = __ballot(lane < sb_n && box_maybe(isl, ish, qlo, qhi, qmax));
+    unsigned long long tests = (unsigned long long)sb_n;  // box tests (lane-level: one query against one box)
+    int swept = 0;
+    // visiting order: outward from the seed's superblock (the first lane's seed) when it lies in the
+    // chunk, else from the chunk end nearest to it
     const int seed_pos = w.tinv[(int64_t)p * w.t_stride + __builtin_amdgcn_readfirstlane((uint32_t)best[0])];
-    const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (B * kSuper);
+    const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos) / (B * kSuper) - sb_lo;
+    uint64_t um = sb0 <= 0 ? cmask : sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
     const cv4f_ptr ts = as_const(tsg);
     const cv4f_ptr tb = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
-    const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
-    int up = sb0, dn = sb0 - 1, swept = 0;
-    unsigned long long tests = 0;  // box tests (lane-level: one query against one box)
-    for (int k = 0; k < nsb; ++k) {
-        const int sb = (up < nsb && (dn < 0 || !(k & 1))) ? up++ : dn--;
-        const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
-        ++tests;
-        if (!box_maybe(slo, shi, qlo, qhi, qmax)) continue;
+    for (bool upnext = true; um | dm; upnext = !upnext) {
+        int l;
+        if (um && (upnext || !dm)) {
+            l = __builtin_ctzll(um);
+            um &= um - 1;
+        } else {
+            l = 63 - __builtin_clzll(dm);
+            dm &= ~(1ull << l);
+        }
+        const v4f slo = {rdlane(isl.x, l), rdlane(isl.y, l), rdlane(isl.z, l), 0.f};
+        const v4f shi = {rdlane(ish.x, l), rdlane(ish.y, l), rdlane(ish.z, l), 0.f};
         tests += 64 * Q;
         if (!box_needed<Q>(slo, shi, x, y, z, best)) continue;
+        const int sb = sb_lo + l;
         for (int b = sb * kSuper; b < (sb + 1) * kSuper; ++b) {  // blocks past nb have empty boxes
             const v4f blo = tb[2 * b], bhi = tb[2 * b + 1];
             ++tests;
@@ -1100,6 +1152,13 @@ __global__ __launch_bounds__(kNNWG) void nn_pruned_kernel(PairArgs a, WorkArgs w
     if (lane == 0) {
         count_add(w.evals, 0, (unsigned long long)swept * B * (unsigned long long)min(n - base, 64 * Q));
         count_add(w.evals, 1, tests);
+    }
+    if (chunks > 1) {  // merge; corr_kernel writes the correspondence records after every chunk
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            if (orig[q] >= 0 && best[q] < seed[q])
+                atomicMin(reinterpret_cast<unsigned long long*>(key + orig[q]), (unsigned long long)best[q]);
+        return;
     }
     if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence arrays
 #pragma unroll
@@ -1746,10 +1805,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             __syncthreads();  // the compacted list visible to the whole workgroup
         }
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
-        const cv4f_ptr tbx = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-        const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
         const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+        // lane l holds superblock l's box for every run of the item (nsb <= 64 on this plan)
+        v4f isl, ish;
+        {
+            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+            const int sbl = min(lane, nsb - 1);
+            isl = sbv[2 * sbl];
+            ish = sbv[2 * sbl + 1];
+        }
         unsigned long long* bestl = sh.best[wave];
         uint32_t* secl = sh.u.sec[wave];
         uint16_t* ring = sh.items[wave];
@@ -1802,9 +1867,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const int bj = pj[q] / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
                 const v4f* tb = sh.tl + bj * kLdsLeaf;
                 NNKey lo = ~0ull, hi = ~0ull;  // the two smallest distinct keys seen
+                v4f cs[kLdsLeaf];
+#pragma unroll
+                for (int t = 0; t < kLdsLeaf; ++t) cs[t] = tb[t ^ sw];
+                __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) {
-                    const v4f c = tb[t ^ sw];
+                    const v4f c = cs[t];
                     const NNKey kn = make_key(l2_simple(x[q], y[q], z[q], c.x, c.y, c.z), __float_as_uint(c.w));
                     hi = kn < lo ? lo : (kn != lo && kn < hi ? kn : hi);
                     lo = kn < lo ? kn : lo;
@@ -1843,20 +1912,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 qmax = fmaxf(qmax, bnd[q]);
             }
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    qlo[k] = fminf(qlo[k], __shfl_xor(qlo[k], off, 64));
-                    qhi[k] = fmaxf(qhi[k], __shfl_xor(qhi[k], off, 64));
-                }
-                qmax = fmaxf(qmax, __shfl_xor(qmax, off, 64));
+            for (int k = 0; k < 3; ++k) {  // DPP reductions (no LDS round trips), wave-uniform results
+                qlo[k] = wave_minf(qlo[k]);
+                qhi[k] = wave_maxf(qhi[k]);
             }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                qlo[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qlo[k])));
-                qhi[k] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qhi[k])));
-            }
-            qmax = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, qmax)));
+            qmax = wave_maxf(qmax);
 
             // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
             uint32_t head = 0, tail = 0;
@@ -1884,9 +1944,15 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
                     const v4f* tb = sh.tl + b * kLdsLeaf;
                     const int sw = b & (kLdsLeaf - 1);
+                    // all 16 reads issued before the first compare (the compiler otherwise keeps two
+                    // in flight: 8 dependent LDS round trips per drain)
+                    v4f cs[kLdsLeaf];
+#pragma unroll
+                    for (int t = 0; t < kLdsLeaf; ++t) cs[t] = tb[t ^ sw];
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int t = 0; t < kLdsLeaf; ++t) {
-                        const v4f c = tb[t ^ sw];
+                        const v4f c = cs[t];
                         const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
                         const NNKey kn = make_key(d2, __float_as_uint(c.w));
                         if (CACHE && !SC) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
@@ -1936,19 +2002,17 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     if (tail - head >= 64) drain(64);
                 }
             };
-            // coarse test of every superblock at once (lane = superblock; nsb <= 64 here)
-            uint64_t cmask;
-            {
-                const int sbl = min(lane, nsb - 1);
-                const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-                cmask = __ballot(lane < nsb && box_maybe(sbv[2 * sbl], sbv[2 * sbl + 1], qlo, qhi, qmax));
-                tests += nsb;
-            }
+            // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
+            // sit in the lanes' registers for the whole item (isl / ish)
+            const uint64_t cmask = __ballot(lane < nsb && box_maybe(isl, ish, qlo, qhi, qmax));
+            tests += nsb;
             const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos0) / (kLdsLeaf * kSuper);
             // the candidate superblocks outward from the seed's, alternating up / down (only set bits
             // of cmask are visited: a scalar loop over all nsb cost ~10 SALU per superblock per run)
             uint64_t um = sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
-            for (bool upnext = true; um | dm; upnext = !upnext) {
+            bool upnext = true;
+            auto next_sb = [&]() -> int {
+                if (!(um | dm)) return -1;
                 int sb;
                 if (um && (upnext || !dm)) {
                     sb = __builtin_ctzll(um);
@@ -1957,25 +2021,54 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     sb = 63 - __builtin_clzll(dm);
                     dm &= ~(1ull << sb);
                 }
-                const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
+                upnext = !upnext;
+                return sb;
+            };
+            // A candidate's 8 block boxes are loaded by lanes 0..7 (lo, hi) one candidate AHEAD, so the
+            // loads are in flight while the current superblock is tested and its blocks queued; the
+            // per-block boxes for the queries' tests are then broadcast from those lanes (readlane)
+            // instead of a dependent scalar load per block.
+            int sb = next_sb();
+            v4f blo = {0.f, 0.f, 0.f, 0.f}, bhi = blo;
+            if (sb >= 0) {
+                const int bl = sb * kSuper + (lane & (kSuper - 1));
+                blo = tbv[2 * bl];
+                bhi = tbv[2 * bl + 1];
+            }
+            while (sb >= 0) {
+                const int nsb_ = next_sb();
+                v4f nlo = blo, nhi = bhi;
+                if (nsb_ >= 0) {
+                    const int bl = nsb_ * kSuper + (lane & (kSuper - 1));
+                    nlo = tbv[2 * bl];
+                    nhi = tbv[2 * bl + 1];
+                }
+                const float slx = rdlane(isl.x, sb), sly = rdlane(isl.y, sb), slz = rdlane(isl.z, sb);
+                const float shx = rdlane(ish.x, sb), shy = rdlane(ish.y, sb), shz = rdlane(ish.z, sb);
                 tests += 64 * Q + kSuper;
                 uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    const float gx = fmaxf(fmaxf(slo.x - x[q], x[q] - shi.x), 0.0f);
-                    const float gy = fmaxf(fmaxf(slo.y - y[q], y[q] - shi.y), 0.0f);
-                    const float gz = fmaxf(fmaxf(slo.z - z[q], z[q] - shi.z), 0.0f);
+                    const float gx = fmaxf(fmaxf(slx - x[q], x[q] - shx), 0.0f);
+                    const float gy = fmaxf(fmaxf(sly - y[q], y[q] - shy), 0.0f);
+                    const float gz = fmaxf(fmaxf(slz - z[q], z[q] - shz), 0.0f);
                     const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
                     if (__ballot(lbd * kLbShrink <= bnd[q]) != 0) qslots |= 1u << q;
                 }
-                if (qslots == 0) continue;
-                // coarse test of the superblock's blocks at once (lanes 0..7)
-                const int bl = sb * kSuper + (lane & (kSuper - 1));
-                const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(tbv[2 * bl], tbv[2 * bl + 1], qlo, qhi, qmax));
-                const cv4f_ptr sbb = tbx + 2 * sb * kSuper;  // the superblock's block boxes: immediate offsets
+                if (qslots != 0) {
+                    // coarse test of the superblock's blocks at once (lanes 0..7)
+                    const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(blo, bhi, qlo, qhi, qmax));
 #pragma unroll
-                for (int k = 0; k < kSuper; ++k)
-                    if ((bmask >> k) & 1) push(sb * kSuper + k, sbb[2 * k], sbb[2 * k + 1], qslots);
+                    for (int k = 0; k < kSuper; ++k)
+                        if ((bmask >> k) & 1) {
+                            const v4f lo = {rdlane(blo.x, k), rdlane(blo.y, k), rdlane(blo.z, k), 0.f};
+                            const v4f hi = {rdlane(bhi.x, k), rdlane(bhi.y, k), rdlane(bhi.z, k), 0.f};
+                            push(sb * kSuper + k, lo, hi, qslots);
+                        }
+                }
+                sb = nsb_;
+                blo = nlo;
+                bhi = nhi;
             }
             if (tail != head) drain(tail - head);
             // every load before the first store (on gfx9 a load waits behind earlier stores on vmcnt)
@@ -2713,11 +2806,15 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
     return hipGetLastError();
 }
 
-hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass,
-                            int first, hipStream_t st) {
+hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, const WorkArgs& w, int npairs,
+                            int max_n, int fitness_pass, int first, hipStream_t st) {
     const int per_block = kNNWG * q;
-    const dim3 grid((max_n + per_block - 1) / per_block, npairs), block(kNNWG);
-#define ICP4R_PR_CASE(QQ, BB) hipLaunchKernelGGL((nn_pruned_kernel<QQ, BB>), grid, block, 0, st, a, w, fitness_pass, first)
+    const dim3 grid((max_n + per_block - 1) / per_block, npairs, chunks), block(kNNWG);
+    if (chunk_sb < 1 || chunk_sb > 64 || chunks < 1) return hipErrorInvalidValue;
+    if (chunks > 1)
+        hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass, first);
+#define ICP4R_PR_CASE(QQ, BB) \
+    hipLaunchKernelGGL((nn_pruned_kernel<QQ, BB>), grid, block, 0, st, a, w, fitness_pass, first, chunk_sb)
     if (w.leaf == 16) {
         switch (q) {
             case 1: ICP4R_PR_CASE(1, 16); break;
@@ -2736,6 +2833,8 @@ hipError_t launch_nn_pruned(int q, const PairArgs& a, const WorkArgs& w, int npa
         return hipErrorInvalidValue;
     }
 #undef ICP4R_PR_CASE
+    if (chunks > 1 && w.corr != nullptr && !fitness_pass)  // records from the merged keys
+        hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();
 }
 
