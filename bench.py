@@ -481,14 +481,15 @@ def run_gpu(args) -> int:
         except (OSError, ValueError):
             traffic = None
 
-    # cached-neighbour test kernel (HBM-bound): per tested query X (16) + nn_t (16) + L (4) + sinv (4)
-    # read; per hit its key (8) written.  The iteration passes' tests run in the tail of
-    # fold_update_kernel (ICP4R_FUSE_TEST, default); the rest (the fitness pass) is this kernel's.
+    # cached-neighbour test kernel (HBM-bound; by default only the fitness pass's test runs here, the
+    # iteration passes' tests are fused into fold_update_kernel's tail): per tested query X (16, .w =
+    # L) + nn_t (16) read, per hit its key (8) written; in an iteration pass (ICP4R_FUSE_TEST=0) also
+    # U (4) read, X (16) + U (4) written.
     cache_test = None
     t_own = st["cache_tested"] - st["tested_in_update"]
     h_own = st["cache_hits"] - st["hits_in_update"]
     if test_launches:
-        tb = (t_own * 40 + h_own * 8 + st["records_written_by_test"] * 32) / test_launches
+        tb = (t_own * 32 + h_own * 8) / test_launches
         cache_test = {"kernel": "nn_cache_test_kernel", "bound": "hbm", "avg_launch_ms": test_ms,
                       "launches": test_launches, "bytes_per_launch": tb,
                       "achieved": tb / (test_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -496,13 +497,13 @@ def run_gpu(args) -> int:
                       "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1),
                       "tests_fused_into_update": st["tested_in_update"]}
     # fold_update_kernel (HBM), one-read algorithmic bytes (never count re-reads): X and
-    # nn_t read once per point (32 B) for the two fold passes; fused, the next pass's test adds L/U and
-    # sinv (12 B) read, X and L/U written (24 B), a key per hit (8 B).  The kernel actually reads X and
-    # nn_t twice more (pass B, the test tail): `bytes_with_rereads` prices those too.
+    # nn_t read once per point (32 B) for the two fold passes; fused, the next pass's test adds U
+    # (4 B) read and X (16) + U (4) written per tested point.  The kernel actually reads X and nn_t
+    # twice more (pass B, the test tail): `bytes_with_rereads` prices those too.
     update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches}
     if upd_launches and upd_ms > 0:
-        ub = (P * n * 32 * upd_launches + st["tested_in_update"] * 36 + st["hits_in_update"] * 8) / upd_launches
-        ub_re = (P * n * 64 * upd_launches + st["tested_in_update"] * 68 + st["hits_in_update"] * 8) / upd_launches
+        ub = (P * n * 32 * upd_launches + st["tested_in_update"] * 24) / upd_launches
+        ub_re = (P * n * 64 * upd_launches + st["tested_in_update"] * 56) / upd_launches
         update.update({"bound": "hbm", "bytes_per_launch": ub, "achieved": ub / (upd_ms * 1e-3) / 1e9,
                        "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                        "bytes_with_rereads": ub_re, "frac_with_rereads": ub_re / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS})

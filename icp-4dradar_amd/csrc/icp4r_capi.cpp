@@ -258,31 +258,21 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         }
         if (pl.cache) {
             w.need_stride = (x_stride + 31) / 32;
-            HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float2)));
+            HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float)));
             HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
             w.nn_t = static_cast<float4*>(ctx->nn_t.p);
-            HIP_TRY(ctx->nn_xs.ensure((size_t)slots * sizeof(float4)));
-            w.nn_xs = static_cast<float4*>(ctx->nn_xs.p);
-            w.second_chance = env_int("ICP4R_SECOND_CHANCE", 0) != 0 ? 1 : 0;
             HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
             HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
             HIP_TRY(ctx->miss_cnt.ensure((size_t)npairs * sizeof(int32_t)));
-            w.nn_lu = static_cast<float2*>(ctx->nn_lu.p);
+            w.nn_u = static_cast<float*>(ctx->nn_lu.p);
             w.defer_xform = 1;
             w.sinv = static_cast<int32_t*>(ctx->sinv.p);
             w.qlist = static_cast<int32_t*>(ctx->qlist.p);
             w.need = static_cast<uint32_t*>(ctx->need.p);
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
-            w.light_max = env_int("ICP4R_LIGHT_MAX", kDefaultLightMax);
             w.part_size = env_int("ICP4R_PART", kDefaultPartSize);
             if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
-            if (w.light_max > 0) {
-                HIP_TRY(ctx->ilist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
-                HIP_TRY(ctx->ilist_n.ensure(2 * kMaxGroups * sizeof(int32_t)));
-                w.ilist = static_cast<int32_t*>(ctx->ilist.p);
-                w.ilist_n = static_cast<int32_t*>(ctx->ilist_n.p);
-            }
             // the search clears what it consumed; a fresh registration starts from zero anyway
             HIP_TRY(hipMemsetAsync(w.need, 0, (size_t)npairs * w.need_stride * sizeof(uint32_t), st));
             HIP_TRY(hipMemsetAsync(w.miss_cnt, 0, (size_t)npairs * sizeof(int32_t), st));
@@ -348,10 +338,9 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.sperm += xs;
         if (wg.kdn) wg.kdn += (int64_t)p0 * kKdnStride;
     }
-    if (wg.nn_lu) {
-        wg.nn_lu += xs;
+    if (wg.nn_u) {
+        wg.nn_u += xs;
         wg.nn_t += xs;
-        wg.nn_xs += xs;
         wg.sinv += xs;
         wg.qlist += xs;
         wg.need += (int64_t)p0 * w.need_stride;
@@ -361,10 +350,6 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.plist += (int64_t)p0 * ((w.x_stride + 63) / 64);
         wg.plist_n += 4 * g;
         wg.queue = wg.plist_n + 1;
-    }
-    if (wg.ilist) {
-        wg.ilist += (int64_t)p0 * ((w.x_stride + 63) / 64);
-        wg.ilist_n += 2 * g;
     }
     if (g > 0) wg.ticks = nullptr;  // debug slots are pair-0 / global
 }
@@ -572,8 +557,8 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     }
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->nn_xs, &ctx->kdn, &ctx->sinv, &ctx->qlist, &ctx->need,
-                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ilist, &ctx->ilist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->kdn, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})
         b->release();

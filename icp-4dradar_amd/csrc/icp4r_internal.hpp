@@ -16,10 +16,9 @@ constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_ke
 constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.py)
 constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
-constexpr int kDefaultLightMax = 0;  // batched search: pairs with at most this many misses -> nn_light_kernel (0: off; measured slower)
 constexpr int kMaxGroups = 4;        // batched plans: pair groups on their own streams (run_pairs)
 constexpr int kDefaultGroups = 2;
-constexpr int kDefaultPartSize = 1024;  // batched search: misses per work item of a heavy pair  // batched search: pairs with at most this many misses -> nn_light_kernel
+constexpr int kDefaultPartSize = 1024;  // batched search: misses per work item of a heavy pair
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
 constexpr int kPrunedMinM = 512;  // ICP4R_NN_AUTO prunes when the largest target has >= this many points
@@ -124,16 +123,14 @@ struct WorkArgs {
     int64_t t_stride, b_stride, sb_stride;
     float4* corr;       // PCL numerics: [npairs * x_stride * 2] per source point {s.xyz, w}, {d.xyz, d²}
     // Cached-neighbour test (nn_lds_kernel<true>; nullptr = off):
-    float2* nn_lu;      // [npairs * x_stride] (L_i, U_i): L a lower bound on |X_i - t_k| for every
-                        // target k other than the NN, U an upper bound of the second-nearest distance;
-                        // set by a search, widened by every kernel that moves X_i
+    // L_i (X_i.w): a lower bound on |X_i - t_k| for every target k other than the NN; U_i (nn_u[i]):
+    // an upper bound of the second-nearest distance.  Set by a search, widened by every kernel that
+    // moves X_i.
+    float* nn_u;        // [npairs * x_stride] U_i
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
-    float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index (bits)
-    float4* nn_xs;      // [npairs * x_stride] (X_i at its last search, Lo_i): Lo a lower bound, at that
-                        // position, on |X_i - t_k| for every target k outside the NN's kd leaf (the
-                        // second-chance test inside the leaf, nn_lds_kernel); .w = 0: no second chance
-    int32_t second_chance;  // 1: nn_lds_kernel<true> keeps Lo (block-level losers) and runs the second chance
-    int32_t* sinv;      // [npairs * x_stride] source index -> Morton position (inverse of sperm)
+    float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index | the query's
+                        // sorted position << 14 (nt_pack)
+    int32_t* sinv;      // [npairs * x_stride] source index -> sorted position (inverse of sperm)
     int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)
     uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed
     int64_t need_stride;
@@ -142,11 +139,6 @@ struct WorkArgs {
     int32_t* plist;     // [npairs * ceil(x_stride / 64)] items (pair << 10 | part)
     int32_t* plist_n;   // [4]: items, (queue), the pass's part size (nn_order_kernel)
     int32_t* queue;     // [1] next work-list index (reset by nn_order_kernel)
-    // nn_light_kernel (nullptr = off): items (pair << 10 | chunk of 64 misses) of the pairs with
-    // 1..light_max misses; ilist_n[0] = items, ilist_n[1] = the light queue
-    int32_t* ilist;     // [npairs * ceil(x_stride / 64)]
-    int32_t* ilist_n;   // [2]
-    int32_t light_max;
     int32_t part_size;  // nn_lds_kernel: misses per work item of a heavy pair (0: one item per pair);
                         // plist holds items (pair << 10 | part)
     unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,

@@ -1229,7 +1229,19 @@ struct LdsNN {
 // bits — an involution per block (bank spreading for the drain, see nn_lds_kernel)
 __device__ __forceinline__ int lds_swz(int p) { return p ^ ((p >> 4) & (kLdsLeaf - 1)); }
 
-// Bounds on the second-nearest distance of X_i (float2 nn_lu[i]):
+// nn_t[i].w packs the NN's target index (bits 0..13) and the query's sorted position (bits 14..27):
+// the test reads one record for the key and for the miss bitmap's bit.  Sizes: <= kCacheMaxN = 2^14
+// sources, <= 8192 targets on the batched plan.
+constexpr int kNtPosShift = 14;
+constexpr int kNtIdxMask = (1 << kNtPosShift) - 1;
+static_assert(kCacheMaxN <= (1 << kNtPosShift) && kLdsTargets <= (1 << kNtPosShift), "nn_t.w packing");
+__device__ __forceinline__ float nt_pack(int idx, int pos) {
+    return __uint_as_float((uint32_t)idx | ((uint32_t)pos << kNtPosShift));
+}
+__device__ __forceinline__ uint32_t nt_idx(float w) { return __float_as_uint(w) & kNtIdxMask; }
+__device__ __forceinline__ uint32_t nt_pos(float w) { return __float_as_uint(w) >> kNtPosShift; }
+
+// Bounds on the second-nearest distance of X_i (L in X_i.w, U in nn_u[i]):
 //  L (.x): lower bound on |X_i - t_k| for every target k other than the NN — the cache test's;
 //  U (.y): upper bound on the second-nearest distance — the next search's initial pruning bound.
 // From the second-smallest d² a search saw (every other target has float d² >= sec; the true
@@ -1248,26 +1260,6 @@ __device__ __forceinline__ float2 move_lu(float2 lu, float ox, float oy, float o
 
 __device__ __forceinline__ bool cache_hit(float L, float dj2) {
     return L * L * (1.0f - kCacheMargin) > dj2 * (1.0f + kCacheMargin);
-}
-
-// Smallest (d², index) key of LDS block b (lds_swz layout) for query (x, y, z); `cb` = that target.
-// s2: the second-smallest d² (bits) of the block's other targets (+inf bits when none).
-__device__ __forceinline__ NNKey lds_block_min(const v4f* tl, int b, float x, float y, float z, uint32_t& s2, v4f& cb) {
-    const v4f* tb = tl + b * kLdsLeaf;
-    const int sw = b & (kLdsLeaf - 1);
-    NNKey k1 = ~0ull;
-    s2 = 0x7f800000u;
-    cb = tb[sw];
-#pragma unroll
-    for (int t = 0; t < kLdsLeaf; ++t) {
-        const v4f c = tb[t ^ sw];
-        const float d2 = l2_simple(x, y, z, c.x, c.y, c.z);
-        const NNKey kn = make_key(d2, __float_as_uint(c.w));
-        s2 = kn < k1 ? (t == 0 ? s2 : (uint32_t)(k1 >> 32)) : min(s2, __float_as_uint(d2));
-        cb = kn < k1 ? c : cb;
-        k1 = kn < k1 ? kn : k1;
-    }
-    return k1;
 }
 
 __device__ __forceinline__ void write_corr_t(const WorkArgs& w, const PairArgs& a, int p, int i, float sx, float sy,
@@ -1311,9 +1303,8 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     __syncthreads();
     float4* X = w.X + (int64_t)p * w.x_stride;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
-    float2* lu = w.nn_lu + (int64_t)p * w.x_stride;
+    float* uu = w.nn_u + (int64_t)p * w.x_stride;
     const float4* nt = w.nn_t + (int64_t)p * w.x_stride;
-    const int32_t* sinv = w.sinv + (int64_t)p * w.x_stride;
     // In the iteration passes the previous update's transformCloud(T_inc) is applied here (the
     // update defers it: X_i is read and written once per iteration, and the bounds move with it).
     const bool xform = !fitness_pass;
@@ -1323,15 +1314,13 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     // Every load is coalesced (the NN's coordinates come from nn_t, not a gather from the target
     // cloud) and issued before the first store (a load after a store waits behind it on vmcnt).
     float4 v[kTestPer], t[kTestPer];
-    float2 L[kTestPer];
-    int32_t sp[kTestPer];
+    float U[kTestPer];
 #pragma unroll
     for (int e = 0; e < kTestPer; ++e) {
         const int i = min(i0 + e * kTestWG + tid, n - 1);
-        v[e] = X[i];
+        v[e] = X[i];  // .w = L
         t[e] = nt[i];
-        L[e] = lu[i];
-        sp[e] = sinv[i];
+        U[e] = xform ? uu[i] : 0.0f;
     }
     int hits = 0, misses = 0;
 #pragma unroll
@@ -1341,21 +1330,22 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
         if (xform) {
             float4 o = v[e];
             xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
-            L[e] = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            o.w = Lm.x;
             v[e] = o;
             if (valid) {
                 X[i] = o;
-                lu[i] = L[e];
+                uu[i] = Lm.y;
             }
         }
         const float d2 = l2_simple(v[e].x, v[e].y, v[e].z, t[e].x, t[e].y, t[e].z);
-        const bool hit = valid & cache_hit(L[e].x, d2);  // '&': a conditional use would sink the load
-        asm volatile("" ::"v"(sp[e]));                    // ... and keep the sinv load up front as well
+        const bool hit = valid & cache_hit(v[e].w, d2);  // '&': a conditional use would sink the load
+        const uint32_t sp = nt_pos(t[e].w);
         if (hit) {
-            key[i] = make_key(d2, __float_as_uint(t[e].w));
+            key[i] = make_key(d2, nt_idx(t[e].w));  // the finish kernel's fitness reads the keys
             ++hits;
         } else if (valid) {
-            atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
+            atomicOr(&need[sp >> 5], 1u << (sp & 31));
             ++misses;
         }
     }
@@ -1384,23 +1374,16 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
 // CACHE), work = its source count.
 constexpr int kOrderWG = 1024;
 constexpr int kOrderBuckets = 32;
-constexpr int kLightWG = 256;
-constexpr int kLightQ = 64;  // nn_light_kernel: queries per work item
-constexpr int kLightChunkBits = 10;
-static_assert(kCacheMaxN / kLightQ <= (1 << kLightChunkBits), "chunk field");
-constexpr int kLightCand = 64;  // nn_light_kernel: candidate blocks per query held in LDS
+constexpr int kPartBits = 10;  // work item = pair << kPartBits | part (parts of >= 64 misses)
+static_assert(kCacheMaxN / 64 <= (1 << kPartBits), "part field");
 
 __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
                                                             int all, int ncu) {
     __shared__ int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
-    __shared__ int32_t nitem;
     __shared__ unsigned long long tot_s;
     const int tid = threadIdx.x;
     if (tid < kOrderBuckets) bcnt[tid] = 0;
-    if (tid == 0) {
-        nitem = 0;
-        tot_s = 0;
-    }
+    if (tid == 0) tot_s = 0;
     __syncthreads();
     if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
         unsigned long long t = 0;
@@ -1410,8 +1393,6 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
         if ((tid & 63) == 0) atomicAdd(&tot_s, t);
     }
     __syncthreads();
-    // light: a pair with 1..light_max misses goes to nn_light_kernel as ceil(misses / 64) items
-    const bool light_ok = !all && w.ilist != nullptr;
     auto work = [&](int p) {
         return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
     };
@@ -1426,13 +1407,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
         const int c = work(p);
         if (w.ticks) w.ticks[32 + p] = (uint64_t)c;  // debug: this pass' work per pair (tools/miss_hist.py)
         if (c <= 0) continue;
-        if (light_ok && c <= w.light_max) {
-            const int ni = (c + kLightQ - 1) / kLightQ;
-            const int at = atomicAdd(&nitem, ni);
-            for (int k = 0; k < ni; ++k) w.ilist[at + k] = (p << kLightChunkBits) | k;
-        } else {
-            for (int k = 0, np = heavy_parts(c); k < np; ++k) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1);
-        }
+        for (int k = 0, np = heavy_parts(c); k < np; ++k) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1);
     }
     __syncthreads();
     if (tid == 0) {
@@ -1444,226 +1419,29 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
         *w.plist_n = run;
         *w.queue = 0;
         w.plist_n[2] = ps == (1 << 30) ? 0 : ps;  // nn_lds_kernel: misses per part (0: whole pairs)
-        if (w.ilist) {
-            w.ilist_n[0] = nitem;
-            w.ilist_n[1] = 0;
-        }
     }
     __syncthreads();
     for (int p = tid; p < npairs; p += kOrderWG) {
         const int c = work(p);
-        if (c > 0 && !(light_ok && c <= w.light_max))
+        if (c > 0)
             for (int k = 0, np = heavy_parts(c); k < np; ++k)
-                w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1)] = (p << kLightChunkBits) | k;
+                w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1)] = (p << kPartBits) | k;
     }
 }
 
-// ---- nn_light_kernel: the cached-neighbour misses of pairs with few of them (<= light_max).
-// Each query is searched on its own by a 16-lane group straight from the index, with the pair's
-// block and superblock boxes staged in LDS: the pruning bound is known up front (U of the previous
-// search: an upper bound of the second-nearest distance), so the superblock tests (4 per lane), the
-// block tests (8 lanes per superblock) and the evaluations (lane gl takes target gl of a candidate
-// block, 4 blocks' loads in flight) are lane-parallel; after each candidate list the bound drops to
-// the second-nearest found so far.  The result is the same exact (best key, second-nearest) pair as
-// nn_lds_kernel<true> (tests/test_gpu_parity.py::test_light_search_identical).  Work items
-// (pair << 10 | chunk) of <= 64 queries come from nn_order_kernel.
-// Off by default (light_max = 0): on the C3 workload it adds ~40 us per pass while the LDS search
-// it relieves is bound by its heavy pairs, not by the light ones.
-__global__ __launch_bounds__(kLightWG) void nn_light_kernel(PairArgs a, WorkArgs w) {
-    __shared__ v4f boxes[2 * (kLdsTargets / kLdsLeaf)];  // the pair's block boxes (lo, hi)
-    __shared__ v4f sboxes[2 * (kLdsTargets / kLdsLeaf / kSuper)];
-    __shared__ int16_t cand[kLightWG / 16][kLightCand];  // per group: candidate blocks of its query
-    __shared__ int32_t qs[kLightQ];
-    __shared__ int32_t wtot[kLightWG / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int gl = tid & 15, gw = (tid >> 4) & 3, g = tid >> 4;  // lane in group, group in wave, group
-    const int nitems = uload(w.ilist_n);
-    unsigned long long evals = 0, tests = 0;
-    // items are near-equal (<= 64 queries): a static round-robin, no shared queue counter (thousands
-    // of workgroups on one atomic word serialise at its L2 channel: ~40 us per launch, measured)
-    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const int item = w.ilist[it];
-        const int p = item >> kLightChunkBits, lo = (item & ((1 << kLightChunkBits) - 1)) * kLightQ;
-        const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
-        const int64_t xs = w.x_stride;
-        const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
-        {  // the pair's boxes into LDS (all loads first)
-            const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-            constexpr int PB = 2 * (kLdsTargets / kLdsLeaf) / kLightWG;
-            v4f t[PB];
-#pragma unroll
-            for (int k = 0; k < PB; ++k) t[k] = tbv[min(tid + k * kLightWG, 2 * nb - 1)];
-            const v4f sv = sbv[min(tid, 2 * nsb - 1)];
-#pragma unroll
-            for (int k = 0; k < PB; ++k)
-                if (tid + k * kLightWG < 2 * nb) boxes[tid + k * kLightWG] = t[k];
-            if (tid < 2 * nsb) sboxes[tid] = sv;
-        }
-        // misses with rank [lo, lo + kLightQ) in index order, from the pair's bitmap
-        {
-            constexpr int W = kNeedWords / kLightWG;
-            const int nwords = (n + 31) >> 5;
-            const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
-            const int32_t* sperm = w.sperm + (int64_t)p * xs;
-            uint32_t f[W];
-            int c = 0;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-                const int wi = tid * W + k;
-                f[k] = wi < nwords ? gneed[wi] : 0u;
-                c += __builtin_popcount(f[k]);
-            }
-            int incl = c;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int o = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += o;
-            }
-            if (lane == 63) wtot[wave] = incl;
-            __syncthreads();
-            int r = incl - c;
-            for (int v = 0; v < wave; ++v) r += wtot[v];
-            if (r < lo + kLightQ && r + c > lo) {
-#pragma unroll
-                for (int k = 0; k < W; ++k) {
-                    uint32_t bits = f[k];
-                    while (bits) {
-                        const int b = __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        if (r >= lo && r < lo + kLightQ) qs[r - lo] = sperm[(tid * W + k) * 32 + b];
-                        ++r;
-                    }
-                }
-            }
-        }
-        const int total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-        const int cnt = min(kLightQ, total - lo);
-        __syncthreads();  // qs, boxes complete; wtot is rewritten only after the next barrier
-        const float4* ts = w.tsort + (int64_t)p * w.t_stride;
-        const float4* tgt = a.tgt + uload(a.tgt_off + p);
-        for (int j = g; j < cnt; j += kLightWG / 16) {  // group-uniform
-            const int o = qs[j];
-            const int64_t slot = (int64_t)p * xs + o;
-            const float4 X = w.X[slot];
-            // pruning bound: U of the previous search, moved since — an upper bound of the
-            // second-nearest distance, so every target that can be the nearest or the second-nearest
-            // lies within it
-            const float u = w.nn_lu[slot].y;
-            const float bnd = u * u * 1.00001f;
-            auto lbox = [&](const v4f l, const v4f h, float bound) {
-                const float gx = fmaxf(fmaxf(l.x - X.x, X.x - h.x), 0.0f);
-                const float gy = fmaxf(fmaxf(l.y - X.y, X.y - h.y), 0.0f);
-                const float gz = fmaxf(fmaxf(l.z - X.z, X.z - h.z), 0.0f);
-                return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx)) * kLbShrink <= bound;
-            };
-            uint64_t smask = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int sb = gl + 16 * r;
-                const bool need = sb < nsb && lbox(sboxes[2 * sb], sboxes[2 * sb + 1], bnd);
-                smask |= ((__ballot(need) >> (16 * gw)) & 0xffffull) << (16 * r);
-            }
-            const int nsbc = __builtin_popcountll(smask);
-            NNKey kb = ~0ull;            // this lane's best key
-            uint32_t ls = 0x7f800000u;   // the smallest d² (bits) that lost a comparison on this lane
-            int nev = 0;                 // blocks evaluated
-            // Candidate blocks are gathered two superblocks per step (lanes 0-7 / 8-15 test their
-            // blocks) into the group's LDS list and evaluated a list at a time, lane gl taking target
-            // gl of 4 blocks per round trip; after each list the bound drops to the second-nearest
-            // found so far (a far-off query with a loose U would otherwise evaluate most blocks).
-            float cb = bnd;
-            while (smask) {
-                int nc = 0;  // group-uniform
-                while (smask && nc <= kLightCand - 2 * kSuper) {
-                    const int sa = __builtin_ctzll(smask);
-                    smask &= smask - 1;
-                    const int sb2 = smask ? __builtin_ctzll(smask) : -1;
-                    if (sb2 >= 0) smask &= smask - 1;
-                    const int mysb = gl < kSuper ? sa : sb2;
-                    const int b = mysb * kSuper + (gl & (kSuper - 1));
-                    const bool need = mysb >= 0 && b < nb && lbox(boxes[2 * b], boxes[2 * b + 1], cb);
-                    const uint32_t bm = (uint32_t)((__ballot(need) >> (16 * gw)) & 0xffffu);
-                    if (need) cand[g][nc + __builtin_popcount(bm & ((1u << gl) - 1))] = (int16_t)b;
-                    nc += __builtin_popcount(bm);
-                }
-                for (int c0 = 0; c0 < nc; c0 += 4) {
-                    float4 t4[4];
-#pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) t4[u4] = ts[(int)cand[g][min(c0 + u4, nc - 1)] * kLdsLeaf + gl];
-#pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) {
-                        if (c0 + u4 >= nc) break;
-                        const NNKey kn = make_key(l2_simple(X.x, X.y, X.z, t4[u4].x, t4[u4].y, t4[u4].z), __float_as_uint(t4[u4].w));
-                        ls = min(ls, (uint32_t)((kn < kb ? kb : kn) >> 32));
-                        kb = kn < kb ? kn : kb;
-                    }
-                }
-                nev += nc;
-                if (smask) {  // tighten: the group's second-nearest so far
-                    NNKey K = kb;
-#pragma unroll
-                    for (int off = 1; off < 16; off <<= 1) {
-                        const uint32_t hi = __shfl_xor((uint32_t)(K >> 32), off, 64);
-                        const uint32_t lw = __shfl_xor((uint32_t)K, off, 64);
-                        const NNKey o2 = ((NNKey)hi << 32) | lw;
-                        K = o2 < K ? o2 : K;
-                    }
-                    uint32_t S = kb != K ? min(ls, (uint32_t)(kb >> 32)) : ls;
-#pragma unroll
-                    for (int off = 1; off < 16; off <<= 1) S = min(S, (uint32_t)__shfl_xor(S, off, 64));
-                    cb = fminf(cb, __uint_as_float(S));
-                }
-            }
-            // the group's best key and second-nearest d² (bits): every key but the winner lost once
-            NNKey K = kb;
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) {
-                const uint32_t hi = __shfl_xor((uint32_t)(K >> 32), off, 64);
-                const uint32_t lw = __shfl_xor((uint32_t)K, off, 64);
-                const NNKey o2 = ((NNKey)hi << 32) | lw;
-                K = o2 < K ? o2 : K;
-            }
-            uint32_t S = kb != K ? min(ls, (uint32_t)(kb >> 32)) : ls;
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) S = min(S, (uint32_t)__shfl_xor(S, off, 64));
-            if (gl == 0) {
-                w.nn_key[slot] = K;
-                w.nn_lu[slot] = lu_from_sec(__uint_as_float(S));
-                if (w.nn_xs) w.nn_xs[slot] = make_float4(0.f, 0.f, 0.f, 0.f);  // no Lo: no second chance
-                const float4 t = tgt[key_idx(K)];
-                w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(K)));
-                evals += (unsigned long long)nev * kLdsLeaf;
-                tests += (unsigned long long)(nsb + kSuper * nsbc);
-            }
-        }
-        __syncthreads();  // qs / wtot / boxes are rewritten by the next item
-    }
-    evals = wave_sum(evals);
-    tests = wave_sum(tests);
-    if (lane == 0) {
-        count_add(w.evals, 0, evals);
-        count_add(w.evals, 1, tests);
-    }
-}
-
-// ---- nn_lds_kernel<CACHE, SC>: persistent search over the pair work list.
-// SC (second chance, CACHE only): the pruning bound and the smallest-loser bookkeeping work on block
-// minima instead of single targets, so a search also yields Lo = the distance to the nearest target
-// outside the winner's 16-target kd leaf (every block is evaluated whole: the smallest losing block
-// minimum is that distance).  Stored with the query's position (nn_xs), it lets a later pass settle a
-// query the cached-neighbour test missed by evaluating just that leaf: when the leaf's best target is
-// closer than Lo - |X - X_s|, it is the exact NN (before any traversal, below).
-template <bool CACHE, bool SC>
+// ---- nn_lds_kernel<CACHE>: persistent search over the pair work list.
+// CACHE: per searched query the exact second-nearest distance too, stored as the cached-neighbour
+// state: L in X_i.w, U in nn_u[i], the NN's coordinates in nn_t[i] with .w = its index | the query's
+// sorted position << 14 (nt_pack) — the position is what the next test flags a miss at.
+template <bool CACHE>
 __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
-    static_assert(CACHE || !SC, "the second chance needs the cached-neighbour state");
     constexpr int Q = kLdsQ;
     __shared__ LdsNN sh;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool corr = w.corr != nullptr && !fitness_pass;
     const int npl = uload(w.plist_n);
-    unsigned long long evals = 0, tests = 0, sc_hits = 0;
+    unsigned long long evals = 0, tests = 0;
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
@@ -1674,7 +1452,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const bool tk = w.ticks != nullptr && tid == 0;
         uint64_t tk0 = tk ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = tk0, tk2 = tk0;
         const int item = w.plist[idx];
-        const int p = item >> kLightChunkBits, part = item & ((1 << kLightChunkBits) - 1);
+        const int p = item >> kPartBits, part = item & ((1 << kPartBits) - 1);
         const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
         const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
         float4* X = w.X + (int64_t)p * w.x_stride;
@@ -1716,16 +1494,17 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const int4* s4 = reinterpret_cast<const int4*>(sperm + tid * 32);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sv[e] = s4[e];
-                auto put = [&](int v) {
-                    if (o >= lo && o < hi) qlist[o] = v;
+                // entry = source index | sorted position << 14 (the position for nn_t's packed .w)
+                auto put = [&](int v, int pos) {
+                    if (o >= lo && o < hi) qlist[o] = v | (pos << kNtPosShift);
                     ++o;
                 };
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    if ((f >> (4 * e)) & 1) put(sv[e].x);
-                    if ((f >> (4 * e + 1)) & 1) put(sv[e].y);
-                    if ((f >> (4 * e + 2)) & 1) put(sv[e].z);
-                    if ((f >> (4 * e + 3)) & 1) put(sv[e].w);
+                    if ((f >> (4 * e)) & 1) put(sv[e].x, tid * 32 + 4 * e);
+                    if ((f >> (4 * e + 1)) & 1) put(sv[e].y, tid * 32 + 4 * e + 1);
+                    if ((f >> (4 * e + 2)) & 1) put(sv[e].z, tid * 32 + 4 * e + 2);
+                    if ((f >> (4 * e + 3)) & 1) put(sv[e].w, tid * 32 + 4 * e + 3);
                 }
             }
             nlist = min(hi, total) - lo;
@@ -1740,70 +1519,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int i = tid; i < nt; i += kLdsWG) sh.tl[lds_swz(i)] = tsg[i];
         }
         __syncthreads();
-        if (SC && !first && nlist > 0) {
-            // Second chance: a listed query (the test missed) whose previous NN's leaf still holds the
-            // exact NN — the leaf's best target closer than Lo moved by |X - X_s| — is settled here
-            // and dropped from the list (stable in-place compaction, chunk by chunk: a chunk's
-            // entries are all read before any of its survivors is written back, at or below them).
-            int32_t* lst = const_cast<int32_t*>(list);
-            const int32_t* tinv_p = w.tinv + (int64_t)p * w.t_stride;
-            float2* lup = w.nn_lu + (int64_t)p * w.x_stride;
-            const float4* xsp = w.nn_xs + (int64_t)p * w.x_stride;
-            float4* ntp = w.nn_t + (int64_t)p * w.x_stride;
-            int outc = 0;
-            for (int c0 = 0; c0 < nlist; c0 += kLdsWG) {
-                const int s = c0 + tid;
-                const bool in = s < nlist;
-                const int o = lst[in ? s : c0];
-                const float4 v = X[o];
-                const NNKey pk = key[o];
-                const float4 xs = xsp[o];
-                const float2 lu = lup[o];
-                const int pos = tinv_p[key_idx(pk)];
-                // the leaf's best target and runner-up d² (as lds_block_min; a partial unroll keeps the
-                // pass inside the run loop's register budget — a full one spilled)
-                const int bq = pos / kLdsLeaf, swq = bq & (kLdsLeaf - 1);
-                const v4f* tbq = sh.tl + bq * kLdsLeaf;
-                NNKey k1 = ~0ull;
-                uint32_t s2 = 0x7f800000u;
-                v4f cb = tbq[swq];
-#pragma unroll 2
-                for (int t = 0; t < kLdsLeaf; ++t) {
-                    const v4f c = tbq[t ^ swq];
-                    const float d2 = l2_simple(v.x, v.y, v.z, c.x, c.y, c.z);
-                    const NNKey kn = make_key(d2, __float_as_uint(c.w));
-                    s2 = kn < k1 ? (t == 0 ? s2 : (uint32_t)(k1 >> 32)) : min(s2, __float_as_uint(d2));
-                    cb = kn < k1 ? c : cb;
-                    k1 = kn < k1 ? kn : k1;
-                }
-                const float mx = v.x - xs.x, my = v.y - xs.y, mz = v.z - xs.z;
-                const float mv = sqrtf(mx * mx + my * my + mz * mz) * 1.00001f;
-                const float Lo = fmaxf((xs.w - mv) * 0.999999f, 0.0f);
-                const bool hit = in && cache_hit(Lo, key_d2(k1));
-                if (hit) {
-                    key[o] = k1;
-                    ntp[o] = make_float4(cb.x, cb.y, cb.z, cb.w);  // .w: the original index bits
-                    lup[o] = make_float2(fminf(lu_from_sec(__uint_as_float(s2)).x, Lo), lu.y);
-                }
-                const uint64_t km = __ballot(in && !hit);
-                evals += (unsigned long long)__builtin_popcountll(__ballot(in)) * kLdsLeaf;
-                sc_hits += (unsigned long long)__builtin_popcountll(__ballot(hit));
-                if (lane == 0) sh.u.wsum[wave] = __builtin_popcountll(km);
-                __syncthreads();
-                int base = 0, total = 0;
-                for (int u = 0; u < kLdsWaves; ++u) {
-                    const int c = sh.u.wsum[u];
-                    base += u < wave ? c : 0;
-                    total += c;
-                }
-                __syncthreads();  // every wsum read (and every entry of the chunk) before the writes
-                if (in && !hit)
-                    lst[outc + base + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))] = o;
-                outc += total;
-            }
-            nlist = outc;
-            __syncthreads();  // the compacted list visible to the whole workgroup
-        }
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
         const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
@@ -1833,12 +1548,15 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             int orig[Q];
             // the run's query data in three dependent rounds, every load of a round issued together
             // (list -> X, key, U -> the previous match's sorted position)
-            int sidx[Q], o_[Q];
+            int sidx[Q], o_[Q], spos[Q];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const int s0 = base + lane + q * 64;
                 sidx[q] = s0 < cend ? s0 : base;  // idle lanes shadow the run's first query
-                o_[q] = list[sidx[q]];
+                const int e = list[sidx[q]];
+                // the miss list packs the sorted position (compaction above); sperm is in position order
+                o_[q] = (CACHE && !first) ? (e & kNtIdxMask) : e;
+                spos[q] = (CACHE && !first) ? (int)((uint32_t)e >> kNtPosShift) : sidx[q];
             }
             float4 v[Q];
             NNKey pk[Q];
@@ -1847,8 +1565,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) {
                 orig[q] = base + lane + q * 64 < cend ? o_[q] : -1;
                 v[q] = X[o_[q]];
-                pk[q] = key[o_[q]];  // first pass: src_order_kernel's seed key (d² = +inf) or stale
-                uu[q] = (CACHE && !first) ? w.nn_lu[(int64_t)p * w.x_stride + o_[q]].y : 0.0f;
+                pk[q] = key[o_[q]];  // the last search's key (its index = the NN the test kept since)
+                uu[q] = (CACHE && !first) ? w.nn_u[(int64_t)p * w.x_stride + o_[q]] : 0.0f;
             }
             int pj[Q];
 #pragma unroll
@@ -1880,16 +1598,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
                 if (CACHE) {
                     // U of the previous search, moved since: an upper bound of the second-nearest
-                    // distance (SC: of Lo) even if no evaluated target attains it (first pass: none)
+                    // distance even if no evaluated target attains it (first pass: none)
                     uint32_t sec0 = (uint32_t)(hi >> 32);
-                    if (SC) {  // block minima: the seed leaf's and its kd sibling's (same superblock)
-                        uint32_t s2u;
-                        v4f cu;
-                        const NNKey ms = lds_block_min(sh.tl, bj ^ 1, x[q], y[q], z[q], s2u, cu);
-                        sec0 = (uint32_t)((ms > lo ? ms : lo) >> 32);
-                        lo = ms < lo ? ms : lo;
-                        evals += 64 * kLdsLeaf;
-                    }
                     if (!first) sec0 = min(sec0, __float_as_uint(uu[q] * uu[q] * 1.00001f));
                     bestl[q * 64 + lane] = lo;
                     secl[q * 64 + lane] = sec0;
@@ -1955,16 +1665,14 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         const v4f c = cs[t];
                         const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
                         const NNKey kn = make_key(d2, __float_as_uint(c.w));
-                        if (CACHE && !SC) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
+                        if (CACHE) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
                         k1 = kn < k1 ? kn : k1;
                     }
                     if (CACHE) {
                         // every key but the final winner loses exactly one comparison: keep the smallest loser
                         const NNKey old = atomicMin(&bestl[qi], k1);
-                        // (SC: per block minimum — a block evaluated again yields the same minimum)
                         const uint32_t cand =
-                            SC ? (k1 < old ? (uint32_t)(old >> 32) : (k1 == old ? 0x7f800000u : (uint32_t)(k1 >> 32)))
-                               : (k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32)));
+                            k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
                         atomicMin(&secl[qi], cand);
                     } else {
                         atomicMin(&bestl[qi], k1);
@@ -2078,28 +1786,18 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int q = 0; q < Q; ++q) kbq[q] = bestl[q * 64 + lane];
 #pragma unroll
             for (int q = 0; q < Q; ++q) tq[q] = tgt[key_idx(kbq[q])];
-            int wpos[Q];  // SC: the winner's sorted position (its leaf)
-#pragma unroll
-            for (int q = 0; q < Q; ++q) wpos[q] = SC ? tinv[key_idx(kbq[q])] : 0;
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (orig[q] < 0) continue;
                 const NNKey kb = kbq[q];
                 const float4 t = tq[q];
                 key[orig[q]] = kb;
-                if (CACHE) {  // the update reads X, nn_t and the key: no correspondence record
+                if (CACHE) {  // the update reads X, nn_t: no correspondence record
                     const int64_t slot = (int64_t)p * w.x_stride + orig[q];
-                    float2 lu = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
-                    if (SC) {
-                        // secl is Lo: L (every target but the NN) also needs the winner leaf's runner-up
-                        uint32_t s2;
-                        v4f cw;
-                        (void)lds_block_min(sh.tl, wpos[q] / kLdsLeaf, x[q], y[q], z[q], s2, cw);
-                        w.nn_xs[slot] = make_float4(x[q], y[q], z[q], lu.x);
-                        lu.x = fminf(lu.x, lu_from_sec(__uint_as_float(s2)).x);
-                    }
-                    w.nn_lu[slot] = lu;
-                    w.nn_t[slot] = make_float4(t.x, t.y, t.z, __uint_as_float((uint32_t)key_idx(kb)));
+                    const float2 lu = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
+                    X[orig[q]] = make_float4(x[q], y[q], z[q], lu.x);  // .w = L
+                    w.nn_u[slot] = lu.y;
+                    w.nn_t[slot] = make_float4(t.x, t.y, t.z, nt_pack(key_idx(kb), spos[q]));
                 } else if (corr) {
                     write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
                 }
@@ -2117,7 +1815,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     if (lane == 0) {
         count_add(w.evals, 0, evals);
         count_add(w.evals, 1, tests);
-        if (SC) count_add(w.evals, 7, sc_hits);
     }
 }
 
@@ -2485,7 +2182,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     // transformCloud(T_inc), the bounds moved, the test, hit keys, the miss bitmap — done here, where
     // its HBM stream overlaps the other workgroups' latency-bound fold chains instead of taking a
     // launch of its own.  The workgroup owns the pair, so the bitmap is built in LDS and stored whole.
-    if (tail_test && w.nn_lu && sh.s.flag == 0) {
+    if (tail_test && w.nn_u && sh.s.flag == 0) {
         uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
         const int nwords = (n + 31) >> 5;
         for (int k = tid; k < nwords; k += kFoldWG) need[k] = 0u;
@@ -2494,53 +2191,52 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
         __syncthreads();
         float4* X = w.X + (int64_t)p * xs;
-        NNKey* key = w.nn_key + (int64_t)p * xs;
-        float2* lu = w.nn_lu + (int64_t)p * xs;
+        float* uu = w.nn_u + (int64_t)p * xs;
         const float4* nt = w.nn_t + (int64_t)p * xs;
-        const int32_t* sinv = w.sinv + (int64_t)p * xs;
         // kPer points per thread per group, software-pipelined: the next group's loads are issued
         // before this group's stores, so the stores drain while the loads are in flight (a load
         // issued after a store would wait behind it on vmcnt)
         constexpr int kPer = ICP4R_TAIL_PER;
         constexpr int kStep = kFoldWG * kPer;
         int hits = 0, misses = 0;
+        // Per point: X (.w = L) and nn_t (.w = index | sorted position) read, U read; X and U written.
+        // A hit's key is not written: nothing reads it before the next search (which only takes its
+        // index, unchanged by a hit) — the update folds recompute d² from X and nn_t.
         float4 v[kPer], t[kPer];
-        float2 L[kPer];
-        int32_t sp[kPer];
-        auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float2 (&LL)[kPer], int32_t (&ss)[kPer]) {
+        float U[kPer];
+        auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float (&UU)[kPer]) {
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
                 const int i = min(i0 + e * kFoldWG + tid, n - 1);
                 vv[e] = X[i];
                 tt[e] = nt[i];
-                LL[e] = lu[i];
-                ss[e] = sinv[i];
+                UU[e] = uu[i];
             }
         };
-        load(0, v, t, L, sp);
+        load(0, v, t, U);
         for (int i0 = 0; i0 < n; i0 += kStep) {
             float4 vn[kPer], tn[kPer];
-            float2 Ln[kPer];
-            int32_t spn[kPer];
-            if (i0 + kStep < n) load(i0 + kStep, vn, tn, Ln, spn);
+            float Un[kPer];
+            if (i0 + kStep < n) load(i0 + kStep, vn, tn, Un);
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
                 const int i = i0 + e * kFoldWG + tid;
                 const bool valid = i < n;
                 float4 o = v[e];
                 xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
-                const float2 Lm = move_lu(L[e], v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+                const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+                o.w = Lm.x;
                 const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
                 const bool hit = valid & cache_hit(Lm.x, d2);
                 if (valid) {
                     X[i] = o;
-                    lu[i] = Lm;
+                    uu[i] = Lm.y;
                 }
                 if (hit) {
-                    key[i] = make_key(d2, __float_as_uint(t[e].w));
                     ++hits;
                 } else if (valid) {
-                    atomicOr(&need[sp[e] >> 5], 1u << (sp[e] & 31));
+                    const uint32_t sp = nt_pos(t[e].w);
+                    atomicOr(&need[sp >> 5], 1u << (sp & 31));
                     ++misses;
                 }
             }
@@ -2548,8 +2244,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
             for (int e = 0; e < kPer; ++e) {
                 v[e] = vn[e];
                 t[e] = tn[e];
-                L[e] = Ln[e];
-                sp[e] = spn[e];
+                U[e] = Un[e];
             }
         }
         hits = wave_sum(hits);
@@ -2637,14 +2332,16 @@ __global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs 
     const int n = a.src_n[p];
     const float4* src = a.src + a.src_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
-    float2* lu = w.nn_lu ? w.nn_lu + (int64_t)p * w.x_stride : nullptr;
+    float* uu = w.nn_u ? w.nn_u + (int64_t)p * w.x_stride : nullptr;
     for (int i = threadIdx.x; i < n; i += 256) {
         const float4 s = src[i];
         float4 o = s;
         xform_pt(Tf, s.x, s.y, s.z, o.x, o.y, o.z);
-        if (lu) {  // X still holds the last NN pass's points (a deferred transform never ran)
+        if (uu) {  // X still holds the last NN pass's points (a deferred transform never ran), .w = L
             const float4 old = X[i];
-            lu[i] = move_lu(lu[i], old.x, old.y, old.z, o.x, o.y, o.z);
+            const float2 Lm = move_lu(make_float2(old.w, uu[i]), old.x, old.y, old.z, o.x, o.y, o.z);
+            o.w = Lm.x;
+            uu[i] = Lm.y;
         }
         X[i] = o;
     }
@@ -2778,9 +2475,8 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
                          int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
-    const bool cache = w.nn_lu != nullptr;
-    if (cache && (w.x_stride > kCacheMaxN || !w.sinv || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t ||
-                  !w.nn_xs || !w.defer_xform))
+    const bool cache = w.nn_u != nullptr;
+    if (cache && (w.x_stride > kCacheMaxN || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t || !w.defer_xform))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
     hipError_t e;
@@ -2794,14 +2490,10 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
                        (first || !cache) ? 1 : 0, ncu);
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
     if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
-    if (cache && w.second_chance)
-        hipLaunchKernelGGL((nn_lds_kernel<true, true>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
-    else if (cache)
-        hipLaunchKernelGGL((nn_lds_kernel<true, false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+    if (cache)
+        hipLaunchKernelGGL((nn_lds_kernel<true>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     else
-        hipLaunchKernelGGL((nn_lds_kernel<false, false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
-    if (cache && !first && w.ilist)
-        hipLaunchKernelGGL(nn_light_kernel, dim3(ncu * 8), dim3(kLightWG), 0, st, a, w);
+        hipLaunchKernelGGL((nn_lds_kernel<false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -317,72 +317,6 @@ def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
     assert (out["1"]["status"] == 0).all()
 
 
-@pytest.mark.parametrize("early", [False, True])
-def test_second_chance_identical(gpu_ctx, oracle_mod, early, monkeypatch):
-    """The second chance (nn_lds_kernel<true, true>: searches keep Lo, the distance to the nearest
-    target outside the NN's kd leaf; a later miss whose leaf still provably holds the NN is settled
-    without a traversal): bit-identical batches with it off, with the light per-query search taking
-    the small pairs (it resets Lo), over ragged shapes, lattice ties and duplicate targets; the oracle
-    on sampled pairs; and it settles a good share of the misses."""
-    import icp4r
-
-    rng = np.random.default_rng(11)
-    lat = _lattice(rng, 14)
-    ls = lat.copy()
-    ls[:, :3] += np.float32(0.25)
-    dup = _pair(1499, 4096)
-    dup = (dup[0], np.concatenate([dup[1], dup[1][::3]]))  # exact duplicate targets
-    shapes = [(8192, 8192)] * 240 + [(8000, 8100), (4096, 8192), (2048, 600), (1000, 1200), (37, 4000)] * 3
-    pairs = [_pair(1400 + k, n, m) for k, (n, m) in enumerate(shapes)] + [(ls, lat), dup]
-    args = _batch(pairs)
-    assert icp4r.plan(len(pairs), 8192, 8192)["lds"] and icp4r.plan(len(pairs), 8192, 8192)["cache"]
-    kw = {} if early else dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-    p = icp4r.default_params(max_iterations=20, **kw)
-    out = {}
-    for sc, light in (("0", "0"), ("1", "0"), ("1", "200")):
-        monkeypatch.setenv("ICP4R_SECOND_CHANCE", sc)
-        monkeypatch.setenv("ICP4R_LIGHT_MAX", light)
-        gpu_ctx.reset_timers()
-        out[sc + light] = gpu_ctx.align_batch_host(*args, params=p)
-        st = gpu_ctx.nn_stats()
-        if sc == "1" and light == "0":
-            assert st["second_chance_hits"] > 0.2 * (st["cache_tested"] - st["cache_hits"])
-        if sc == "0":
-            assert st["second_chance_hits"] == 0
-    assert out["10"].tobytes() == out["00"].tobytes()
-    assert out["1200"].tobytes() == out["00"].tobytes()
-    assert (out["10"]["status"] == 0).all()
-    for k in (0, 239, 243, 244, len(pairs) - 2, len(pairs) - 1):
-        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20, **kw)
-        assert (out["10"][k]["T"].reshape(4, 4).T == o["T"]).all() and out["10"][k]["fitness"] == o["fitness"]
-        assert out["10"][k]["iterations"] == o["iterations"]
-
-
-def test_light_search_identical(gpu_ctx, oracle_mod, monkeypatch):
-    """nn_light_kernel (per-query 16-lane search from the index in HBM, for pairs with few cache
-    misses) returns exactly what the LDS work-list search returns: the batch is bit-identical with
-    the light path off, at its default threshold, and taking every pass-2+ pair; PCL defaults
-    (early stops live) and the oracle on sampled pairs."""
-    import icp4r
-
-    npairs, n = 256, 8192
-    pairs = [_pair(900 + k, n) for k in range(npairs)]
-    args = _batch(pairs)
-    p = icp4r.default_params(max_iterations=20)
-    out = {}
-    for lm in ("0", "1024", "16384"):
-        monkeypatch.setenv("ICP4R_LIGHT_MAX", lm)
-        gpu_ctx.reset_timers()
-        out[lm] = gpu_ctx.align_batch_host(*args, params=p)
-        assert (out[lm]["status"] == 0).all()
-    assert out["0"].tobytes() == out["1024"].tobytes() == out["16384"].tobytes()
-    for k in (0, 77, 255):
-        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=20)
-        r = out["16384"][k]
-        assert (r["T"].reshape(4, 4).T == o["T"]).all() and r["fitness"] == o["fitness"]
-        assert r["iterations"] == o["iterations"] and r["converged"] == o["converged"]
-
-
 def test_pruned_evaluates_fewer_pairs(gpu_ctx):
     """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer."""
     import icp4r
