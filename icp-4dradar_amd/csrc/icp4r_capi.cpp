@@ -253,6 +253,10 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             HIP_TRY(ctx->plist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
             HIP_TRY(ctx->plist_n.ensure(4 * kMaxGroups * sizeof(int32_t)));  // per group: items, queue, part size
             w.plist = static_cast<int32_t*>(ctx->plist.p);
+            HIP_TRY(ctx->qv.ensure((size_t)slots * sizeof(float4)));
+            HIP_TRY(ctx->qm.ensure((size_t)slots * sizeof(uint2)));
+            w.qv = static_cast<float4*>(ctx->qv.p);
+            w.qm = static_cast<uint2*>(ctx->qm.p);
             w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
             w.queue = w.plist_n + 1;
         }
@@ -261,14 +265,16 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float)));
             HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
             w.nn_t = static_cast<float4*>(ctx->nn_t.p);
-            HIP_TRY(ctx->sinv.ensure((size_t)slots * sizeof(int32_t)));
-            HIP_TRY(ctx->qlist.ensure((size_t)slots * sizeof(int32_t)));
+            HIP_TRY(ctx->sq.ensure((size_t)slots * sizeof(float4)));
+            HIP_TRY(ctx->sm.ensure((size_t)slots * sizeof(uint2)));
+
             HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
             HIP_TRY(ctx->miss_cnt.ensure((size_t)npairs * sizeof(int32_t)));
             w.nn_u = static_cast<float*>(ctx->nn_lu.p);
             w.defer_xform = 1;
-            w.sinv = static_cast<int32_t*>(ctx->sinv.p);
-            w.qlist = static_cast<int32_t*>(ctx->qlist.p);
+            w.sq = static_cast<float4*>(ctx->sq.p);
+            w.sm = static_cast<uint2*>(ctx->sm.p);
+
             w.need = static_cast<uint32_t*>(ctx->need.p);
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
             w.part_size = env_int("ICP4R_PART", kDefaultPartSize);
@@ -341,12 +347,14 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
     if (wg.nn_u) {
         wg.nn_u += xs;
         wg.nn_t += xs;
-        wg.sinv += xs;
-        wg.qlist += xs;
+        wg.sq += xs;
+        wg.sm += xs;
         wg.need += (int64_t)p0 * w.need_stride;
         wg.miss_cnt += p0;
     }
     if (wg.plist) {
+        wg.qv += xs;
+        wg.qm += xs;
         wg.plist += (int64_t)p0 * ((w.x_stride + 63) / 64);
         wg.plist_n += 4 * g;
         wg.queue = wg.plist_n + 1;
@@ -557,7 +565,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     }
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
-                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->kdn, &ctx->sinv, &ctx->qlist, &ctx->need,
+                      &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->kdn, &ctx->sq, &ctx->sm, &ctx->qv, &ctx->qm, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})

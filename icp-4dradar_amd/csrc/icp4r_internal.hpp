@@ -128,10 +128,13 @@ struct WorkArgs {
     // moves X_i.
     float* nn_u;        // [npairs * x_stride] U_i
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
-    float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its index | the query's
-                        // sorted position << 14 (nt_pack)
-    int32_t* sinv;      // [npairs * x_stride] source index -> sorted position (inverse of sperm)
-    int32_t* qlist;     // [npairs * x_stride] the pass's search list (source indices, Morton order)
+    float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |
+                        // the query's sorted position << 14 (nt_pack)
+    float4* sq;         // [npairs * x_stride] the pass's miss list in the order the test found them: a
+                        // missed query's {X.xyz, U} (the test appends, the search stages by rank) ...
+    uint2* sm;          // ... {its source index | its NN's sorted target position << 14, its sorted position}
+    float4* qv;         // [npairs * x_stride] a search item's queries in list order {x, y, z, U} ...
+    uint2* qm;          // ... {source index | sorted position << 14, seed's sorted target position}
     uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed
     int64_t need_stride;
     int32_t* miss_cnt;  // [npairs] misses of the current pass (cleared by the search)

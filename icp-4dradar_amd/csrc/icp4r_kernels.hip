@@ -703,12 +703,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             if (tk) tk[3] = __builtin_amdgcn_s_memrealtime();
         } else {
             int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
-            int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
-            for (int pos = tid; pos < n; pos += kIdxWG) {
-                const int i = ord[pos];
-                sp[pos] = i;
-                if (si) si[i] = pos;
-            }
+            for (int pos = tid; pos < n; pos += kIdxWG) sp[pos] = ord[pos];
         }
         return;
     }
@@ -791,12 +786,10 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
         index_boxes(w, p, n);
     } else {
         int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
-        int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
         for (int i = tid; i < n; i += kIdxWG) {
             const float4 v = pts[i];
             const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
             sp[pos] = i;
-            if (si) si[i] = (int32_t)pos;
         }
     }
 }
@@ -805,7 +798,7 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
 // source point descends the target's kd tree (the quantised key of the node's axis against the key of
 // the first point right of the split; equal keys sit on both sides, so they may go either way — the
 // order only decides how well the search prunes), and a counting sort by the leaf reached gives the
-// source order (sperm / sinv): consecutive queries fall in the same or neighbouring target leaves, so
+// source order (sperm): consecutive queries fall in the same or neighbouring target leaves, so
 // query runs stay compact, and the leaf's first target seeds the query's first search (nn_key with
 // d² = +inf, read by the first pass).  It replaces the source's own kd build (index_kernel).
 constexpr int kSoWG = 256;
@@ -871,14 +864,12 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     }
     __syncthreads();
     int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
-    int32_t* si = w.sinv ? w.sinv + (int64_t)p * w.x_stride : nullptr;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const float4* ts = w.tsort + (int64_t)p * w.t_stride;
     for (int i = tid; i < n; i += kSoWG) {
         const int b = leaf_of(src[i]);
         const uint32_t pos = atomicAdd(&bins[b], 1u);
         sp[pos] = i;
-        if (si) si[i] = (int32_t)pos;
         key[i] = make_key(INFINITY, __float_as_uint(ts[b * B].w));  // first-pass seed: the leaf's first target
     }
 }
@@ -1216,12 +1207,16 @@ static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
-    unsigned long long best[kLdsWaves][64 * kLdsQ];    // 8 KB: best (d², index) key per query
     union {
-        uint32_t sec[kLdsWaves][64 * kLdsQ];           // 4 KB: second-smallest d² bits (CACHE search)
-        int32_t wsum[kLdsWaves];                       // compaction
-    } u;
-    uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query slot << 9) | block; + a spare slot per lane
+        unsigned long long best[kLdsWaves][64];        // 8 KB: best (d², index << 13 | position) key per query
+        struct {                                       // staging: the miss bitmap and its word prefixes
+            uint32_t bits[kNeedWords];
+            int32_t pre[kNeedWords];
+        } cz;
+    } r;
+    uint32_t sec[kLdsWaves][64];                       // 4 KB: second-smallest d² bits (CACHE search)
+    uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query lane << 9) | block; + a spare slot per lane
+    int32_t wsum[kLdsWaves];                           // staging: bitmap popcounts per wave
     int32_t cur;                                       // the pair this workgroup works on
 };
 
@@ -1229,17 +1224,49 @@ struct LdsNN {
 // bits — an involution per block (bank spreading for the drain, see nn_lds_kernel)
 __device__ __forceinline__ int lds_swz(int p) { return p ^ ((p >> 4) & (kLdsLeaf - 1)); }
 
-// nn_t[i].w packs the NN's target index (bits 0..13) and the query's sorted position (bits 14..27):
-// the test reads one record for the key and for the miss bitmap's bit.  Sizes: <= kCacheMaxN = 2^14
-// sources, <= 8192 targets on the batched plan.
+// nn_t[i].w packs the NN's sorted target position (bits 0..13) and the query's sorted source position
+// (bits 14..27): the test reads one record for the miss bitmap's bit and for the search record it
+// writes (sq / sm: the next search's seed is that target position, no index lookup).  Sizes:
+// <= kCacheMaxN = 2^14 sources, <= 8192 targets on the batched plan.
 constexpr int kNtPosShift = 14;
 constexpr int kNtIdxMask = (1 << kNtPosShift) - 1;
 static_assert(kCacheMaxN <= (1 << kNtPosShift) && kLdsTargets <= (1 << kNtPosShift), "nn_t.w packing");
-__device__ __forceinline__ float nt_pack(int idx, int pos) {
-    return __uint_as_float((uint32_t)idx | ((uint32_t)pos << kNtPosShift));
+__device__ __forceinline__ float nt_pack(int tpos, int pos) {
+    return __uint_as_float((uint32_t)tpos | ((uint32_t)pos << kNtPosShift));
 }
-__device__ __forceinline__ uint32_t nt_idx(float w) { return __float_as_uint(w) & kNtIdxMask; }
+__device__ __forceinline__ uint32_t nt_tpos(float w) { return __float_as_uint(w) & kNtIdxMask; }
 __device__ __forceinline__ uint32_t nt_pos(float w) { return __float_as_uint(w) >> kNtPosShift; }
+
+// LDS target record .w during the batched search: original index << 13 | sorted position.  Keys
+// compare (d², original index) exactly as before (the index is unique and the position follows
+// it), and the winner's slot in LDS comes back with its key.
+constexpr int kLdsPosBits = 13;
+static_assert(kLdsTargets <= (1 << kLdsPosBits), "LDS key packing");
+__device__ __forceinline__ uint32_t lk_idx(NNKey k) { return (uint32_t)k >> kLdsPosBits; }
+__device__ __forceinline__ uint32_t lk_pos(NNKey k) { return (uint32_t)k & ((1u << kLdsPosBits) - 1); }
+
+// A missed query's search record, appended to its pair's miss list at slot k (in the order the
+// test found them): {X.xyz, U} and {its index | its NN's sorted target position << 14, its sorted
+// position}.  The search stages these by rank instead of gathering X, U and a seed per query.
+__device__ __forceinline__ void put_miss(const WorkArgs& w, int p, int k, uint32_t sp, int i, float x, float y,
+                                         float z, float U, uint32_t tpos) {
+    const int64_t slot = (int64_t)p * w.x_stride + k;
+    w.sq[slot] = make_float4(x, y, z, U);
+    w.sm[slot] = make_uint2((uint32_t)i | (tpos << kNtPosShift), sp);
+}
+
+// Slot of this lane's record in an append list shared by the workgroup (ctr: an LDS counter): one
+// LDS atomic per wave.  Every lane of the wave must call it.
+__device__ __forceinline__ int wave_append(bool flag, int32_t* ctr) {
+    const uint64_t mask = __ballot(flag);
+    if (mask == 0) return -1;
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(ctr, __builtin_popcountll(mask));
+    base = __builtin_amdgcn_readfirstlane(base);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    return flag ? base + (int)rank : -1;
+}
 
 // Bounds on the second-nearest distance of X_i (L in X_i.w, U in nn_u[i]):
 //  L (.x): lower bound on |X_i - t_k| for every target k other than the NN — the cache test's;
@@ -1270,6 +1297,12 @@ __device__ __forceinline__ void write_corr_t(const WorkArgs& w, const PairArgs& 
     C[1] = make_float4(t.x, t.y, t.z, d2);
 }
 
+// With the cached-neighbour state a pass's keys are read only by the finish kernel's fitness (the
+// fitness pass) and by the F64 update (load_nn); the PCL-numerics update folds X and nn_t.
+__device__ __forceinline__ bool keys_read(const PairArgs& a, int fitness_pass) {
+    return fitness_pass || a.kp.numerics != kNumericsPCL;
+}
+
 __device__ __forceinline__ bool pass_wants(int phase, int fitness_pass) {
     return fitness_pass ? (phase != kPhaseInvalid) : (phase == kPhaseActive);
 }
@@ -1290,6 +1323,7 @@ constexpr int kTestPer = 8;
 __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, WorkArgs w, int fitness_pass) {
     __shared__ uint32_t need[kNeedWords];
     __shared__ int32_t wmiss[kTestWG / 64];
+    __shared__ int32_t mbase;  // this workgroup's first slot in the pair's miss list
     const int chunks = gridDim.x;
     const int g = xcd_remap(blockIdx.x + chunks * blockIdx.y, chunks * gridDim.y);
     const int p = g / chunks, chunk = g - p * chunks;
@@ -1305,6 +1339,7 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     float* uu = w.nn_u + (int64_t)p * w.x_stride;
     const float4* nt = w.nn_t + (int64_t)p * w.x_stride;
+    const float4* ts = w.tsort + (int64_t)p * w.t_stride;
     // In the iteration passes the previous update's transformCloud(T_inc) is applied here (the
     // update defers it: X_i is read and written once per iteration, and the bounds move with it).
     const bool xform = !fitness_pass;
@@ -1320,9 +1355,10 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
         const int i = min(i0 + e * kTestWG + tid, n - 1);
         v[e] = X[i];  // .w = L
         t[e] = nt[i];
-        U[e] = xform ? uu[i] : 0.0f;
+        U[e] = uu[i];
     }
     int hits = 0, misses = 0;
+    bool miss[kTestPer];
 #pragma unroll
     for (int e = 0; e < kTestPer; ++e) {
         const int i = i0 + e * kTestWG + tid;
@@ -1333,6 +1369,7 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
             const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
             o.w = Lm.x;
             v[e] = o;
+            U[e] = Lm.y;
             if (valid) {
                 X[i] = o;
                 uu[i] = Lm.y;
@@ -1341,31 +1378,48 @@ __global__ __launch_bounds__(kTestWG) void nn_cache_test_kernel(PairArgs a, Work
         const float d2 = l2_simple(v[e].x, v[e].y, v[e].z, t[e].x, t[e].y, t[e].z);
         const bool hit = valid & cache_hit(v[e].w, d2);  // '&': a conditional use would sink the load
         const uint32_t sp = nt_pos(t[e].w);
+        miss[e] = valid && !hit;
         if (hit) {
-            key[i] = make_key(d2, nt_idx(t[e].w));  // the finish kernel's fitness reads the keys
+            // the finish kernel's fitness reads the keys (their d²; the index from the sorted target)
+            if (keys_read(a, fitness_pass)) key[i] = make_key(d2, __float_as_uint(ts[nt_tpos(t[e].w)].w));
             ++hits;
         } else if (valid) {
             atomicOr(&need[sp >> 5], 1u << (sp & 31));
             ++misses;
         }
     }
+    // this thread's misses -> slots [mbase + the workgroup's prefix, ...) of the pair's miss list
+    int incl = misses;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wmiss[wave] = incl;
     hits = wave_sum(hits);
-    misses = wave_sum(misses);
-    if (lane == 0) wmiss[wave] = misses;
     if (lane == 0) {
         count_add(w.evals, 0, (unsigned long long)hits);
         count_add(w.evals, 2, (unsigned long long)hits);
-        count_add(w.evals, 3, (unsigned long long)(hits + misses));
+        count_add(w.evals, 3, (unsigned long long)hits);
     }
     __syncthreads();
+    int wbase = 0, tot = 0;
+    for (int q = 0; q < kTestWG / 64; ++q) {
+        wbase += q < wave ? wmiss[q] : 0;
+        tot += wmiss[q];
+    }
+    if (tid == 0) {
+        mbase = tot ? atomicAdd(w.miss_cnt + p, tot) : 0;
+        count_add(w.evals, 3, (unsigned long long)tot);
+    }
+    __syncthreads();
+    int k = mbase + wbase + incl - misses;
+#pragma unroll
+    for (int e = 0; e < kTestPer; ++e)
+        if (miss[e]) put_miss(w, p, k++, nt_pos(t[e].w), i0 + e * kTestWG + tid, v[e].x, v[e].y, v[e].z, U[e], nt_tpos(t[e].w));
     uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
     for (int q = tid; q < nwords; q += kTestWG)
         if (need[q]) atomicOr(gneed + q, need[q]);
-    if (tid == 0) {
-        int tot = 0;
-        for (int q = 0; q < kTestWG / 64; ++q) tot += wmiss[q];
-        if (tot) atomicAdd(w.miss_cnt + p, tot);
-    }
 }
 
 // ---- nn_order_kernel: one workgroup.  Pairs to search, bucketed by floor(log2(work)) heaviest
@@ -1435,13 +1489,19 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
 // sorted position << 14 (nt_pack) — the position is what the next test flags a miss at.
 template <bool CACHE>
 __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
-    constexpr int Q = kLdsQ;
+    static_assert(kLdsQ == 1, "one query per lane");
     __shared__ LdsNN sh;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool corr = w.corr != nullptr && !fitness_pass;
+    // keys: without the cached-neighbour state the next search's seed and the records read them
+    const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
     unsigned long long evals = 0, tests = 0;
+    // debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1, ticks[16..26];
+    // tools/nn_events.py): wave-uniform adds, stored once at the end
+    uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
+    uint64_t ck_setup = 0, ck_trav = 0, ck_write = 0;
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
@@ -1455,18 +1515,25 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const int p = item >> kPartBits, part = item & ((1 << kPartBits) - 1);
         const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
         const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
-        float4* X = w.X + (int64_t)p * w.x_stride;
-        const int32_t* sperm = w.sperm + (int64_t)p * w.x_stride;
-        NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
-        const float4* tgt = a.tgt + uload(a.tgt_off + p);
+        const int64_t xs0 = (int64_t)p * w.x_stride;
+        float4* X = w.X + xs0;
+        NNKey* key = w.nn_key + xs0;
+        // (the parts of a heavy pair run concurrently on other workgroups: each stages at its own
+        // absolute ranks [lo, hi) and reads back from qv + lo)
+        float4* qv = w.qv + xs0;
+        uint2* qm = w.qm + xs0;
 
-        // the queries to search: all (first pass / no CACHE) or the test kernel's misses with rank
-        // [lo, lo + part_size) (this item's part), compacted from the pair's bitmap in index order
-        // (stable).  The update kernel clears the bitmap (other parts may still be reading it).
-        int nlist = n;
-        const int32_t* list = sperm;
+        // Stage the item's queries into qv / qm in list order, so every run below reads its
+        // queries with one coalesced load that is issued a run ahead:
+        //  * all queries (first pass / no cached state): sorted position k -> sperm[k]; X gathered,
+        //    U = +inf, the seed = the target at the same relative position (or the source-order
+        //    kernel's seed, or the previous key's target);
+        //  * the test's misses with rank [lo, lo + part_size) (this item's part), in sorted position
+        //    order: the records the test appended to the pair's miss list (sq / sm), each put at its
+        //    rank in the miss bitmap.  The update kernel clears the bitmap (other parts may still be
+        //    reading it).
+        int nlist;
         if (CACHE && !first) {
-            int32_t* qlist = w.qlist + (int64_t)p * w.x_stride;
             const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
             const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
             const int lo = ps > 0 ? part * ps : 0;
@@ -1480,48 +1547,95 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const int o = __shfl_up(incl, off, 64);
                 if (lane >= off) incl += o;
             }
-            if (lane == 63) sh.u.wsum[wave] = incl;
+            if (lane == 63) sh.wsum[wave] = incl;
             __syncthreads();
             int base = 0, total = 0;
             for (int v = 0; v < kLdsWaves; ++v) {
-                const int s = sh.u.wsum[v];
+                const int s = sh.wsum[v];
                 base += v < wave ? s : 0;
                 total += s;
             }
-            int o = base + incl - c;
-            if (f && o < hi && o + c > lo) {  // all 32 source indices of the word in one go (no load behind a store)
-                int4 sv[8];
-                const int4* s4 = reinterpret_cast<const int4*>(sperm + tid * 32);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) sv[e] = s4[e];
-                // entry = source index | sorted position << 14 (the position for nn_t's packed .w)
-                auto put = [&](int v, int pos) {
-                    if (o >= lo && o < hi) qlist[o] = v | (pos << kNtPosShift);
-                    ++o;
-                };
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    if ((f >> (4 * e)) & 1) put(sv[e].x, tid * 32 + 4 * e);
-                    if ((f >> (4 * e + 1)) & 1) put(sv[e].y, tid * 32 + 4 * e + 1);
-                    if ((f >> (4 * e + 2)) & 1) put(sv[e].z, tid * 32 + 4 * e + 2);
-                    if ((f >> (4 * e + 3)) & 1) put(sv[e].w, tid * 32 + 4 * e + 3);
-                }
+            if (tid < nwords) {
+                sh.r.cz.bits[tid] = f;
+                sh.r.cz.pre[tid] = base + incl - c;
             }
             nlist = min(hi, total) - lo;
-            list = qlist + lo;
-            __syncthreads();  // qlist (global, this workgroup's) visible to the whole workgroup
-            if (tk) tk1 = __builtin_amdgcn_s_memrealtime();
+            __syncthreads();
+            // every record of the pair's miss list (in the test's order) goes to its rank: the
+            // rank of sorted position sp = its word's prefix + the set bits below it
+            const float4* sq = w.sq + xs0;
+            const uint2* sm = w.sm + xs0;
+            auto get = [&](int k, float4& v, uint2& mm) {
+                k = min(k, total - 1);
+                v = sq[k];
+                mm = sm[k];
+            };
+            auto put = [&](int k, const float4& v, const uint2& mm) {
+                const uint32_t sp = min(mm.y, (uint32_t)(n - 1));
+                const int r = sh.r.cz.pre[sp >> 5] + __builtin_popcount(sh.r.cz.bits[sp >> 5] & ((1u << (sp & 31)) - 1u));
+                if (k < total && r >= lo && r < hi) {
+                    qv[r] = v;
+                    qm[r] = make_uint2((mm.x & kNtIdxMask) | (sp << kNtPosShift), mm.x >> kNtPosShift);
+                }
+            };
+#pragma nounroll
+            for (int k0 = tid; k0 < total; k0 += 4 * kLdsWG) {
+                float4 v0, v1, v2, v3;  // (named, not an array: an array here went to scratch)
+                uint2 m0, m1, m2, m3;
+                get(k0, v0, m0);  // all loads of the round issued together
+                get(k0 + kLdsWG, v1, m1);
+                get(k0 + 2 * kLdsWG, v2, m2);
+                get(k0 + 3 * kLdsWG, v3, m3);
+                put(k0, v0, m0);
+                put(k0 + kLdsWG, v1, m1);
+                put(k0 + 2 * kLdsWG, v2, m2);
+                put(k0 + 3 * kLdsWG, v3, m3);
+            }
+            qv += lo;  // this item's slice, read back by the runs
+            qm += lo;
+        } else {
+            const int32_t* sperm = w.sperm + xs0;
+            const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
+            for (int k0 = 0; k0 < n; k0 += 4 * kLdsWG) {
+                int o[4];
+                float4 v[4];
+                NNKey pk[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = sperm[min(k0 + e * kLdsWG + tid, n - 1)];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = X[o[e]];
+                    pk[e] = key[o[e]];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = k0 + e * kLdsWG + tid;
+                    if (k >= n) continue;
+                    // seed: the previous match (no cached state), the source-order kernel's leaf, or
+                    // the target at the same relative position
+                    const bool prev = !first || seed_key(pk[e], m);
+                    const int seed = prev ? tinv[min((uint32_t)key_idx(pk[e]), (uint32_t)(m - 1))]
+                                          : (int)(((int64_t)k * m) / n);
+                    qv[k] = make_float4(v[e].x, v[e].y, v[e].z, INFINITY);
+                    qm[k] = make_uint2((uint32_t)o[e] | ((uint32_t)k << kNtPosShift), (uint32_t)seed);
+                }
+            }
+            nlist = n;
         }
+        if (tk) tk1 = __builtin_amdgcn_s_memrealtime();
 
-        {  // stage the pair's sorted targets into LDS
+        {  // stage the pair's sorted targets into LDS, .w = original index << 13 | position
             const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
             const int nt = nsb * kSuper * kLdsLeaf;
-            for (int i = tid; i < nt; i += kLdsWG) sh.tl[lds_swz(i)] = tsg[i];
+            for (int i = tid; i < nt; i += kLdsWG) {
+                v4f t = tsg[i];
+                t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
+                sh.tl[lds_swz(i)] = t;
+            }
         }
-        __syncthreads();
+        __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-        const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
         // lane l holds superblock l's box for every run of the item (nsb <= 64 on this plan)
         v4f isl, ish;
         {
@@ -1530,59 +1644,47 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             isl = sbv[2 * sbl];
             ish = sbv[2 * sbl + 1];
         }
-        unsigned long long* bestl = sh.best[wave];
-        uint32_t* secl = sh.u.sec[wave];
+        unsigned long long* bestl = sh.r.best[wave];
+        uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
 
-        // Queries per wave run: the list is cut into R rounds of kLdsWaves equal Morton-contiguous
-        // runs of at most 64*Q (R = ceil(nlist / (kLdsWaves * 64 Q))), so every wave gets the same
-        // share — a short list (the misses of a late pass) spreads over all waves, and the traversal,
+        // Queries per wave run: the list is cut into R rounds of kLdsWaves equal position-contiguous
+        // runs of at most 64 (R = ceil(nlist / (kLdsWaves * 64))), so every wave gets the same share —
+        // a short list (the misses of a late pass) spreads over all waves, and the traversal,
         // latency-bound per wave, runs on small runs whose tight query box prunes most superblocks.
-        const int rounds = max(1, (nlist + kLdsWaves * 64 * Q - 1) / (kLdsWaves * 64 * Q));
+        const int rounds = max(1, (nlist + kLdsWaves * 64 - 1) / (kLdsWaves * 64));
         const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
-        for (int base = wave * per; base < nlist; base += kLdsWaves * per) {
+        const int stride = kLdsWaves * per;
+        // the run's records (idle lanes shadow the run's first query: they never queue work and
+        // never widen the run's box); the next run's are loaded while this one is searched
+        auto fetch = [&](int b, float4& v, uint2& mq) {
+            const int s = (b + lane < min(b + per, nlist)) ? b + lane : b;
+            v = qv[s];
+            mq = qm[s];
+        };
+        float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint2 nm = make_uint2(0u, 0u);
+        if (wave * per < nlist) fetch(wave * per, nv, nm);
+        for (int base = wave * per; base < nlist; base += stride) {
             const int cend = min(base + per, nlist);
-            float x[Q], y[Q], z[Q];
-            float bnd[Q];  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
-                           // -1 on idle lanes (never queue work, never widen the coarse bound)
-            int orig[Q];
-            // the run's query data in three dependent rounds, every load of a round issued together
-            // (list -> X, key, U -> the previous match's sorted position)
-            int sidx[Q], o_[Q], spos[Q];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                const int s0 = base + lane + q * 64;
-                sidx[q] = s0 < cend ? s0 : base;  // idle lanes shadow the run's first query
-                const int e = list[sidx[q]];
-                // the miss list packs the sorted position (compaction above); sperm is in position order
-                o_[q] = (CACHE && !first) ? (e & kNtIdxMask) : e;
-                spos[q] = (CACHE && !first) ? (int)((uint32_t)e >> kNtPosShift) : sidx[q];
-            }
-            float4 v[Q];
-            NNKey pk[Q];
-            float uu[Q];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                orig[q] = base + lane + q * 64 < cend ? o_[q] : -1;
-                v[q] = X[o_[q]];
-                pk[q] = key[o_[q]];  // the last search's key (its index = the NN the test kept since)
-                uu[q] = (CACHE && !first) ? w.nn_u[(int64_t)p * w.x_stride + o_[q]] : 0.0f;
-            }
-            int pj[Q];
-#pragma unroll
-            for (int q = 0; q < Q; ++q)
-                pj[q] = (first && !seed_key(pk[q], m)) ? (int)(((int64_t)sidx[q] * m) / n)
-                                                       : tinv[min((uint32_t)key_idx(pk[q]), (uint32_t)(m - 1))];
-            const int seed_pos0 = pj[0];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                x[q] = v[q].x;
-                y[q] = v[q].y;
-                z[q] = v[q].z;
-                // seed: the previous match (first pass: the target at the same relative index
-                // position) and the rest of its 16-target block, evaluated up front from LDS — tight
-                // initial bounds, so the coarse tests below already prune with them
-                const int bj = pj[q] / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
+            const uint64_t ck0 = __builtin_readcyclecounter();
+            ++ev_runs;
+            ev_q += (uint32_t)(cend - base);
+            const float x = nv.x, y = nv.y, z = nv.z, uu = nv.w;
+            const bool live = base + lane < cend;
+            const int orig = (int)(nm.x & kNtIdxMask);
+            const int spos = (int)(nm.x >> kNtPosShift);
+            const int pj = min((int)nm.y, m - 1);
+            __builtin_amdgcn_sched_barrier(0);  // the current record consumed before the prefetch
+            if (base + stride < nlist) fetch(base + stride, nv, nm);
+            float bnd;  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
+                        // -1 on idle lanes (never queue work, never widen the coarse bound)
+            const int seed_pos0 = __builtin_amdgcn_readfirstlane(pj);
+            {
+                // seed: the previous match (first pass: the target at the same relative position)
+                // and the rest of its 16-target block, evaluated up front from LDS — tight initial
+                // bounds, so the coarse tests below already prune with them
+                const int bj = pj / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
                 const v4f* tb = sh.tl + bj * kLdsLeaf;
                 NNKey lo = ~0ull, hi = ~0ull;  // the two smallest distinct keys seen
                 v4f cs[kLdsLeaf];
@@ -1592,60 +1694,41 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) {
                     const v4f c = cs[t];
-                    const NNKey kn = make_key(l2_simple(x[q], y[q], z[q], c.x, c.y, c.z), __float_as_uint(c.w));
+                    const NNKey kn = make_key(l2_simple(x, y, z, c.x, c.y, c.z), __float_as_uint(c.w));
                     hi = kn < lo ? lo : (kn != lo && kn < hi ? kn : hi);
                     lo = kn < lo ? kn : lo;
                 }
+                bestl[lane] = lo;
                 if (CACHE) {
                     // U of the previous search, moved since: an upper bound of the second-nearest
-                    // distance even if no evaluated target attains it (first pass: none)
-                    uint32_t sec0 = (uint32_t)(hi >> 32);
-                    if (!first) sec0 = min(sec0, __float_as_uint(uu[q] * uu[q] * 1.00001f));
-                    bestl[q * 64 + lane] = lo;
-                    secl[q * 64 + lane] = sec0;
-                    bnd[q] = orig[q] >= 0 ? __uint_as_float(sec0) : -1.0f;
+                    // distance even if no evaluated target attains it (all-query passes: +inf)
+                    const uint32_t sec0 = min((uint32_t)(hi >> 32), __float_as_uint(uu * uu * 1.00001f));
+                    secl[lane] = sec0;
+                    bnd = live ? __uint_as_float(sec0) : -1.0f;
                 } else {
-                    bestl[q * 64 + lane] = lo;
-                    bnd[q] = orig[q] >= 0 ? key_d2(lo) : -1.0f;
+                    bnd = live ? key_d2(lo) : -1.0f;
                 }
                 evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
             }
-            float qlo[3], qhi[3], qmax = 0.0f;
-            qlo[0] = qhi[0] = x[0];
-            qlo[1] = qhi[1] = y[0];
-            qlo[2] = qhi[2] = z[0];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                qlo[0] = fminf(qlo[0], x[q]); qhi[0] = fmaxf(qhi[0], x[q]);
-                qlo[1] = fminf(qlo[1], y[q]); qhi[1] = fmaxf(qhi[1], y[q]);
-                qlo[2] = fminf(qlo[2], z[q]); qhi[2] = fmaxf(qhi[2], z[q]);
-                qmax = fmaxf(qmax, bnd[q]);
-            }
+            float qlo[3] = {x, y, z}, qhi[3] = {x, y, z};
 #pragma unroll
             for (int k = 0; k < 3; ++k) {  // DPP reductions (no LDS round trips), wave-uniform results
                 qlo[k] = wave_minf(qlo[k]);
                 qhi[k] = wave_maxf(qhi[k]);
             }
-            qmax = wave_maxf(qmax);
+            const float qmax = wave_maxf(bnd);
 
             // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
             uint32_t head = 0, tail = 0;
             auto drain = [&](uint32_t cnt) {
+                ++ev_drain;
+                ev_items += cnt;
                 const bool act = (uint32_t)lane < cnt;
                 const uint32_t it = ring[(head + lane) & (kRing - 1)];
-                const int qi = act ? (int)(it >> 9) : 0;
+                const int owner = act ? (int)(it >> 9) : 0;
                 const int b = act ? (int)(it & 0x1ffu) : 0;
-                const int owner = qi & 63, slot = qi >> 6;
-                float qx = 0.f, qy = 0.f, qz = 0.f;
-#pragma unroll
-                for (int q = 0; q < Q; ++q) {  // the query's coordinates from its owner lane
-                    const float vx = __shfl(x[q], owner, 64), vy = __shfl(y[q], owner, 64), vz = __shfl(z[q], owner, 64);
-                    if (slot == q) {
-                        qx = vx;
-                        qy = vy;
-                        qz = vz;
-                    }
-                }
+                // the query's coordinates from its owner lane
+                const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
                 if (act) {
                     NNKey k1 = ~0ull;
                     uint32_t s2 = 0x7f800000u;  // second-smallest d² of the block (bits; +inf)
@@ -1670,51 +1753,45 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     }
                     if (CACHE) {
                         // every key but the final winner loses exactly one comparison: keep the smallest loser
-                        const NNKey old = atomicMin(&bestl[qi], k1);
+                        const NNKey old = atomicMin(&bestl[owner], k1);
                         const uint32_t cand =
                             k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
-                        atomicMin(&secl[qi], cand);
+                        atomicMin(&secl[owner], cand);
                     } else {
-                        atomicMin(&bestl[qi], k1);
+                        atomicMin(&bestl[owner], k1);
                     }
                 }
                 head += cnt;
                 evals += (unsigned long long)cnt * kLdsLeaf;
-#pragma unroll
-                for (int q = 0; q < Q; ++q)  // tighter bounds for the tests
-                    bnd[q] = orig[q] < 0 ? -1.0f
-                             : CACHE     ? __uint_as_float(secl[q * 64 + lane])
-                                         : key_d2(bestl[q * 64 + lane]);
+                // tighter bounds for the tests
+                bnd = !live ? -1.0f : CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane]);
             };
-            // Queue the lanes whose query `q` may reach block b.
-            auto push = [&](int b, const v4f lo, const v4f hi, uint32_t qslots) {
-#pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    if (!((qslots >> q) & 1)) continue;
-                    tests += 64;
-                    const float gx = fmaxf(fmaxf(lo.x - x[q], x[q] - hi.x), 0.0f);
-                    const float gy = fmaxf(fmaxf(lo.y - y[q], y[q] - hi.y), 0.0f);
-                    const float gz = fmaxf(fmaxf(lo.z - z[q], z[q] - hi.z), 0.0f);
-                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                    const bool need = lbd * kLbShrink <= bnd[q];
-                    const uint64_t mask = __ballot(need);
-                    if (mask == 0) continue;
-                    {  // every lane writes (no exec-mask branch): lanes that do not need b write their own
-                       // spare slot past the ring
-                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                        const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
-                        ring[at] = (uint16_t)(((uint32_t)(q * 64 + lane) << 9) | (uint32_t)b);
-                    }
-                    tail += (uint32_t)__builtin_popcountll(mask);
-                    if (tail - head >= 64) drain(64);
+            // Queue the lanes whose query may reach block b.
+            auto push = [&](int b, const v4f lo, const v4f hi) {
+                tests += 64;
+                const float gx = fmaxf(fmaxf(lo.x - x, x - hi.x), 0.0f);
+                const float gy = fmaxf(fmaxf(lo.y - y, y - hi.y), 0.0f);
+                const float gz = fmaxf(fmaxf(lo.z - z, z - hi.z), 0.0f);
+                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                const bool need = lbd * kLbShrink <= bnd;
+                const uint64_t mask = __ballot(need);
+                if (mask == 0) return;
+                ++ev_push;
+                {  // every lane writes (no exec-mask branch): lanes that do not need b write their own
+                   // spare slot past the ring
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                    const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
+                    ring[at] = (uint16_t)(((uint32_t)lane << 9) | (uint32_t)b);
                 }
+                tail += (uint32_t)__builtin_popcountll(mask);
+                if (tail - head >= 64) drain(64);
             };
             // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
             // sit in the lanes' registers for the whole item (isl / ish)
             const uint64_t cmask = __ballot(lane < nsb && box_maybe(isl, ish, qlo, qhi, qmax));
             tests += nsb;
-            const int sb0 = __builtin_amdgcn_readfirstlane(seed_pos0) / (kLdsLeaf * kSuper);
+            const int sb0 = seed_pos0 / (kLdsLeaf * kSuper);
             // the candidate superblocks outward from the seed's, alternating up / down (only set bits
             // of cmask are visited: a scalar loop over all nsb cost ~10 SALU per superblock per run)
             uint64_t um = sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
@@ -1736,6 +1813,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             // loads are in flight while the current superblock is tested and its blocks queued; the
             // per-block boxes for the queries' tests are then broadcast from those lanes (readlane)
             // instead of a dependent scalar load per block.
+            const uint64_t ck1 = __builtin_readcyclecounter();
             int sb = next_sb();
             v4f blo = {0.f, 0.f, 0.f, 0.f}, bhi = blo;
             if (sb >= 0) {
@@ -1753,25 +1831,24 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 }
                 const float slx = rdlane(isl.x, sb), sly = rdlane(isl.y, sb), slz = rdlane(isl.z, sb);
                 const float shx = rdlane(ish.x, sb), shy = rdlane(ish.y, sb), shz = rdlane(ish.z, sb);
-                tests += 64 * Q + kSuper;
-                uint32_t qslots = 0;  // query slots with a lane that may reach this superblock
-#pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    const float gx = fmaxf(fmaxf(slx - x[q], x[q] - shx), 0.0f);
-                    const float gy = fmaxf(fmaxf(sly - y[q], y[q] - shy), 0.0f);
-                    const float gz = fmaxf(fmaxf(slz - z[q], z[q] - shz), 0.0f);
-                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                    if (__ballot(lbd * kLbShrink <= bnd[q]) != 0) qslots |= 1u << q;
-                }
-                if (qslots != 0) {
+                tests += 64 + kSuper;
+                ++ev_sbv;
+                // the lanes that may reach this superblock
+                const float gx = fmaxf(fmaxf(slx - x, x - shx), 0.0f);
+                const float gy = fmaxf(fmaxf(sly - y, y - shy), 0.0f);
+                const float gz = fmaxf(fmaxf(slz - z, z - shz), 0.0f);
+                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                if (__ballot(lbd * kLbShrink <= bnd) != 0) {
                     // coarse test of the superblock's blocks at once (lanes 0..7)
                     const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(blo, bhi, qlo, qhi, qmax));
+                    ++ev_sbp;
+                    ev_blk += __builtin_popcount(bmask);
 #pragma unroll
                     for (int k = 0; k < kSuper; ++k)
                         if ((bmask >> k) & 1) {
                             const v4f lo = {rdlane(blo.x, k), rdlane(blo.y, k), rdlane(blo.z, k), 0.f};
                             const v4f hi = {rdlane(bhi.x, k), rdlane(bhi.y, k), rdlane(bhi.z, k), 0.f};
-                            push(sb * kSuper + k, lo, hi, qslots);
+                            push(sb * kSuper + k, lo, hi);
                         }
                 }
                 sb = nsb_;
@@ -1779,29 +1856,27 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 bhi = nhi;
             }
             if (tail != head) drain(tail - head);
-            // every load before the first store (on gfx9 a load waits behind earlier stores on vmcnt)
-            NNKey kbq[Q];
-            float4 tq[Q];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) kbq[q] = bestl[q * 64 + lane];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) tq[q] = tgt[key_idx(kbq[q])];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                if (orig[q] < 0) continue;
-                const NNKey kb = kbq[q];
-                const float4 t = tq[q];
-                key[orig[q]] = kb;
+            const uint64_t ck2 = __builtin_readcyclecounter();
+            // the winner's coordinates come from its LDS slot (the key carries its position)
+            const NNKey kb = bestl[lane];
+            const uint32_t tpos = lk_pos(kb);
+            const v4f t = sh.tl[lds_swz((int)tpos)];
+            if (live) {
+                const NNKey ko = make_key(key_d2(kb), lk_idx(kb));  // (d², original index): PCL's answer
+                if (want_key) key[orig] = ko;
                 if (CACHE) {  // the update reads X, nn_t: no correspondence record
-                    const int64_t slot = (int64_t)p * w.x_stride + orig[q];
-                    const float2 lu = lu_from_sec(__uint_as_float(secl[q * 64 + lane]));
-                    X[orig[q]] = make_float4(x[q], y[q], z[q], lu.x);  // .w = L
-                    w.nn_u[slot] = lu.y;
-                    w.nn_t[slot] = make_float4(t.x, t.y, t.z, nt_pack(key_idx(kb), spos[q]));
+                    const float2 lu = lu_from_sec(__uint_as_float(secl[lane]));
+                    X[orig] = make_float4(x, y, z, lu.x);  // .w = L
+                    w.nn_u[xs0 + orig] = lu.y;
+                    w.nn_t[xs0 + orig] = make_float4(t.x, t.y, t.z, nt_pack((int)tpos, spos));
                 } else if (corr) {
-                    write_corr_t(w, a, p, orig[q], x[q], y[q], z[q], key_d2(kb), t);
+                    write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(t.x, t.y, t.z, 0.f));
                 }
             }
+            const uint64_t ck3 = __builtin_readcyclecounter();
+            ck_setup += ck1 - ck0;
+            ck_trav += ck2 - ck1;
+            ck_write += ck3 - ck2;
         }
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
         if (tk) {
@@ -1815,6 +1890,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     if (lane == 0) {
         count_add(w.evals, 0, evals);
         count_add(w.evals, 1, tests);
+        if (w.ticks) {
+            unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
+            const unsigned long long ev[11] = {ev_runs, ev_q,  ev_sbv,  ev_sbp,   ev_blk,  ev_push,
+                                               ev_drain, ev_items, ck_setup, ck_trav, ck_write};
+            for (int k = 0; k < 11; ++k) atomicAdd(tt + 16 + k, ev[k]);
+        }
     }
 }
 
@@ -2011,6 +2092,7 @@ struct FoldShared {
     float buf[2][9][kFoldRow];
     float res[8];
     int32_t cnt[kFoldWaves];
+    int32_t mcount;  // tail: the pair's miss list length so far
     SolveShared s;
 };
 
@@ -2186,6 +2268,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
         uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
         const int nwords = (n + 31) >> 5;
         for (int k = tid; k < nwords; k += kFoldWG) need[k] = 0u;
+        if (tid == 0) sh.mcount = 0;
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
@@ -2199,9 +2282,10 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
         constexpr int kPer = ICP4R_TAIL_PER;
         constexpr int kStep = kFoldWG * kPer;
         int hits = 0, misses = 0;
-        // Per point: X (.w = L) and nn_t (.w = index | sorted position) read, U read; X and U written.
-        // A hit's key is not written: nothing reads it before the next search (which only takes its
-        // index, unchanged by a hit) — the update folds recompute d² from X and nn_t.
+        // Per point: X (.w = L) and nn_t (.w = target position | sorted position) read, U read; X and U
+        // written; a miss's search record appended to the pair's miss list (sq / sm).  No key is
+        // written: nothing reads one before the fitness pass — the update folds recompute d² from X
+        // and nn_t, and the next search seeds from the record.
         float4 v[kPer], t[kPer];
         float U[kPer];
         auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float (&UU)[kPer]) {
@@ -2232,11 +2316,13 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
                     X[i] = o;
                     uu[i] = Lm.y;
                 }
+                const int k = wave_append(valid && !hit, &sh.mcount);
                 if (hit) {
                     ++hits;
                 } else if (valid) {
                     const uint32_t sp = nt_pos(t[e].w);
                     atomicOr(&need[sp >> 5], 1u << (sp & 31));
+                    put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
                     ++misses;
                 }
             }
@@ -2476,9 +2562,9 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
                          int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused) {
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
     const bool cache = w.nn_u != nullptr;
-    if (cache && (w.x_stride > kCacheMaxN || !w.qlist || !w.need || !w.miss_cnt || !w.nn_t || !w.defer_xform))
+    if (cache && (w.x_stride > kCacheMaxN || !w.sq || !w.qv || !w.need || !w.miss_cnt || !w.nn_t || !w.defer_xform))
         return hipErrorInvalidValue;
-    if (!w.plist || !w.plist_n || !w.queue) return hipErrorInvalidValue;
+    if (!w.plist || !w.plist_n || !w.queue || !w.qv || !w.qm) return hipErrorInvalidValue;
     hipError_t e;
     if (cache && !first && !test_fused) {  // (test_fused: the previous fold_update_kernel ran it)
         const int chunks = (max_n + kTestWG * kTestPer - 1) / (kTestWG * kTestPer);
