@@ -1205,8 +1205,14 @@ constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
+#ifndef ICP4R_BOX_LDS
+#define ICP4R_BOX_LDS 1  // block boxes staged in LDS (else read from the index one superblock ahead)
+#endif
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
+#if ICP4R_BOX_LDS
+    float bx[kLdsTargets / kLdsLeaf][6];               // 12 KB: block boxes lo.xyz, hi.xyz
+#endif
     union {
         unsigned long long best[kLdsWaves][64];        // 8 KB: best (d², index << 13 | position) key per query
         struct {                                       // staging: the miss bitmap and its word prefixes
@@ -1632,10 +1638,21 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
                 sh.tl[lds_swz(i)] = t;
             }
+#if ICP4R_BOX_LDS
+            const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
+            for (int b = tid; b < nsb * kSuper; b += kLdsWG) {
+                const v4f lo = tb[2 * b], hi = tb[2 * b + 1];
+                float* d = sh.bx[b];
+                d[0] = lo.x; d[1] = lo.y; d[2] = lo.z;
+                d[3] = hi.x; d[4] = hi.y; d[5] = hi.z;
+            }
+#endif
         }
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
+#if !ICP4R_BOX_LDS
         const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
+#endif
         // lane l holds superblock l's box for every run of the item (nsb <= 64 on this plan)
         v4f isl, ish;
         {
@@ -1816,19 +1833,23 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             const uint64_t ck1 = __builtin_readcyclecounter();
             int sb = next_sb();
             v4f blo = {0.f, 0.f, 0.f, 0.f}, bhi = blo;
+#if !ICP4R_BOX_LDS
             if (sb >= 0) {
                 const int bl = sb * kSuper + (lane & (kSuper - 1));
                 blo = tbv[2 * bl];
                 bhi = tbv[2 * bl + 1];
             }
+#endif
             while (sb >= 0) {
                 const int nsb_ = next_sb();
+#if !ICP4R_BOX_LDS
                 v4f nlo = blo, nhi = bhi;
                 if (nsb_ >= 0) {
                     const int bl = nsb_ * kSuper + (lane & (kSuper - 1));
                     nlo = tbv[2 * bl];
                     nhi = tbv[2 * bl + 1];
                 }
+#endif
                 const float slx = rdlane(isl.x, sb), sly = rdlane(isl.y, sb), slz = rdlane(isl.z, sb);
                 const float shx = rdlane(ish.x, sb), shy = rdlane(ish.y, sb), shz = rdlane(ish.z, sb);
                 tests += 64 + kSuper;
@@ -1839,6 +1860,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const float gz = fmaxf(fmaxf(slz - z, z - shz), 0.0f);
                 const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
                 if (__ballot(lbd * kLbShrink <= bnd) != 0) {
+#if ICP4R_BOX_LDS
+                    {
+                        const float* bb = sh.bx[sb * kSuper + (lane & (kSuper - 1))];
+                        blo = {bb[0], bb[1], bb[2], 0.f};
+                        bhi = {bb[3], bb[4], bb[5], 0.f};
+                    }
+#endif
                     // coarse test of the superblock's blocks at once (lanes 0..7)
                     const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(blo, bhi, qlo, qhi, qmax));
                     ++ev_sbp;
@@ -1852,8 +1880,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         }
                 }
                 sb = nsb_;
+#if !ICP4R_BOX_LDS
                 blo = nlo;
                 bhi = nhi;
+#endif
             }
             if (tail != head) drain(tail - head);
             const uint64_t ck2 = __builtin_readcyclecounter();
