@@ -1205,14 +1205,14 @@ constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
-#ifndef ICP4R_BOX_LDS
-#define ICP4R_BOX_LDS 1  // block boxes staged in LDS (else read from the index one superblock ahead)
+#ifndef ICP4R_SB_BATCH
+#define ICP4R_SB_BATCH 1  // candidate superblocks tested together per traversal step
 #endif
+constexpr int kSbBatch = ICP4R_SB_BATCH;
+static_assert(kSbBatch >= 1 && kSbBatch <= 5, "six bits per superblock in a 32-bit pack");
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
-#if ICP4R_BOX_LDS
     float bx[kLdsTargets / kLdsLeaf][6];               // 12 KB: block boxes lo.xyz, hi.xyz
-#endif
     union {
         unsigned long long best[kLdsWaves][64];        // 8 KB: best (d², index << 13 | position) key per query
         struct {                                       // staging: the miss bitmap and its word prefixes
@@ -1638,7 +1638,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
                 sh.tl[lds_swz(i)] = t;
             }
-#if ICP4R_BOX_LDS
             const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
             for (int b = tid; b < nsb * kSuper; b += kLdsWG) {
                 const v4f lo = tb[2 * b], hi = tb[2 * b + 1];
@@ -1646,13 +1645,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 d[0] = lo.x; d[1] = lo.y; d[2] = lo.z;
                 d[3] = hi.x; d[4] = hi.y; d[5] = hi.z;
             }
-#endif
         }
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
-#if !ICP4R_BOX_LDS
-        const v4f* tbv = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-#endif
         // lane l holds superblock l's box for every run of the item (nsb <= 64 on this plan)
         v4f isl, ish;
         {
@@ -1783,27 +1778,6 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 // tighter bounds for the tests
                 bnd = !live ? -1.0f : CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane]);
             };
-            // Queue the lanes whose query may reach block b.
-            auto push = [&](int b, const v4f lo, const v4f hi) {
-                tests += 64;
-                const float gx = fmaxf(fmaxf(lo.x - x, x - hi.x), 0.0f);
-                const float gy = fmaxf(fmaxf(lo.y - y, y - hi.y), 0.0f);
-                const float gz = fmaxf(fmaxf(lo.z - z, z - hi.z), 0.0f);
-                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                const bool need = lbd * kLbShrink <= bnd;
-                const uint64_t mask = __ballot(need);
-                if (mask == 0) return;
-                ++ev_push;
-                {  // every lane writes (no exec-mask branch): lanes that do not need b write their own
-                   // spare slot past the ring
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                    const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
-                    ring[at] = (uint16_t)(((uint32_t)lane << 9) | (uint32_t)b);
-                }
-                tail += (uint32_t)__builtin_popcountll(mask);
-                if (tail - head >= 64) drain(64);
-            };
             // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
             // sit in the lanes' registers for the whole item (isl / ish)
             const uint64_t cmask = __ballot(lane < nsb && box_maybe(isl, ish, qlo, qhi, qmax));
@@ -1826,64 +1800,78 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 upnext = !upnext;
                 return sb;
             };
-            // A candidate's 8 block boxes are loaded by lanes 0..7 (lo, hi) one candidate AHEAD, so the
-            // loads are in flight while the current superblock is tested and its blocks queued; the
-            // per-block boxes for the queries' tests are then broadcast from those lanes (readlane)
-            // instead of a dependent scalar load per block.
+            // Candidates are taken kSbBatch at a time: their per-query superblock tests run as
+            // independent chains (the traversal is bound by dependent latency, not by issue); then
+            // every superblock some lane may reach has its 8 blocks tested for every lane in one
+            // straight-line sequence (boxes broadcast from LDS, 8 independent tests in flight), and
+            // the non-empty ones are queued.  A test may use a bound a drain has since tightened:
+            // that only queues more work, never loses a target.
             const uint64_t ck1 = __builtin_readcyclecounter();
-            int sb = next_sb();
-            v4f blo = {0.f, 0.f, 0.f, 0.f}, bhi = blo;
-#if !ICP4R_BOX_LDS
-            if (sb >= 0) {
-                const int bl = sb * kSuper + (lane & (kSuper - 1));
-                blo = tbv[2 * bl];
-                bhi = tbv[2 * bl + 1];
-            }
-#endif
-            while (sb >= 0) {
-                const int nsb_ = next_sb();
-#if !ICP4R_BOX_LDS
-                v4f nlo = blo, nhi = bhi;
-                if (nsb_ >= 0) {
-                    const int bl = nsb_ * kSuper + (lane & (kSuper - 1));
-                    nlo = tbv[2 * bl];
-                    nhi = tbv[2 * bl + 1];
-                }
-#endif
-                const float slx = rdlane(isl.x, sb), sly = rdlane(isl.y, sb), slz = rdlane(isl.z, sb);
-                const float shx = rdlane(ish.x, sb), shy = rdlane(ish.y, sb), shz = rdlane(ish.z, sb);
-                tests += 64 + kSuper;
-                ++ev_sbv;
-                // the lanes that may reach this superblock
-                const float gx = fmaxf(fmaxf(slx - x, x - shx), 0.0f);
-                const float gy = fmaxf(fmaxf(sly - y, y - shy), 0.0f);
-                const float gz = fmaxf(fmaxf(slz - z, z - shz), 0.0f);
-                const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                if (__ballot(lbd * kLbShrink <= bnd) != 0) {
-#if ICP4R_BOX_LDS
-                    {
-                        const float* bb = sh.bx[sb * kSuper + (lane & (kSuper - 1))];
-                        blo = {bb[0], bb[1], bb[2], 0.f};
-                        bhi = {bb[3], bb[4], bb[5], 0.f};
-                    }
-#endif
-                    // coarse test of the superblock's blocks at once (lanes 0..7)
-                    const uint32_t bmask = (uint32_t)__ballot(lane < kSuper && box_maybe(blo, bhi, qlo, qhi, qmax));
-                    ++ev_sbp;
-                    ev_blk += __builtin_popcount(bmask);
+            for (;;) {
+                uint32_t sbpack = 0, valid = 0;
 #pragma unroll
-                    for (int k = 0; k < kSuper; ++k)
-                        if ((bmask >> k) & 1) {
-                            const v4f lo = {rdlane(blo.x, k), rdlane(blo.y, k), rdlane(blo.z, k), 0.f};
-                            const v4f hi = {rdlane(bhi.x, k), rdlane(bhi.y, k), rdlane(bhi.z, k), 0.f};
-                            push(sb * kSuper + k, lo, hi);
-                        }
+                for (int j = 0; j < kSbBatch; ++j) {
+                    const int sbj = next_sb();
+                    if (sbj >= 0) {
+                        sbpack |= (uint32_t)sbj << (6 * j);
+                        valid |= 1u << j;
+                    }
                 }
-                sb = nsb_;
-#if !ICP4R_BOX_LDS
-                blo = nlo;
-                bhi = nhi;
-#endif
+                if (!valid) break;
+                uint32_t pass = 0;
+#pragma unroll
+                for (int j = 0; j < kSbBatch; ++j) {
+                    const int sbj = (sbpack >> (6 * j)) & 63;
+                    const float slx = rdlane(isl.x, sbj), sly = rdlane(isl.y, sbj), slz = rdlane(isl.z, sbj);
+                    const float shx = rdlane(ish.x, sbj), shy = rdlane(ish.y, sbj), shz = rdlane(ish.z, sbj);
+                    // the lanes that may reach this superblock
+                    const float gx = fmaxf(fmaxf(slx - x, x - shx), 0.0f);
+                    const float gy = fmaxf(fmaxf(sly - y, y - shy), 0.0f);
+                    const float gz = fmaxf(fmaxf(slz - z, z - shz), 0.0f);
+                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+                    if (__ballot(lbd * kLbShrink <= bnd) != 0) pass |= 1u << j;
+                }
+                pass &= valid;
+                const int nv = __builtin_popcount(valid);
+                ev_sbv += nv;
+                tests += 64 * nv;
+                for (; pass; pass &= pass - 1) {
+                    const int sb = (sbpack >> (6 * __builtin_ctz(pass))) & 63;
+                    ++ev_sbp;
+                    uint64_t nmk[kSuper];
+#pragma unroll
+                    for (int h = 0; h < kSuper; h += 4) {
+                        float bb[4][6];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+#pragma unroll
+                            for (int c = 0; c < 6; ++c) bb[j][c] = sh.bx[sb * kSuper + h + j][c];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float bgx = fmaxf(fmaxf(bb[j][0] - x, x - bb[j][3]), 0.0f);
+                            const float bgy = fmaxf(fmaxf(bb[j][1] - y, y - bb[j][4]), 0.0f);
+                            const float bgz = fmaxf(fmaxf(bb[j][2] - z, z - bb[j][5]), 0.0f);
+                            const float bl = __builtin_fmaf(bgz, bgz, __builtin_fmaf(bgy, bgy, bgx * bgx));
+                            nmk[h + j] = __ballot(bl * kLbShrink <= bnd);
+                        }
+                    }
+                    tests += 64 * kSuper;
+#pragma unroll
+                    for (int k = 0; k < kSuper; ++k) {  // (unrolled: a rolled loop with one drain
+                        const uint64_t mask = nmk[k];  //  copy measured 9 % slower)
+                        if (mask == 0) continue;
+                        ++ev_blk;
+                        // every lane writes (no exec-mask branch): lanes that do not need the block
+                        // write their own spare slot past the ring
+                        const bool need = (mask >> lane) & 1ull;
+                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                        const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
+                        ring[at] = (uint16_t)(((uint32_t)lane << 9) | (uint32_t)(sb * kSuper + k));
+                        tail += (uint32_t)__builtin_popcountll(mask);
+                        if (tail - head >= 64) drain(64);
+                    }
+                }
             }
             if (tail != head) drain(tail - head);
             const uint64_t ck2 = __builtin_readcyclecounter();
