@@ -1205,6 +1205,25 @@ constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
+// The batched search's box tests against a bound pre-multiplied by kLbGrow (> 1 / kLbShrink with
+// margin): lb <= bnd·kLbGrow rejects only what lb·kLbShrink <= bnd rejects, one multiply fewer per
+// test.  The per-axis gap v - clamp(v, lo, hi) (a med3) has the magnitude of max(lo - v, v - hi, 0)
+// bit for bit (IEEE subtraction is sign-symmetric); a box staged as FLT_MAX (empty) gives +inf.
+constexpr float kLbGrow = 1.00002f;
+__device__ __forceinline__ float pt_lb(const float* b, float x, float y, float z) {
+    const float gx = x - __builtin_amdgcn_fmed3f(x, b[0], b[3]);
+    const float gy = y - __builtin_amdgcn_fmed3f(y, b[1], b[4]);
+    const float gz = z - __builtin_amdgcn_fmed3f(z, b[2], b[5]);
+    return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+}
+// lower bound of the distance between boxes [lo, hi] and [qlo, qhi] (squared; empty: +inf)
+__device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float (&qlo)[3], const float (&qhi)[3]) {
+    const float gx = fmaxf(fmaxf(lo.x - qhi[0], qlo[0] - hi.x), 0.0f);
+    const float gy = fmaxf(fmaxf(lo.y - qhi[1], qlo[1] - hi.y), 0.0f);
+    const float gz = fmaxf(fmaxf(lo.z - qhi[2], qlo[2] - hi.z), 0.0f);
+    return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+}
+
 #ifndef ICP4R_SB_BATCH
 #define ICP4R_SB_BATCH 1  // candidate superblocks tested together per traversal step
 #endif
@@ -1212,7 +1231,8 @@ constexpr int kSbBatch = ICP4R_SB_BATCH;
 static_assert(kSbBatch >= 1 && kSbBatch <= 5, "six bits per superblock in a 32-bit pack");
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
-    float bx[kLdsTargets / kLdsLeaf][6];               // 12 KB: block boxes lo.xyz, hi.xyz
+    float bx[kLdsTargets / kLdsLeaf][6];               // 12 KB: block boxes lo.xyz, hi.xyz (empty: FLT_MAX)
+    float sbx[kLdsTargets / kLdsLeaf / kSuper][6];     // 1.5 KB: superblock boxes
     union {
         unsigned long long best[kLdsWaves][64];        // 8 KB: best (d², index << 13 | position) key per query
         struct {                                       // staging: the miss bitmap and its word prefixes
@@ -1639,11 +1659,15 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 sh.tl[lds_swz(i)] = t;
             }
             const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-            for (int b = tid; b < nsb * kSuper; b += kLdsWG) {
-                const v4f lo = tb[2 * b], hi = tb[2 * b + 1];
-                float* d = sh.bx[b];
-                d[0] = lo.x; d[1] = lo.y; d[2] = lo.z;
-                d[3] = hi.x; d[4] = hi.y; d[5] = hi.z;
+            const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+            for (int b = tid; b < nsb * (kSuper + 1); b += kLdsWG) {
+                const bool blk = b < nsb * kSuper;
+                const int k = blk ? b : b - nsb * kSuper;
+                const v4f lo = blk ? tb[2 * k] : sbg[2 * k], hi = blk ? tb[2 * k + 1] : sbg[2 * k + 1];
+                const bool empty = !(lo.x <= hi.x);  // (+inf, -inf): a box no point reaches
+                float* d = blk ? sh.bx[k] : sh.sbx[k];
+                d[0] = empty ? FLT_MAX : lo.x; d[1] = empty ? FLT_MAX : lo.y; d[2] = empty ? FLT_MAX : lo.z;
+                d[3] = empty ? FLT_MAX : hi.x; d[4] = empty ? FLT_MAX : hi.y; d[5] = empty ? FLT_MAX : hi.z;
             }
         }
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
@@ -1698,7 +1722,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 // bounds, so the coarse tests below already prune with them
                 const int bj = pj / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
                 const v4f* tb = sh.tl + bj * kLdsLeaf;
-                NNKey lo = ~0ull, hi = ~0ull;  // the two smallest distinct keys seen
+                NNKey lo = ~0ull;       // the smallest key seen
+                uint32_t s2 = ~0u;      // the smallest d² of every other target seen (bits)
                 v4f cs[kLdsLeaf];
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) cs[t] = tb[t ^ sw];
@@ -1706,19 +1731,20 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) {
                     const v4f c = cs[t];
-                    const NNKey kn = make_key(l2_simple(x, y, z, c.x, c.y, c.z), __float_as_uint(c.w));
-                    hi = kn < lo ? lo : (kn != lo && kn < hi ? kn : hi);
+                    const float d2 = l2_simple(x, y, z, c.x, c.y, c.z);
+                    const NNKey kn = make_key(d2, __float_as_uint(c.w));
+                    if (CACHE) s2 = kn < lo ? (uint32_t)(lo >> 32) : min(s2, __float_as_uint(d2));
                     lo = kn < lo ? kn : lo;
                 }
                 bestl[lane] = lo;
                 if (CACHE) {
                     // U of the previous search, moved since: an upper bound of the second-nearest
                     // distance even if no evaluated target attains it (all-query passes: +inf)
-                    const uint32_t sec0 = min((uint32_t)(hi >> 32), __float_as_uint(uu * uu * 1.00001f));
+                    const uint32_t sec0 = min(s2, __float_as_uint(uu * uu * 1.00001f));
                     secl[lane] = sec0;
-                    bnd = live ? __uint_as_float(sec0) : -1.0f;
+                    bnd = live ? __uint_as_float(sec0) * kLbGrow : -1.0f;
                 } else {
-                    bnd = live ? key_d2(lo) : -1.0f;
+                    bnd = live ? key_d2(lo) * kLbGrow : -1.0f;
                 }
                 evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
             }
@@ -1776,11 +1802,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 head += cnt;
                 evals += (unsigned long long)cnt * kLdsLeaf;
                 // tighter bounds for the tests
-                bnd = !live ? -1.0f : CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane]);
+                bnd = !live ? -1.0f : (CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane])) * kLbGrow;
             };
             // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
             // sit in the lanes' registers for the whole item (isl / ish)
-            const uint64_t cmask = __ballot(lane < nsb && box_maybe(isl, ish, qlo, qhi, qmax));
+            const uint64_t cmask = __ballot(lane < nsb && box_lb(isl, ish, qlo, qhi) <= qmax);
             tests += nsb;
             const int sb0 = seed_pos0 / (kLdsLeaf * kSuper);
             // the candidate superblocks outward from the seed's, alternating up / down (only set bits
@@ -1822,14 +1848,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                 for (int j = 0; j < kSbBatch; ++j) {
                     const int sbj = (sbpack >> (6 * j)) & 63;
-                    const float slx = rdlane(isl.x, sbj), sly = rdlane(isl.y, sbj), slz = rdlane(isl.z, sbj);
-                    const float shx = rdlane(ish.x, sbj), shy = rdlane(ish.y, sbj), shz = rdlane(ish.z, sbj);
-                    // the lanes that may reach this superblock
-                    const float gx = fmaxf(fmaxf(slx - x, x - shx), 0.0f);
-                    const float gy = fmaxf(fmaxf(sly - y, y - shy), 0.0f);
-                    const float gz = fmaxf(fmaxf(slz - z, z - shz), 0.0f);
-                    const float lbd = __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
-                    if (__ballot(lbd * kLbShrink <= bnd) != 0) pass |= 1u << j;
+                    // the lanes that may reach this superblock (its box broadcast from LDS)
+                    const float* sbb = sh.sbx[sbj];
+                    if (__ballot(pt_lb(sbb, x, y, z) <= bnd) != 0) pass |= 1u << j;
                 }
                 pass &= valid;
                 const int nv = __builtin_popcount(valid);
@@ -1847,13 +1868,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                             for (int c = 0; c < 6; ++c) bb[j][c] = sh.bx[sb * kSuper + h + j][c];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const float bgx = fmaxf(fmaxf(bb[j][0] - x, x - bb[j][3]), 0.0f);
-                            const float bgy = fmaxf(fmaxf(bb[j][1] - y, y - bb[j][4]), 0.0f);
-                            const float bgz = fmaxf(fmaxf(bb[j][2] - z, z - bb[j][5]), 0.0f);
-                            const float bl = __builtin_fmaf(bgz, bgz, __builtin_fmaf(bgy, bgy, bgx * bgx));
-                            nmk[h + j] = __ballot(bl * kLbShrink <= bnd);
-                        }
+                        for (int j = 0; j < 4; ++j) nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd);
                     }
                     tests += 64 * kSuper;
 #pragma unroll
