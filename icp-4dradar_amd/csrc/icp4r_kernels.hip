@@ -1205,12 +1205,39 @@ constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
+// An LDS address held in a VGPR: a wave-uniform LDS address otherwise sits in an SGPR and every
+// ds_read of a row pays its own v_mov; from a VGPR base the row's reads take immediate offsets.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(3))) T* lds_vbase(const T* p) {
+    const auto* l = (const __attribute__((address_space(3))) T*)p;
+    uint32_t a = (uint32_t)(uintptr_t)l, v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(a));
+    return (const __attribute__((address_space(3))) T*)(uintptr_t)v;
+}
+
+// Per lane: bit `lane` of the wave mask m set ? if1 : if0 (one v_cndmask on the mask itself)
+__device__ __forceinline__ uint32_t lane_select(uint64_t m, uint32_t if0, uint32_t if1) {
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+    return r;
+}
+
+// The 16 targets of LDS block b (lds_swz order) into cs: slot t sits at byte A ^ (t << 4) with
+// A = the block's base | (b & 15) << 4 — one v_xor per read instead of an xor, shift and or.
+__device__ __forceinline__ void lds_block(const v4f* tl, int b, v4f (&cs)[16]) {
+    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) v4f*)tl;
+    const uint32_t A = (base + ((uint32_t)b << 8)) | (((uint32_t)b & 15u) << 4);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) cs[t] = *(const __attribute__((address_space(3))) v4f*)(uintptr_t)(A ^ ((uint32_t)t << 4));
+}
+
 // The batched search's box tests against a bound pre-multiplied by kLbGrow (> 1 / kLbShrink with
 // margin): lb <= bnd·kLbGrow rejects only what lb·kLbShrink <= bnd rejects, one multiply fewer per
 // test.  The per-axis gap v - clamp(v, lo, hi) (a med3) has the magnitude of max(lo - v, v - hi, 0)
 // bit for bit (IEEE subtraction is sign-symmetric); a box staged as FLT_MAX (empty) gives +inf.
 constexpr float kLbGrow = 1.00002f;
-__device__ __forceinline__ float pt_lb(const float* b, float x, float y, float z) {
+template <typename P>
+__device__ __forceinline__ float pt_lb(const P b, float x, float y, float z) {
     const float gx = x - __builtin_amdgcn_fmed3f(x, b[0], b[3]);
     const float gy = y - __builtin_amdgcn_fmed3f(y, b[1], b[4]);
     const float gz = z - __builtin_amdgcn_fmed3f(z, b[2], b[5]);
@@ -1224,6 +1251,9 @@ __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float 
     return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
 }
 
+#ifndef ICP4R_SKIP_SEED
+#define ICP4R_SKIP_SEED 1  // the lane's seed block (evaluated whole up front) is never queued again
+#endif
 #ifndef ICP4R_SB_BATCH
 #define ICP4R_SB_BATCH 1  // candidate superblocks tested together per traversal step
 #endif
@@ -1231,7 +1261,7 @@ constexpr int kSbBatch = ICP4R_SB_BATCH;
 static_assert(kSbBatch >= 1 && kSbBatch <= 5, "six bits per superblock in a 32-bit pack");
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
-    float bx[kLdsTargets / kLdsLeaf][6];               // 12 KB: block boxes lo.xyz, hi.xyz (empty: FLT_MAX)
+    alignas(16) float bx[kLdsTargets / kLdsLeaf][6];   // 12 KB: block boxes lo.xyz, hi.xyz (empty: FLT_MAX)
     float sbx[kLdsTargets / kLdsLeaf / kSuper][6];     // 1.5 KB: superblock boxes
     union {
         unsigned long long best[kLdsWaves][64];        // 8 KB: best (d², index << 13 | position) key per query
@@ -1716,17 +1746,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             float bnd;  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
                         // -1 on idle lanes (never queue work, never widen the coarse bound)
             const int seed_pos0 = __builtin_amdgcn_readfirstlane(pj);
+            const int seed_blk = pj / kLdsLeaf;
+            const uint32_t lane9 = (uint32_t)lane << 9;  // ring item: query lane << 9 | block
             {
                 // seed: the previous match (first pass: the target at the same relative position)
                 // and the rest of its 16-target block, evaluated up front from LDS — tight initial
                 // bounds, so the coarse tests below already prune with them
-                const int bj = pj / kLdsLeaf, sw = bj & (kLdsLeaf - 1);
-                const v4f* tb = sh.tl + bj * kLdsLeaf;
                 NNKey lo = ~0ull;       // the smallest key seen
                 uint32_t s2 = ~0u;      // the smallest d² of every other target seen (bits)
                 v4f cs[kLdsLeaf];
-#pragma unroll
-                for (int t = 0; t < kLdsLeaf; ++t) cs[t] = tb[t ^ sw];
+                lds_block(sh.tl, pj / kLdsLeaf, cs);
                 __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) {
@@ -1773,13 +1802,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     // block b's targets sit XOR-swizzled (lds_swz): at step t lane L reads slot
                     // t ^ (b_L & 15), so lanes on different blocks spread over the 64 banks instead of
                     // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
-                    const v4f* tb = sh.tl + b * kLdsLeaf;
-                    const int sw = b & (kLdsLeaf - 1);
                     // all 16 reads issued before the first compare (the compiler otherwise keeps two
                     // in flight: 8 dependent LDS round trips per drain)
                     v4f cs[kLdsLeaf];
-#pragma unroll
-                    for (int t = 0; t < kLdsLeaf; ++t) cs[t] = tb[t ^ sw];
+                    lds_block(sh.tl, b, cs);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int t = 0; t < kLdsLeaf; ++t) {
@@ -1849,7 +1875,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 for (int j = 0; j < kSbBatch; ++j) {
                     const int sbj = (sbpack >> (6 * j)) & 63;
                     // the lanes that may reach this superblock (its box broadcast from LDS)
-                    const float* sbb = sh.sbx[sbj];
+                    const auto* sbb = lds_vbase(&sh.sbx[sbj][0]);
                     if (__ballot(pt_lb(sbb, x, y, z) <= bnd) != 0) pass |= 1u << j;
                 }
                 pass &= valid;
@@ -1859,16 +1885,26 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 for (; pass; pass &= pass - 1) {
                     const int sb = (sbpack >> (6 * __builtin_ctz(pass))) & 63;
                     ++ev_sbp;
+                    // the lane's seed block was evaluated whole up front: never queued again
+                    const int rel = seed_blk - sb * kSuper;
                     uint64_t nmk[kSuper];
 #pragma unroll
                     for (int h = 0; h < kSuper; h += 4) {
+                        // 4 rows of 24 B from a multiple of 4 rows (16-B aligned): six ds_read_b128 at
+                        // immediate offsets from one VGPR base
+                        const auto* b4 = (const __attribute__((address_space(3))) v4f*)lds_vbase(&sh.bx[sb * kSuper + h][0]);
+                        v4f r4[6];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) r4[i] = b4[i];
                         float bb[4][6];
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
 #pragma unroll
-                            for (int c = 0; c < 6; ++c) bb[j][c] = sh.bx[sb * kSuper + h + j][c];
+                            for (int c = 0; c < 6; ++c) bb[j][c] = r4[(6 * j + c) >> 2][(6 * j + c) & 3];
+                        // (two ballots: a ballot of the '&&' went through a VGPR select, 3 VALU more)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd);
+                        for (int j = 0; j < 4; ++j)
+                            nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd) & (ICP4R_SKIP_SEED ? __ballot(rel != h + j) : ~0ull);
                     }
                     tests += 64 * kSuper;
 #pragma unroll
@@ -1877,12 +1913,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         if (mask == 0) continue;
                         ++ev_blk;
                         // every lane writes (no exec-mask branch): lanes that do not need the block
-                        // write their own spare slot past the ring
-                        const bool need = (mask >> lane) & 1ull;
-                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                        const uint32_t at = need ? ((tail + rank) & (kRing - 1)) : (uint32_t)(kRing + lane);
-                        ring[at] = (uint16_t)(((uint32_t)lane << 9) | (uint32_t)(sb * kSuper + k));
+                        // write their own spare slot past the ring (the mask itself is the select)
+                        const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, tail));
+                        const uint32_t at = lane_select(mask, (uint32_t)(kRing + lane), slot & (kRing - 1));
+                        ring[at] = (uint16_t)(lane9 | (uint32_t)(sb * kSuper + k));
                         tail += (uint32_t)__builtin_popcountll(mask);
                         if (tail - head >= 64) drain(64);
                     }
