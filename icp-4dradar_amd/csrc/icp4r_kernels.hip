@@ -320,13 +320,21 @@ constexpr int kKdPer = kKdMaxN / kIdxWG;  // consecutive list positions per thre
 
 constexpr int kKdBins = 2048;             // counting-sort bins per axis (11-bit quantised coordinate)
 
+#ifndef ICP4R_FLAG32
+#define ICP4R_FLAG32 0  // kd levels: one dword per point flag instead of a byte (measured: no change)
+#endif
+#if ICP4R_FLAG32
+typedef uint32_t kd_flag_t;
+#else
+typedef uint8_t kd_flag_t;
+#endif
 struct KdShared {
     uint16_t L[3][kKdMaxN];  // per axis: the point indices, sorted by that axis inside every segment
     uint16_t q[3][kKdMaxN];  // per point: its quantised coordinates (the sort keys; segment extents)
     union {
         uint32_t hist[3][kKdBins];  // the per-axis counting sorts
         struct {
-            uint8_t left[kKdMaxN];     // per point: left of its segment's split
+            kd_flag_t left[kKdMaxN];   // per point: left of its segment's split
             uint16_t tpre[3][kIdxWG];  // per list: exclusive prefix of "left" at each thread's first position
         } p;
         float4 bbox[2 * kKdMaxN / 16];  // index_kernel: block boxes (lo, hi) for the superblock boxes
