@@ -358,9 +358,8 @@ def run_gpu(args) -> int:
         freed = [torch.cuda.Event() for _ in range(2)]
         for e in freed:
             e.record(comp)
-        barrier_sync()
-        tu = time.perf_counter()
-        for k in range(args.steps):
+
+        def upload_step(k):
             sl = k % 2
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(freed[sl])
@@ -371,6 +370,15 @@ def run_gpu(args) -> int:
             ctx.align_batch_device(slot_batches[sl], params, results.data_ptr(), stream)
             gather()
             freed[sl].record(comp)
+
+        # untimed warmup of this leg too: the copy stream's first transfers and both slots' first
+        # registrations carry one-time costs (queue creation, first touch) that are not per batch
+        for k in range(max(args.warmup, 1) * 2):
+            upload_step(k)
+        barrier_sync()
+        tu = time.perf_counter()
+        for k in range(args.steps):
+            upload_step(k)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()

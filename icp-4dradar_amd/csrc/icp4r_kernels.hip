@@ -1997,9 +1997,43 @@ __device__ __forceinline__ void load_group(float4 (&g)[8], const float* f) {
     for (int u = 0; u < 8; ++u) g[u] = *reinterpret_cast<const float4*>(f + 4 * u);
 }
 
+#ifndef ICP4R_FOLD_AHEAD
+#define ICP4R_FOLD_AHEAD 2  // groups of 32 floats in flight ahead of the adds (1 or 2)
+#endif
 template <typename TAcc>
 __device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
     int k = 0;
+    if (ICP4R_FOLD_AHEAD >= 2 && len >= 96) {
+        // three register groups in rotation, two loads in flight while a group is summed: 6.4-6.7
+        // cycles per dependent add on gfx950 vs 7.6-9.0 with one group ahead (tools/chain_bench.hip)
+        float4 a[8], b[8], c[8];
+        load_group(a, f);
+        load_group(b, f + 32);
+        for (; k + 96 <= len; k += 96) {
+            // the loads past this round re-read group 0 harmlessly when nothing follows
+            const int n1 = (k + 128 <= len) ? k + 96 : 0, n2 = (k + 160 <= len) ? k + 128 : 0;
+            load_group(c, f + k + 64);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group(acc, a);
+            load_group(a, f + n1);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group(acc, b);
+            load_group(b, f + n2);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group(acc, c);
+        }
+        // a, b hold [k, k + 32) and [k + 32, k + 64) when they exist
+        if (k + 32 <= len) {
+            add_group(acc, a);
+            k += 32;
+            if (k + 32 <= len) {
+                add_group(acc, b);
+                k += 32;
+            }
+        }
+        for (; k < len; ++k) acc = acc + (TAcc)f[k];
+        return acc;
+    }
     if (len >= 32) {
         float4 a[8], b[8];
         load_group(a, f);
@@ -2152,6 +2186,12 @@ constexpr int kFoldWG = 256;
 #ifndef ICP4R_TAIL_PER
 #define ICP4R_TAIL_PER 4  // fused test: points per thread per pipelined group
 #endif
+#ifndef ICP4R_WG_TICKS
+#define ICP4R_WG_TICKS 0
+#endif
+#ifndef ICP4R_TAIL_REV
+#define ICP4R_TAIL_REV 1  // fused test: the pair's point groups last to first
+#endif
 constexpr int kFoldWaves = kFoldWG / 64;
 constexpr int kFoldChunkP = 512;
 
@@ -2172,7 +2212,7 @@ struct FoldShared {
     SolveShared s;
 };
 
-__global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test) {
+__global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test) {
     __shared__ FoldShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     PairState& st = w.state[p];
@@ -2213,6 +2253,15 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
 
     const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
     if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
+#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/wg_ticks.py)
+    uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
+                                                              : nullptr;
+    if (wt) wt[0] = __builtin_amdgcn_s_memrealtime();
+#define WG_TICK(k) \
+    if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define WG_TICK(k)
+#endif
     // ---- pass A
     int cnt = 0;
     // Fillers issue every load of their (at most kPerA) elements before the first LDS store, so a
@@ -2272,6 +2321,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
     __syncthreads();
     if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
+    WG_TICK(1);
     if (tid == 0) {
         int total = 0;
         for (int k = 0; k < kFoldWaves; ++k) total += sh.cnt[k];
@@ -2330,9 +2380,11 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
     if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sacc;
     __syncthreads();
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
+    WG_TICK(2);
     if (tid == 0) solve_pair<kNumericsPCL>(sh.s, st, kp);
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
+    WG_TICK(3);
     if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
     if (!w.defer_xform) transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
     // The next pass's cached-neighbour test, fused (tail_test: another iteration follows and the pair
@@ -2373,11 +2425,17 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
                 UU[e] = uu[i];
             }
         };
-        load(0, v, t, U);
-        for (int i0 = 0; i0 < n; i0 += kStep) {
+        // Groups are visited last to first (ICP4R_TAIL_REV): pass B has just streamed the pair's X and
+        // nn_t front to back, so its most recently fetched lines — the ones still in the L2 / MALL —
+        // are the pair's last ones.  (The folds must run in index order; the test may run in any.)
+        const int ngrp = (n + kStep - 1) / kStep;
+        auto grp0 = [&](int g) { return (ICP4R_TAIL_REV ? ngrp - 1 - g : g) * kStep; };
+        if (ngrp > 0) load(grp0(0), v, t, U);
+        for (int g = 0; g < ngrp; ++g) {
+            const int i0 = grp0(g);
             float4 vn[kPer], tn[kPer];
             float Un[kPer];
-            if (i0 + kStep < n) load(i0 + kStep, vn, tn, Un);
+            if (g + 1 < ngrp) load(grp0(g + 1), vn, tn, Un);
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
                 const int i = i0 + e * kFoldWG + tid;
@@ -2429,6 +2487,7 @@ __global__ __launch_bounds__(kFoldWG) void fold_update_kernel(PairArgs a, WorkAr
         }
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
+    WG_TICK(4);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,0 +1,75 @@
+"""Per-workgroup phase timeline of fold_update_kernel in the C3 batch (diagnostic build).
+
+    tools/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
+    ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/wg_ticks.py [--pairs 1024]
+
+Every pair's workgroup stamps s_memrealtime (100 MHz) at its start, after pass A, pass B, the solve
+and the fused test, in its 10th update (single pair group).  Prints the launch span, the start
+spread (do all workgroups start at once?) and the phase durations' percentiles in µs.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["ICP4R_PHASE_TICKS"] = "1"
+os.environ["ICP4R_GROUPS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=1024)
+    ap.add_argument("--points", type=int, default=8192)
+    args = ap.parse_args()
+    import torch
+
+    import icp4r
+    from bench import make_shard
+
+    P, n = args.pairs, args.points
+    src_h, tgt_h = make_shard(0, P, n)
+    dev = torch.device("cuda", 0)
+    src = torch.from_numpy(src_h.reshape(-1, 4)).to(dev)
+    tgt = torch.from_numpy(tgt_h.reshape(-1, 4)).to(dev)
+    off = torch.arange(P, dtype=torch.int64, device=dev) * n
+    cnt = torch.full((P,), n, dtype=torch.int32, device=dev)
+    results = torch.zeros((P, 96), dtype=torch.uint8, device=dev)
+    ctx = icp4r.Context(0)
+    params = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
+                        tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
+                        max_src_n=n, max_tgt_n=n)
+    for _ in range(2):
+        ctx.align_batch_device(batch, params, results.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    k = 32 + 12 * P
+    buf = (C.c_uint64 * k)()
+    lib = icp4r.load()
+    lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
+    if lib.icp4r__debug_ticks(ctx._h, buf, k):
+        raise RuntimeError(lib.icp4r_last_error())
+    t = np.array(buf[32 + 4 * P:], dtype=np.int64).reshape(P, 8)[:, :5].astype(np.float64) * 0.01  # µs
+    ok = (t > 0).all(axis=1)
+    t = t[ok]
+    t0 = t[:, 0].min()
+    out = {"pairs_stamped": int(ok.sum()), "span_us": float(t[:, 4].max() - t0),
+           "start_spread_us": float(t[:, 0].max() - t0)}
+    pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 1) for q in (0, 10, 50, 90, 100)}
+    out["start"] = pct(t[:, 0] - t0)
+    for j, name in enumerate(["passA", "passB", "solve", "tail"]):
+        out[name] = pct(t[:, j + 1] - t[:, j])
+    out["total"] = pct(t[:, 4] - t[:, 0])
+    print(json.dumps(out))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
