@@ -508,7 +508,8 @@ def run_gpu(args) -> int:
     # nn_t read once per point (32 B) for the two fold passes; fused, the next pass's test adds U
     # (4 B) read and X (16) + U (4) written per tested point.  The kernel actually reads X and nn_t
     # twice more (pass B, the test tail): `bytes_with_rereads` prices those too.
-    update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches}
+    update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches,
+              "cache_hit_rate": st["cache_hits"] / max(st["cache_tested"], 1)}
     if upd_launches and upd_ms > 0:
         ub = (P * n * 32 * upd_launches + st["tested_in_update"] * 24) / upd_launches
         ub_re = (P * n * 64 * upd_launches + st["tested_in_update"] * 56) / upd_launches

@@ -425,8 +425,11 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
         }
     }
     for (int g = 0; g < groups; ++g) {
-        if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g]));
-        if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu))) return rc;
+        // the fitness pass' cached-neighbour test runs inside fitness_prep_kernel when fused
+        const int ftest = fuse && a.kp.compute_fitness ? 1 : 0;
+        if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g], ftest));
+        if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu, ftest)))
+            return rc;
         HIP_TRY(launch_finish(ag[g], wg[g], gn[g], gs[g]));
     }
     for (int g = 1; g < groups; ++g) {  // join

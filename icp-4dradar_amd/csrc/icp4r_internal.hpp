@@ -168,7 +168,7 @@ constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this m
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
                          hipStream_t st,
                          int tail_test = 0);
-hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
+hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st, int test = 0);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);
 

@@ -2168,6 +2168,126 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
     }
 }
 
+#ifndef ICP4R_TAIL_PER
+#define ICP4R_TAIL_PER 4  // fused test: points per thread per pipelined group
+#endif
+#ifndef ICP4R_WG_TICKS
+#define ICP4R_WG_TICKS 0
+#endif
+#ifndef ICP4R_TAIL_REV
+#define ICP4R_TAIL_REV 1  // fused test: the pair's point groups last to first
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// The cached-neighbour test of one pair by one workgroup of WG threads (the update's fused tail, and
+// the fitness pass inside fitness_prep_kernel): the same work as nn_cache_test_kernel for the pair —
+// X_i's new position (FROM_SRC: T·input_i, the fitness pass' final·input; else T·X_i, the deferred
+// transformCloud(T_inc)), the bounds moved by |new − old|, the test against the cached NN, a miss's
+// bit in the pair's bitmap (built in LDS: `need`, zeroed by the caller) and its search record
+// appended to the pair's miss list; the fitness pass also writes a hit's key (finish_kernel's
+// fitness reads them).  kPer points per thread per group, software-pipelined: the next group's
+// loads are issued before this group's stores, so the stores drain while the loads are in flight (a
+// load issued after a store would wait behind it on vmcnt).
+// Per point: X (.w = L) and nn_t (.w = target position | sorted position) read, U read (and the
+// input point, FROM_SRC); X and U written.  The iteration passes write no key: nothing reads one
+// before the fitness pass — the update folds recompute d² from X and nn_t, and the next search
+// seeds from the record.
+template <int WG, int kPer, bool FROM_SRC>
+__device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
+                                                uint32_t* need, int32_t* mcount, int32_t* wcnt, bool fitness) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t xs = (int64_t)p * w.x_stride;
+    float4* X = w.X + xs;
+    float* uu = w.nn_u + xs;
+    const float4* nt = w.nn_t + xs;
+    const float4* src = FROM_SRC ? a.src + a.src_off[p] : nullptr;
+    const float4* ts = w.tsort + (int64_t)p * w.t_stride;
+    NNKey* key = w.nn_key + xs;
+    constexpr int kStep = WG * kPer;
+    int hits = 0, misses = 0;
+    float4 v[kPer], t[kPer], sv[kPer];
+    float U[kPer];
+    auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float (&UU)[kPer], float4 (&ss)[kPer]) {
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const int i = min(i0 + e * WG + tid, n - 1);
+            vv[e] = X[i];
+            tt[e] = nt[i];
+            UU[e] = uu[i];
+            if (FROM_SRC) ss[e] = src[i];
+        }
+    };
+    // Groups are visited last to first (ICP4R_TAIL_REV): the update's pass B has just streamed the
+    // pair's X and nn_t front to back, so its most recently fetched lines — the ones still in the
+    // L2 / MALL — are the pair's last ones.  (The folds must run in index order; the test may run in
+    // any.)
+    const int ngrp = (n + kStep - 1) / kStep;
+    auto grp0 = [&](int g) { return (ICP4R_TAIL_REV ? ngrp - 1 - g : g) * kStep; };
+    if (ngrp > 0) load(grp0(0), v, t, U, sv);
+    for (int g = 0; g < ngrp; ++g) {
+        const int i0 = grp0(g);
+        float4 vn[kPer], tn[kPer], sn[kPer];
+        float Un[kPer];
+        if (g + 1 < ngrp) load(grp0(g + 1), vn, tn, Un, sn);
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const int i = i0 + e * WG + tid;
+            const bool valid = i < n;
+            float4 o = v[e];
+            if (FROM_SRC)
+                xform_pt(T, sv[e].x, sv[e].y, sv[e].z, o.x, o.y, o.z);  // final * input
+            else
+                xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
+            const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            o.w = Lm.x;
+            const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
+            const bool hit = valid & cache_hit(Lm.x, d2);
+            if (valid) {
+                X[i] = o;
+                uu[i] = Lm.y;
+            }
+            const int k = wave_append(valid && !hit, mcount);
+            if (hit) {
+                if (fitness) key[i] = make_key(d2, __float_as_uint(ts[nt_tpos(t[e].w)].w));
+                ++hits;
+            } else if (valid) {
+                const uint32_t sp = nt_pos(t[e].w);
+                atomicOr(&need[sp >> 5], 1u << (sp & 31));
+                put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
+                ++misses;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            v[e] = vn[e];
+            t[e] = tn[e];
+            U[e] = Un[e];
+            if (FROM_SRC) sv[e] = sn[e];
+        }
+    }
+    hits = wave_sum(hits);
+    misses = wave_sum(misses);
+    if (lane == 0) {
+        wcnt[wave] = misses;
+        count_add(w.evals, 0, (unsigned long long)hits);
+        count_add(w.evals, 2, (unsigned long long)hits);
+        count_add(w.evals, 3, (unsigned long long)(hits + misses));
+        if (!fitness) {  // ... of which in an update's tail
+            count_add(w.evals, 5, (unsigned long long)(hits + misses));
+            count_add(w.evals, 6, (unsigned long long)hits);
+        }
+    }
+    __syncthreads();
+    uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+    const int nwords = (n + 31) >> 5;
+    for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
+    if (tid == 0) {
+        int tot = 0;
+        for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
+        w.miss_cnt[p] = tot;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // fold_update_kernel (PCL numerics): one workgroup per active pair.  Bit-exact float restatement
 // of TransformationEstimationSVD (use_umeyama, Scalar = float) and calculateMSE: every sum is the
@@ -2183,17 +2303,8 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 //          a plain sum — IEEE addition is commutative, so p + acc == a*b + acc bit for bit.
 // Rejected correspondences contribute the fold's identity (-0.0f / +0), i.e. nothing.
 constexpr int kFoldWG = 256;
-#ifndef ICP4R_TAIL_PER
-#define ICP4R_TAIL_PER 4  // fused test: points per thread per pipelined group
-#endif
-#ifndef ICP4R_WG_TICKS
-#define ICP4R_WG_TICKS 0
-#endif
-#ifndef ICP4R_TAIL_REV
-#define ICP4R_TAIL_REV 1  // fused test: the pair's point groups last to first
-#endif
 constexpr int kFoldWaves = kFoldWG / 64;
-constexpr int kFoldChunkP = 512;
+constexpr int kFoldChunkP = 512;  // points per LDS chunk of the fold passes
 
 // Each fold chain's row is padded by kFoldPad floats: unpadded, rows 2 KB apart start on the same
 // LDS bank, and the 7-9 fold lanes' ds_read_b128 of one column were a 7-9-way bank conflict on every
@@ -2256,7 +2367,12 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
 #if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/wg_ticks.py)
     uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
                                                               : nullptr;
-    if (wt) wt[0] = __builtin_amdgcn_s_memrealtime();
+    if (wt) {
+        wt[0] = __builtin_amdgcn_s_memrealtime();
+        // where the fold wave (wave 0) runs: HW_ID (SIMD [5:4], CU [11:8], SH [12], SE [15:13]) and XCC_ID
+        wt[5] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
 #define WG_TICK(k) \
     if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
 #else
@@ -2267,15 +2383,20 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     // Fillers issue every load of their (at most kPerA) elements before the first LDS store, so a
     // chunk costs one global round trip, not one per element.
     constexpr int kPerA = (kFoldChunkP + (kFoldWG - 128) - 1) / (kFoldWG - 128);
-    auto fill_a = [&](int c) {  // waves 2, 3 (and 1 without the MSE chain)
-        float(*b)[kFoldRow] = sh.buf[c & 1];
+    // fill: load_a issues the loads of chunk c's records (clamped: at most kPerA per filler),
+    // store_a turns them into the chain rows of LDS buffer c & 1.  (Loading two chunks ahead in two
+    // register sets was measured: no faster — pass A at 1024 pairs is not waiting on these loads.)
+    auto load_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {
         const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
-        float4 r[kPerA][2];
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int i = base + min(tid - fill0 + e * nf, len - 1);
             rec(i, r[e][0], r[e][1]);
         }
+    };
+    auto store_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {  // waves 2, 3 (and 1 without the MSE chain)
+        float(*b)[kFoldRow] = sh.buf[c & 1];
+        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int o = tid - fill0 + e * nf;
@@ -2301,16 +2422,32 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     };
     float acc = (lane < 6) ? ident : 0.0f;
     double dacc = 0.0;
-    if (tid >= fill0 && nch > 0) fill_a(0);
-    for (int c = 0; c < nch; ++c) {
-        __syncthreads();
-        const int len = min(kFoldChunkP, n - c * kFoldChunkP);
-        if (wave == 0) {
-            if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], len, acc);
-        } else if (tid < fill0) {
-            if (lane == 0) dacc = fold_seq<double>(sh.buf[c & 1][7], len, dacc);
-        } else if (c + 1 < nch) {
-            fill_a(c + 1);
+    // The roles run as separate wave-uniform loops (the same number of barriers in each), so the
+    // fold lanes' register groups and the fillers' in-flight records are never live together.
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    if (wv == 0) {
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], min(kFoldChunkP, n - c * kFoldChunkP), acc);
+        }
+    } else if (wv * 64 < fill0) {  // the MSE chain
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (lane == 0) dacc = fold_seq<double>(sh.buf[c & 1][7], min(kFoldChunkP, n - c * kFoldChunkP), dacc);
+        }
+    } else {
+        if (nch > 0) {
+            float4 r[kPerA][2];
+            load_a(0, r);
+            store_a(0, r);
+        }
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (c + 1 < nch) {
+                float4 r[kPerA][2];
+                load_a(c + 1, r);
+                store_a(c + 1, r);
+            }
         }
     }
     // |C|: exact integer reduction of the fillers' counts
@@ -2337,15 +2474,17 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     const float ms[3] = {sh.s.mean[0], sh.s.mean[1], sh.s.mean[2]};
     const float md[3] = {sh.s.mean[3], sh.s.mean[4], sh.s.mean[5]};
     constexpr int kFillB = kFoldWG - 64, kPerB = (kFoldChunkP + kFillB - 1) / kFillB;
-    auto fill_b = [&](int c) {  // waves 1..3
-        float(*b)[kFoldRow] = sh.buf[c & 1];
+    auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
         const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
-        float4 r[kPerB][2];
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int i = base + min(tid - 64 + e * kFillB, len - 1);
             rec(i, r[e][0], r[e][1]);
         }
+    };
+    auto store_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {  // waves 1..3
+        float(*b)[kFoldRow] = sh.buf[c & 1];
+        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int o = tid - 64 + e * kFillB;
@@ -2368,13 +2507,24 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
         }
     };
     float sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b)
-    if (wave >= 1 && nch > 0) fill_b(0);
-    for (int c = 0; c < nch; ++c) {
-        __syncthreads();
-        if (wave == 0) {
+    if (wv == 0) {
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
             if (lane < 9) sacc = fold_seq<float>(sh.buf[c & 1][lane], min(kFoldChunkP, n - c * kFoldChunkP), sacc);
-        } else if (c + 1 < nch) {
-            fill_b(c + 1);
+        }
+    } else {
+        if (nch > 0) {
+            float4 r[kPerB][2];
+            load_b(0, r);
+            store_b(0, r);
+        }
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (c + 1 < nch) {
+                float4 r[kPerB][2];
+                load_b(c + 1, r);
+                store_b(c + 1, r);
+            }
         }
     }
     if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sacc;
@@ -2401,90 +2551,7 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
         __syncthreads();
-        float4* X = w.X + (int64_t)p * xs;
-        float* uu = w.nn_u + (int64_t)p * xs;
-        const float4* nt = w.nn_t + (int64_t)p * xs;
-        // kPer points per thread per group, software-pipelined: the next group's loads are issued
-        // before this group's stores, so the stores drain while the loads are in flight (a load
-        // issued after a store would wait behind it on vmcnt)
-        constexpr int kPer = ICP4R_TAIL_PER;
-        constexpr int kStep = kFoldWG * kPer;
-        int hits = 0, misses = 0;
-        // Per point: X (.w = L) and nn_t (.w = target position | sorted position) read, U read; X and U
-        // written; a miss's search record appended to the pair's miss list (sq / sm).  No key is
-        // written: nothing reads one before the fitness pass — the update folds recompute d² from X
-        // and nn_t, and the next search seeds from the record.
-        float4 v[kPer], t[kPer];
-        float U[kPer];
-        auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float (&UU)[kPer]) {
-#pragma unroll
-            for (int e = 0; e < kPer; ++e) {
-                const int i = min(i0 + e * kFoldWG + tid, n - 1);
-                vv[e] = X[i];
-                tt[e] = nt[i];
-                UU[e] = uu[i];
-            }
-        };
-        // Groups are visited last to first (ICP4R_TAIL_REV): pass B has just streamed the pair's X and
-        // nn_t front to back, so its most recently fetched lines — the ones still in the L2 / MALL —
-        // are the pair's last ones.  (The folds must run in index order; the test may run in any.)
-        const int ngrp = (n + kStep - 1) / kStep;
-        auto grp0 = [&](int g) { return (ICP4R_TAIL_REV ? ngrp - 1 - g : g) * kStep; };
-        if (ngrp > 0) load(grp0(0), v, t, U);
-        for (int g = 0; g < ngrp; ++g) {
-            const int i0 = grp0(g);
-            float4 vn[kPer], tn[kPer];
-            float Un[kPer];
-            if (g + 1 < ngrp) load(grp0(g + 1), vn, tn, Un);
-#pragma unroll
-            for (int e = 0; e < kPer; ++e) {
-                const int i = i0 + e * kFoldWG + tid;
-                const bool valid = i < n;
-                float4 o = v[e];
-                xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
-                const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
-                o.w = Lm.x;
-                const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
-                const bool hit = valid & cache_hit(Lm.x, d2);
-                if (valid) {
-                    X[i] = o;
-                    uu[i] = Lm.y;
-                }
-                const int k = wave_append(valid && !hit, &sh.mcount);
-                if (hit) {
-                    ++hits;
-                } else if (valid) {
-                    const uint32_t sp = nt_pos(t[e].w);
-                    atomicOr(&need[sp >> 5], 1u << (sp & 31));
-                    put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
-                    ++misses;
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < kPer; ++e) {
-                v[e] = vn[e];
-                t[e] = tn[e];
-                U[e] = Un[e];
-            }
-        }
-        hits = wave_sum(hits);
-        misses = wave_sum(misses);
-        if (lane == 0) {
-            sh.cnt[wave] = misses;
-            count_add(w.evals, 0, (unsigned long long)hits);
-            count_add(w.evals, 2, (unsigned long long)hits);
-            count_add(w.evals, 3, (unsigned long long)(hits + misses));
-            count_add(w.evals, 5, (unsigned long long)(hits + misses));  // ... of which in this tail
-            count_add(w.evals, 6, (unsigned long long)hits);
-        }
-        __syncthreads();
-        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
-        for (int k = tid; k < nwords; k += kFoldWG) gneed[k] = need[k];
-        if (tid == 0) {
-            int tot = 0;
-            for (int k = 0; k < kFoldWaves; ++k) tot += sh.cnt[k];
-            w.miss_cnt[p] = tot;
-        }
+        pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, &sh.mcount, sh.cnt, false);
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(4);
@@ -2543,18 +2610,34 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
 
 // ---------------------------------------------------------------------------------------------
 // fitness_prep_kernel: X := final * input (Registration::getFitnessScore / align's output).
-__global__ __launch_bounds__(256) void fitness_prep_kernel(PairArgs a, WorkArgs w) {
+// test (cached-neighbour plan): the fitness pass' cached-neighbour test runs here too, by the pair's
+// workgroup (pair_cache_test), instead of as nn_cache_test_kernel after it — one read of X, U, nn_t
+// and the input per point, no launch of its own.
+constexpr int kPrepWG = 256;
+__global__ __launch_bounds__(kPrepWG) void fitness_prep_kernel(PairArgs a, WorkArgs w, int test) {
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     const PairState& st = w.state[p];
     if (st.phase == kPhaseInvalid) return;
     __shared__ float Tf[16];
-    if (threadIdx.x < 16) Tf[threadIdx.x] = st.final_T[threadIdx.x];
-    __syncthreads();
+    __shared__ uint32_t need[kNeedWords];
+    __shared__ int32_t mcount, wcnt[kPrepWG / 64];
     const int n = a.src_n[p];
+    if (threadIdx.x < 16) Tf[threadIdx.x] = st.final_T[threadIdx.x];
+    if (test && w.nn_u) {
+        for (int k = threadIdx.x; k < (n + 31) >> 5; k += kPrepWG) need[k] = 0u;
+        if (threadIdx.x == 0) mcount = 0;
+        __syncthreads();
+        float T[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T[q] = Tf[q];
+        pair_cache_test<kPrepWG, 4, true>(a, w, p, n, T, need, &mcount, wcnt, true);
+        return;
+    }
+    __syncthreads();
     const float4* src = a.src + a.src_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
     float* uu = w.nn_u ? w.nn_u + (int64_t)p * w.x_stride : nullptr;
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = threadIdx.x; i < n; i += kPrepWG) {
         const float4 s = src[i];
         float4 o = s;
         xform_pt(Tf, s.x, s.y, s.z, o.x, o.y, o.z);
@@ -2763,8 +2846,10 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
     return hipGetLastError();
 }
 
-hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
-    hipLaunchKernelGGL(fitness_prep_kernel, dim3(npairs), dim3(256), 0, st, a, w);
+hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st, int test) {
+    if (test && (!w.nn_u || !w.need || !w.miss_cnt || !w.nn_t || !w.sq || !w.tsort || w.x_stride > kCacheMaxN))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fitness_prep_kernel, dim3(npairs), dim3(kPrepWG), 0, st, a, w, test);
     return hipGetLastError();
 }
 

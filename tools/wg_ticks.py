@@ -56,7 +56,20 @@ def main():
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
     if lib.icp4r__debug_ticks(ctx._h, buf, k):
         raise RuntimeError(lib.icp4r_last_error())
-    t = np.array(buf[32 + 4 * P:], dtype=np.int64).reshape(P, 8)[:, :5].astype(np.float64) * 0.01  # µs
+    raw = np.array(buf[32 + 4 * P:], dtype=np.uint64).reshape(P, 8)
+    hw = raw[:, 5]
+    if hw.any():  # fold-wave placement: per CU, how many fold waves share each SIMD
+        hid = (hw & 0xffffffff).astype(np.int64)
+        xcc = (hw >> np.uint64(32)).astype(np.int64) & 0xf
+        simd = (hid >> 4) & 3
+        cu = (xcc << 16) | (((hid >> 13) & 7) << 8) | (((hid >> 12) & 1) << 4) | ((hid >> 8) & 0xf)
+        per = {}
+        for c, s_ in zip(cu.tolist(), simd.tolist()):
+            per.setdefault(c, [0, 0, 0, 0])[s_] += 1
+        worst = [max(v) for v in per.values()]
+        print(json.dumps({"cus": len(per), "fold_waves_max_per_simd_hist": {str(k): worst.count(k) for k in sorted(set(worst))},
+                          "example": list(per.items())[:4]}))
+    t = raw[:, :5].astype(np.int64).astype(np.float64) * 0.01  # µs
     ok = (t > 0).all(axis=1)
     t = t[ok]
     t0 = t[:, 0].min()
