@@ -1688,36 +1688,49 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         }
         if (tk) tk1 = __builtin_amdgcn_s_memrealtime();
 
-        {  // stage the pair's sorted targets into LDS, .w = original index << 13 | position
+        // Stage the pair's sorted targets into LDS (.w = original index << 13 | position) and the block
+        // and superblock boxes, and load every lane's superblock box (isl / ish: lane l holds
+        // superblock l's box for every run of the item; nsb <= 64 on this plan).  Every load is issued
+        // before the first store: a load-store loop waited out one global round trip per target
+        // (8 per thread, ~10-20 us per item under load).
+        v4f isl, ish;
+        {
             const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
             const int nt = nsb * kSuper * kLdsLeaf;
-            for (int i = tid; i < nt; i += kLdsWG) {
-                v4f t = tsg[i];
-                t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
-                sh.tl[lds_swz(i)] = t;
-            }
+            constexpr int kPerT = kLdsTargets / kLdsWG;
+            static_assert(kLdsTargets % kLdsWG == 0, "targets per thread");
+            v4f tv[kPerT];
+#pragma unroll
+            for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * kLdsWG, nt - 1)];
             const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
             const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-            for (int b = tid; b < nsb * (kSuper + 1); b += kLdsWG) {
-                const bool blk = b < nsb * kSuper;
-                const int k = blk ? b : b - nsb * kSuper;
-                const v4f lo = blk ? tb[2 * k] : sbg[2 * k], hi = blk ? tb[2 * k + 1] : sbg[2 * k + 1];
-                const bool empty = !(lo.x <= hi.x);  // (+inf, -inf): a box no point reaches
-                float* d = blk ? sh.bx[k] : sh.sbx[k];
-                d[0] = empty ? FLT_MAX : lo.x; d[1] = empty ? FLT_MAX : lo.y; d[2] = empty ? FLT_MAX : lo.z;
-                d[3] = empty ? FLT_MAX : hi.x; d[4] = empty ? FLT_MAX : hi.y; d[5] = empty ? FLT_MAX : hi.z;
+            static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= kLdsWG, "one box per thread");
+            const int nbx = nsb * (kSuper + 1);
+            const int bq = min(tid, nbx - 1);
+            const bool blk = bq < nsb * kSuper;
+            const int kb = blk ? bq : bq - nsb * kSuper;
+            const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
+#pragma unroll
+            for (int k = 0; k < kPerT; ++k) {
+                const int i = tid + k * kLdsWG;
+                if (i < nt) {
+                    v4f t = tv[k];
+                    t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
+                    sh.tl[lds_swz(i)] = t;
+                }
             }
+            if (tid < nbx) {
+                const bool empty = !(blo.x <= bhi.x);  // (+inf, -inf): a box no point reaches
+                float* d = blk ? sh.bx[kb] : sh.sbx[kb];
+                d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
+                d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
+            }
+            const int sbl = min(lane, nsb - 1);  // (in flight across the barrier)
+            isl = sbg[2 * sbl];
+            ish = sbg[2 * sbl + 1];
         }
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
-        // lane l holds superblock l's box for every run of the item (nsb <= 64 on this plan)
-        v4f isl, ish;
-        {
-            const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-            const int sbl = min(lane, nsb - 1);
-            isl = sbv[2 * sbl];
-            ish = sbv[2 * sbl + 1];
-        }
         unsigned long long* bestl = sh.r.best[wave];
         uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
