@@ -219,7 +219,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
-        const size_t nt = 32 + 12 * (size_t)npairs;  // (see the kernels' debug tick slots)
+        const size_t nt = 32 + 20 * (size_t)npairs;  // (see the kernels' debug tick slots)
         if (ctx->ticks.cap < nt * sizeof(uint64_t)) {
             HIP_TRY(ctx->ticks.ensure(nt * sizeof(uint64_t)));
             HIP_TRY(hipMemsetAsync(ctx->ticks.p, 0, nt * sizeof(uint64_t), st));

@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kNNWG) void nn_kernel(PairArgs a, WorkArgs w, int f
 //  * larger clouds (the C5 scan-to-map target): a counting sort over 2^14 Morton cells of the
 //    bounding box (x, y: 32 cells, z: 16 — radar scans are flat); order inside a cell is whatever
 //    the LDS atomics give.
-constexpr int kIdxWG = 1024;
+constexpr int kIdxWG = 512;  // two index workgroups per CU (74 KB of LDS each): their barrier-bound levels overlap
 constexpr int kIdxWaves = kIdxWG / 64;
 constexpr int kCellBins = 1 << 14;
 constexpr int kKdMaxN = 8192;
@@ -330,7 +330,6 @@ typedef uint8_t kd_flag_t;
 #endif
 struct KdShared {
     uint16_t L[3][kKdMaxN];  // per axis: the point indices, sorted by that axis inside every segment
-    uint16_t q[3][kKdMaxN];  // per point: its quantised coordinates (the sort keys; segment extents)
     union {
         uint32_t hist[3][kKdBins];  // the per-axis counting sorts
         struct {
@@ -352,6 +351,10 @@ struct MortonShared {
     uint32_t wsum[kIdxWaves];
     float lo_s[3], sc_s[3];
 };
+
+#ifndef ICP4R_WG_TICKS
+#define ICP4R_WG_TICKS 0  // diagnostic builds: per-workgroup phase stamps (tools/wg_ticks.py)
+#endif
 
 union IndexShared {
     KdShared kd;
@@ -478,9 +481,6 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         sh.L[0][atomicAdd(&sh.u.hist[0][bx], 1u)] = (uint16_t)i;
         sh.L[1][atomicAdd(&sh.u.hist[1][by], 1u)] = (uint16_t)i;
         sh.L[2][atomicAdd(&sh.u.hist[2][bz], 1u)] = (uint16_t)i;
-        sh.q[0][i] = (uint16_t)bx;
-        sh.q[1][i] = (uint16_t)by;
-        sh.q[2][i] = (uint16_t)bz;
     }
     __syncthreads();
     if (tk) tk[1] = __builtin_amdgcn_s_memrealtime();
@@ -495,14 +495,25 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             const int h = kd_split(e - s, leaf);
             uint8_t ax = 3;
             if (h) {
+                // the segment's extent per axis from the keys of its first and last point in that axis'
+                // list, re-quantised from the (cache-resident) cloud: no per-point key array in LDS
                 float ext[3];
+                float4 pf[3], pl[3];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) ext[a] = (float)(sh.q[a][sh.L[a][e - 1]] - sh.q[a][sh.L[a][s]]) / sc[a];
+                for (int a = 0; a < 3; ++a) {
+                    pf[a] = pts(sh.L[a][s]);
+                    pl[a] = pts(sh.L[a][e - 1]);
+                }
+                ext[0] = (float)(bin(pl[0].x, 0) - bin(pf[0].x, 0)) / sc[0];
+                ext[1] = (float)(bin(pl[1].y, 1) - bin(pf[1].y, 1)) / sc[1];
+                ext[2] = (float)(bin(pl[2].z, 2) - bin(pf[2].z, 2)) / sc[2];
                 ax = ext[0] >= ext[1] && ext[0] >= ext[2] ? 0 : (ext[1] >= ext[2] ? 1 : 2);
                 any = true;
-                if (kdn && node < kKdNodes)
+                if (kdn && node < kKdNodes) {
+                    const float4 pm = pts(sh.L[ax][s + h]);
                     kdn[8 + node] = 0x80000000u | ((uint32_t)(s + h) << 13) | ((uint32_t)ax << 11) |
-                                    (uint32_t)sh.q[ax][sh.L[ax][s + h]];
+                                    (uint32_t)bin(ax == 0 ? pm.x : (ax == 1 ? pm.y : pm.z), ax);
+                }
             }
             sh.seg_mid[tid] = (uint16_t)(s + h);
             sh.seg_ax[tid] = ax;
@@ -517,17 +528,20 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             ax = sh.seg_ax[s / kKdPer];
         }
         // this thread's list entries (one 16-B LDS read per list; entries >= n are never used)
-        uint16_t v[3][kKdPer];
+        uint32_t v[3][kKdPer];  // (32-bit elements: a u16 array went to scratch)
+        static_assert(kKdPer % 8 == 0, "whole 16-B reads of the lists");
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[a][p0]);
-            const uint32_t w4[4] = {r.x, r.y, r.z, r.w};
+        for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int k = 0; k < kKdPer / 2; ++k) {
-                v[a][2 * k] = (uint16_t)(w4[k] & 0xffffu);
-                v[a][2 * k + 1] = (uint16_t)(w4[k] >> 16);
+            for (int q8 = 0; q8 < kKdPer / 8; ++q8) {
+                const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[a][p0 + 8 * q8]);
+                const uint32_t w4[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[a][8 * q8 + 2 * k] = w4[k] & 0xffffu;
+                    v[a][8 * q8 + 2 * k + 1] = w4[k] >> 16;
+                }
             }
-        }
         const int nv = min(kKdPer, n - p0);  // valid entries (<= 0: none)
         if (ax < 3)  // "left" per point, from the split axis' list
 #pragma unroll
@@ -564,10 +578,14 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 if (a == ax) continue;  // already partitioned: every entry stays where it is
-                // the wave totals before `wave` and before `sw` (16 u16 in two LDS reads)
-                const uint4 w0 = *reinterpret_cast<const uint4*>(&sh.wsum[a][0]);
-                const uint4 w1 = *reinterpret_cast<const uint4*>(&sh.wsum[a][8]);
-                const uint32_t ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+                // the wave totals before `wave` and before `sw` (u16 each, 16-B LDS reads)
+                static_assert(kIdxWaves % 8 == 0 && kIdxWaves <= 16, "wave totals in whole 16-B reads");
+                uint32_t ww[kIdxWaves / 2];
+#pragma unroll
+                for (int q8 = 0; q8 < kIdxWaves / 8; ++q8) {
+                    const uint4 r = *reinterpret_cast<const uint4*>(&sh.wsum[a][8 * q8]);
+                    ww[4 * q8] = r.x; ww[4 * q8 + 1] = r.y; ww[4 * q8 + 2] = r.z; ww[4 * q8 + 3] = r.w;
+                }
                 int bw = 0, bs = 0;
 #pragma unroll
                 for (int k = 0; k < kIdxWaves; ++k) {
@@ -579,11 +597,10 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
                 int ones = (bw + incl[a] - cnt[a]) - (bs + (int)sh.u.p.tpre[a][s / kKdPer]);
 #pragma unroll
                 for (int k = 0; k < kKdPer; ++k) {
-                    if (k >= nv) break;
                     const int f = (fb[a] >> k) & 1;
                     const int np = f ? s + ones : mid + (p0 + k - s) - ones;
                     ones += f;
-                    sh.L[a][np] = v[a][k];
+                    if (k < nv) sh.L[a][np] = (uint16_t)v[a][k];
                 }
             }
             if (p0 < mid) {
@@ -643,7 +660,7 @@ __device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArg
     return w.src_by_tgt && w.kdn && (w.kd_index & 1) && m > 0 && m <= kKdMaxN && w.t_stride <= kKdMaxN;
 }
 
-__global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
+__global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
     __shared__ IndexShared shu;
     const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * 2);
     const int p = g >> 1;
@@ -655,6 +672,14 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
     const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
     if (!is_tgt && src_by_tgt_tree(a, w, p)) return;  // src_order_kernel orders it
     if ((w.kd_index & (is_tgt ? 1 : 2)) && n <= kKdMaxN && (!is_tgt || w.t_stride <= kKdMaxN)) {
+#if ICP4R_WG_TICKS  // diagnostic build: every cloud's build start / end and XCC / CU (tools/idx_ticks.py)
+        uint64_t* it = (w.ticks && tid == 0) ? w.ticks + 32 + 12 * (int64_t)gridDim.x + 8 * (int64_t)p + (is_tgt ? 0 : 4) : nullptr;
+        if (it) {
+            it[0] = __builtin_amdgcn_s_memrealtime();
+            it[2] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                    ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+        }
+#endif
         uint64_t* tk = (w.ticks && p == 0 && is_tgt && tid == 0) ? w.ticks + 12 : nullptr;
         uint32_t* kdn = (is_tgt && w.kdn && w.src_by_tgt) ? w.kdn + (int64_t)p * kKdnStride : nullptr;
         if (kdn)
@@ -713,6 +738,10 @@ __global__ __launch_bounds__(kIdxWG) void index_kernel(PairArgs a, WorkArgs w) {
             int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
             for (int pos = tid; pos < n; pos += kIdxWG) sp[pos] = ord[pos];
         }
+#if ICP4R_WG_TICKS
+        __syncthreads();
+        if (it) it[1] = __builtin_amdgcn_s_memrealtime();
+#endif
         return;
     }
     uint32_t* bins = shu.mo.bins;
@@ -887,7 +916,7 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
 // balanced kd-tree on its own (one workgroup per chunk, the same builder): superblocks and blocks —
 // the units the search prunes with — become kd subtrees and leaves, only the chunk boundaries (every
 // 64 superblocks) stay Morton cuts.  Block and superblock boxes of the chunk are recomputed.
-__global__ __launch_bounds__(kIdxWG) void index_refine_kernel(PairArgs a, WorkArgs w) {
+__global__ __launch_bounds__(kIdxWG, 4) void index_refine_kernel(PairArgs a, WorkArgs w) {
     __shared__ IndexShared shu;
     const int c = blockIdx.x, p = blockIdx.y;
     if (w.state[p].phase == kPhaseInvalid) return;
@@ -2183,9 +2212,6 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 
 #ifndef ICP4R_TAIL_PER
 #define ICP4R_TAIL_PER 4  // fused test: points per thread per pipelined group
-#endif
-#ifndef ICP4R_WG_TICKS
-#define ICP4R_WG_TICKS 0
 #endif
 #ifndef ICP4R_TAIL_REV
 #define ICP4R_TAIL_REV 1  // fused test: the pair's point groups last to first
