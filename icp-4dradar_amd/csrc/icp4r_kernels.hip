@@ -2240,7 +2240,6 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
     float* uu = w.nn_u + xs;
     const float4* nt = w.nn_t + xs;
     const float4* src = FROM_SRC ? a.src + a.src_off[p] : nullptr;
-    const float4* ts = w.tsort + (int64_t)p * w.t_stride;
     NNKey* key = w.nn_key + xs;
     constexpr int kStep = WG * kPer;
     int hits = 0, misses = 0;
@@ -2287,7 +2286,9 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
             }
             const int k = wave_append(valid && !hit, mcount);
             if (hit) {
-                if (fitness) key[i] = make_key(d2, __float_as_uint(ts[nt_tpos(t[e].w)].w));
+                // the fitness pass' keys are read for their d² only (finish_kernel): a hit's index
+                // bits carry its NN's sorted position, no gather of the original index
+                if (fitness) key[i] = make_key(d2, nt_tpos(t[e].w));
                 ++hits;
             } else if (valid) {
                 const uint32_t sp = nt_pos(t[e].w);
