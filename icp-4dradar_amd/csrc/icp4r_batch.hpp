@@ -21,6 +21,8 @@ struct Plan {
     int leaf;     // pruned: targets per block
     int chunk_sb; // pruned (streamed): superblocks per target chunk (<= 64)
     int chunks;   // pruned (streamed): target chunks searched by separate waves (merged by atomicMin)
+    bool tile;    // pruned, not batched: nn_tile_kernel (LDS target tiles x query parts; ICP4R_NN_TILE=0: the stream)
+    int max_m;    // the plan's largest target (tile grid)
     int64_t blocks;
 };
 

@@ -106,6 +106,8 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
     pl.leaf = 0;
     pl.chunk_sb = 64;
     pl.chunks = 1;
+    pl.tile = false;
+    pl.max_m = max_m;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
     pl.q = (qcap == 1 || qcap == 2 || qcap == 4 || qcap == 8 || qcap == 16) ? qcap
                                                                              : (pl.pruned ? kDefaultPrunedQ : kDefaultQ);
@@ -137,6 +139,13 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
             pl.blocks = npairs;
             pl.chunks = 1;
             pl.cache = max_n <= kCacheMaxN && env_int("ICP4R_NN_CACHE", 1) != 0;
+        } else {
+            // single pairs / small batches: the LDS-tiled search (target tiles of 8192 x query parts)
+            pl.tile = pl.leaf == 16 && max_m < (1 << 19) && env_int("ICP4R_NN_TILE", 1) != 0;
+            if (pl.tile) {
+                pl.chunks = (max_m + 8191) / 8192;
+                pl.blocks = (int64_t)npairs * ((max_n + 1023) / 1024) * pl.chunks;
+            }
         }
         return pl;
     }
@@ -308,7 +317,9 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
         return ICP4R_OK;
     }
     HIP_TRY(hipEventRecord(ne->start, st));
-    if (pl.pruned) {
+    if (pl.tile) {
+        HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, st));
+    } else if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, pl.chunk_sb, pl.chunks, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));

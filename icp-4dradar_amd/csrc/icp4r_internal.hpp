@@ -157,6 +157,10 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 // chunk_sb: superblocks per target chunk (<= 64); chunks: grid.z (1: one wave searches every superblock)
 hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, const WorkArgs& w, int npairs,
                             int max_n, int fitness_pass, int first, hipStream_t st);
+// the pruned plan's LDS-tiled search: nn_seed_kernel, nn_tile_kernel (target tiles x query parts),
+// corr_kernel (records, when the update reads them)
+hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
+                          int first, hipStream_t st);
 // events recorded around the batched NN's stages (any may be null)
 struct NNLdsEvents {
     hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;

@@ -2018,6 +2018,171 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// nn_tile_kernel: the pruned plan's search (single pairs, small batches, targets of any size — the
+// C1 / C2 pairs and the C5 scan-to-map target) with the batched search's LDS machinery.  Grid:
+// (target tiles of kLdsTargets sorted positions, query parts of kLdsWG sorted sources, pairs).  A
+// workgroup stages its tile (targets and block / superblock boxes) in LDS and searches its queries
+// against it, one query per lane in runs of 64 consecutive sorted sources: the tile's superblocks
+// tested against the run's box at once, a reached superblock's 8 blocks tested for every lane, the
+// non-empty (lane, block) items queued per wave and drained 64 at a time (16 targets from LDS per
+// lane).  A query starts from its current key — nn_seed_kernel's seed, or another tile's minimum read
+// at the start (any key read is an upper bound: keys only fall) — and merges its tile minimum into it
+// with a u64 atomicMin (exact: the lexicographic (d², index) minimum whatever the order of tiles).
+// corr_kernel writes the correspondence records afterwards.  Replaces the scalar-cache stream of
+// nn_pruned_kernel, whose every block visit evaluated the block for all 64 lanes of a wave.
+struct TileShared {
+    v4f tl[kLdsTargets];                              // 128 KB: the tile's targets (.w = index << 13 | position)
+    alignas(16) float bx[kLdsTargets / kLdsLeaf][6];  // block boxes (empty: FLT_MAX)
+    float sbx[kLdsTargets / kLdsLeaf / kSuper][6];    // superblock boxes
+    unsigned long long best[kLdsWaves][64];           // per query: best local key
+    uint16_t items[kLdsWaves][kRing + 64];            // (query lane << 9) | block; + a spare slot per lane
+};
+constexpr int kTileMaxM = 1 << (32 - kLdsPosBits);  // target indices that fit the local key
+
+__global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w, int fitness_pass) {
+    __shared__ TileShared sh;
+    const int tile = blockIdx.x, part = blockIdx.y, p = blockIdx.z;
+    const int phase = uload(&w.state[p].phase);
+    if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
+    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    const int t0 = tile * kLdsTargets, q0 = part * kLdsWG;
+    if (t0 >= m || q0 >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tm = min(kLdsTargets, m - t0);
+    const int nb = (tm + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
+    const int64_t xs0 = (int64_t)p * w.x_stride;
+    unsigned long long evals = 0, tests = 0;
+
+    // Stage the tile (whole superblocks: tsort is padded to them), every load before the first store.
+    v4f isl, ish;
+    {
+        const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride + t0);
+        const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride) + 2 * (t0 / kLdsLeaf);
+        const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride) + 2 * (t0 / (kLdsLeaf * kSuper));
+        const int nt = nsb * kSuper * kLdsLeaf;
+        constexpr int kPerT = kLdsTargets / kLdsWG;
+        v4f tv[kPerT];
+#pragma unroll
+        for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * kLdsWG, nt - 1)];
+        const int nbx = nsb * (kSuper + 1);
+        const int bq = min(tid, nbx - 1);
+        const bool blk = bq < nsb * kSuper;
+        const int kb = blk ? bq : bq - nsb * kSuper;
+        const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
+#pragma unroll
+        for (int k = 0; k < kPerT; ++k) {
+            const int i = tid + k * kLdsWG;
+            if (i < nt) {
+                v4f t = tv[k];
+                t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
+                sh.tl[lds_swz(i)] = t;
+            }
+        }
+        if (tid < nbx) {
+            const bool empty = !(blo.x <= bhi.x);
+            float* d = blk ? sh.bx[kb] : sh.sbx[kb];
+            d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
+            d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
+        }
+        const int sbl = min(lane, nsb - 1);
+        isl = sbg[2 * sbl];
+        ish = sbg[2 * sbl + 1];
+    }
+    __syncthreads();
+    const int r0 = q0 + wave * 64;  // this wave's run: sorted sources [r0, r0 + 64)
+    if (r0 >= n) return;            // (no barrier follows)
+    unsigned long long* bestl = sh.best[wave];
+    uint16_t* ring = sh.items[wave];
+    NNKey* key = w.nn_key + xs0;
+    const bool live = r0 + lane < n;
+    const int o = w.sperm[xs0 + (live ? r0 + lane : r0)];  // idle lanes shadow the run's first query
+    const float4 v = w.X[xs0 + o];
+    const NNKey k0 = key[o];
+    const float x = v.x, y = v.y, z = v.z;
+    // the current key in the tile's encoding, ranked after every real target of the same (d², index)
+    const NNKey init = make_key(key_d2(k0), ((uint32_t)key_idx(k0) << kLdsPosBits) | ((1u << kLdsPosBits) - 1));
+    bestl[lane] = init;
+    float bnd = live ? key_d2(k0) * kLbGrow : -1.0f;
+    float qlo[3] = {x, y, z}, qhi[3] = {x, y, z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        qlo[k] = wave_minf(qlo[k]);
+        qhi[k] = wave_maxf(qhi[k]);
+    }
+    const float qmax = wave_maxf(bnd);
+    const uint32_t lane9 = (uint32_t)lane << 9;
+    uint32_t head = 0, tail = 0;
+    auto drain = [&](uint32_t cnt) {
+        const bool act = (uint32_t)lane < cnt;
+        const uint32_t it = ring[(head + lane) & (kRing - 1)];
+        const int owner = act ? (int)(it >> 9) : 0;
+        const int b = act ? (int)(it & 0x1ffu) : 0;
+        const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
+        if (act) {
+            NNKey k1 = ~0ull;
+            v4f cs[kLdsLeaf];
+            lds_block(sh.tl, b, cs);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < kLdsLeaf; ++t) {
+                const v4f c = cs[t];
+                const NNKey kn = make_key(l2_simple(qx, qy, qz, c.x, c.y, c.z), __float_as_uint(c.w));
+                k1 = kn < k1 ? kn : k1;
+            }
+            atomicMin(&bestl[owner], k1);
+        }
+        head += cnt;
+        evals += (unsigned long long)cnt * kLdsLeaf;
+        bnd = live ? key_d2(bestl[lane]) * kLbGrow : -1.0f;
+    };
+    // the tile's superblocks some query may reach, visited in order (the run's neighbourhood is
+    // unknown here: no seed inside the tile)
+    uint64_t cm = __ballot(lane < nsb && box_lb(isl, ish, qlo, qhi) <= qmax);
+    tests += nsb;
+    for (; cm; cm &= cm - 1) {
+        const int sb = __builtin_ctzll(cm);
+        const auto* sbb = lds_vbase(&sh.sbx[sb][0]);
+        tests += 64;
+        if (__ballot(pt_lb(sbb, x, y, z) <= bnd) == 0) continue;
+        uint64_t nmk[kSuper];
+#pragma unroll
+        for (int h = 0; h < kSuper; h += 4) {
+            const auto* b4 = (const __attribute__((address_space(3))) v4f*)lds_vbase(&sh.bx[sb * kSuper + h][0]);
+            v4f r4[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) r4[i] = b4[i];
+            float bb[4][6];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) bb[j][c] = r4[(6 * j + c) >> 2][(6 * j + c) & 3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd);
+        }
+        tests += 64 * kSuper;
+#pragma unroll
+        for (int k = 0; k < kSuper; ++k) {
+            const uint64_t mask = nmk[k];
+            if (mask == 0) continue;
+            const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, tail));
+            const uint32_t at = lane_select(mask, (uint32_t)(kRing + lane), slot & (kRing - 1));
+            ring[at] = (uint16_t)(lane9 | (uint32_t)(sb * kSuper + k));
+            tail += (uint32_t)__builtin_popcountll(mask);
+            if (tail - head >= 64) drain(64);
+        }
+    }
+    if (tail != head) drain(tail - head);
+    const NNKey kb = bestl[lane];
+    if (live && kb < init) atomicMin(&key[o], make_key(key_d2(kb), lk_idx(kb)));
+    if (lane == 0) {
+        count_add(w.evals, 0, evals);
+        count_add(w.evals, 1, tests);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sequential folds over an LDS chunk, one lane per chain: acc = acc + f[k] for k in [0, len), in
 // that order — exactly the reference loop.  Groups of 32 floats are read 32 elements ahead in two
 // explicit register sets (a/b ping-pong) so the chain runs at the dependent-add latency instead of
@@ -2839,6 +3004,18 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
     else
         hipLaunchKernelGGL((nn_lds_kernel<false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
     if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
+                          int first, hipStream_t st) {
+    if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass, first);
+    const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + kLdsWG - 1) / kLdsWG, npairs);
+    hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass);
+    if (w.corr != nullptr && !fitness_pass)  // records from the merged keys
+        hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();
 }
 

@@ -74,7 +74,7 @@ def test_struct_layouts():
     assert icp4r.Result.fitness.offset == 64
 
 
-def test_plan_geometry():
+def test_plan_geometry(monkeypatch):
     import icp4r
 
     big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
@@ -82,10 +82,16 @@ def test_plan_geometry():
     assert big["cache"] and not icp4r.plan(1024, 16385, 8192)["cache"]  # cached-neighbour test: n <= 16384
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
-    single = icp4r.plan(1, 8192, 8192)  # C2: streamed kernel, one query per lane, the target in 4 chunks
+    single = icp4r.plan(1, 8192, 8192)  # C2: LDS-tiled search, one target tile x 8 query parts of 1024
+    assert single["pruned"] and not single["lds"] and single["nn_blocks"] == 8
+    c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 8 query parts
+    assert c5["pruned"] and not c5["lds"] and c5["nn_blocks"] == 8 * 9
+    monkeypatch.setenv("ICP4R_NN_TILE", "0")  # the streamed kernel instead
+    single = icp4r.plan(1, 8192, 8192)  # one query per lane, the target in 4 chunks
     assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32 * 4
-    c5 = icp4r.plan(1, 8192, 65540)  # C5: 513 superblocks in 9 chunks of <= 64
+    c5 = icp4r.plan(1, 8192, 65540)  # 513 superblocks in 9 chunks of <= 64
     assert c5["pruned"] and not c5["lds"] and c5["nn_blocks"] == 32 * 9
+    monkeypatch.delenv("ICP4R_NN_TILE")
     brute = icp4r.plan(1024, 8192, 8192, icp4r.NN_BRUTE)
     assert not brute["pruned"] and brute["q"] == 4 and brute["splits"] == 1
     bsingle = icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)

@@ -176,16 +176,19 @@ def test_target_split_equals_unsplit(gpu_ctx):
         assert (res[k]["T"] == np.array(r.T, np.float32)).all()
 
 
-@pytest.mark.parametrize("lds,cache", [("0", "1"), ("1", "0"), ("1", "1")])
-@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map"])
-def test_nn_modes_identical(gpu_ctx, case, lds, cache, monkeypatch):
-    """Pruned (streamed, or with the target set in LDS and per-query work lists, with or without the
-    cached-neighbour test), brute-force and packed searches produce bit-identical registrations (T,
-    fitness, iterations, aligned cloud) — the pruned index changes only which targets are evaluated."""
+@pytest.mark.parametrize("lds,cache,tile", [("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")])
+@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map"])
+def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
+    """Pruned (LDS target tiles x query parts, the scalar-cache stream, or with the target set in LDS
+    and per-query work lists, with or without the cached-neighbour test), brute-force and packed
+    searches produce bit-identical registrations (T, fitness, iterations, aligned cloud) — the pruned
+    index changes only which targets are evaluated.  dup_map: every target twice, the copies in
+    different tiles of a > 8192-point target, so ties resolve across tiles (lowest index)."""
     import icp4r
 
     monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
     monkeypatch.setenv("ICP4R_NN_CACHE", cache)
+    monkeypatch.setenv("ICP4R_NN_TILE", tile)  # 0: the scalar-cache stream for the unbatched plan
     guess = None
     if case == "c2":
         pairs = [_pair(310, 8192)]
@@ -205,11 +208,14 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, monkeypatch):
         sr = t.copy()
         sr[:, :3] += np.float32(0.25)
         pairs = [(sr, t)]
-    else:
+    elif case == "map":
         from icp4r import synth
 
         mp = synth.make_map_pair(1)
         pairs = [(mp.src_xyzi()[:4096], mp.tgt_xyzi())]
+    else:
+        sp, tp = _pair(340, 3000, 6000)
+        pairs = [(sp, np.concatenate([tp, tp]))]
     p = dict(max_iterations=12, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     if len(pairs) == 1:
         s, t = pairs[0]
