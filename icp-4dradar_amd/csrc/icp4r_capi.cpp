@@ -386,7 +386,11 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     int rc;
     const bool pcl = a.kp.numerics == kNumericsPCL;
     if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl, st, w))) return rc;
-    w.src_by_tgt = pl.pruned ? (env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0) : 0;
+    // sources ordered by their target's kd tree (src_order_kernel) on the batched plan, where its
+    // better first-pass seeds and one kd build per pair pay (C3 +2.9 %); a single pair's extra launch
+    // does not (C1 0.75 -> 0.80 ms), so the unbatched plans build the source's own tree
+    w.src_by_tgt = (pl.pruned && pl.lds) ? (env_int("ICP4R_SRC_ORDER", 1) != 0 ? 1 : 0)
+                                         : (pl.pruned && env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0);
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));

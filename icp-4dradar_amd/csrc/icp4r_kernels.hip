@@ -662,9 +662,11 @@ __device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArg
 
 __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
     __shared__ IndexShared shu;
-    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * 2);
-    const int p = g >> 1;
-    const bool is_tgt = (g & 1) == 0;
+    // grid (pairs, 2): target and source of every pair; (pairs, 1): targets only (every source is
+    // ordered by src_order_kernel — launched alone, the targets spread over every CU)
+    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int p = gridDim.y == 2 ? g >> 1 : g;
+    const bool is_tgt = gridDim.y == 2 ? (g & 1) == 0 : true;
     if (w.state[p].phase == kPhaseInvalid) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
@@ -838,7 +840,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
 // source order (sperm): consecutive queries fall in the same or neighbouring target leaves, so
 // query runs stay compact, and the leaf's first target seeds the query's first search (nn_key with
 // d² = +inf, read by the first pass).  It replaces the source's own kd build (index_kernel).
-constexpr int kSoWG = 256;
+constexpr int kSoWG = 512;
 
 __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w) {
     __shared__ uint32_t nodes[kKdNodes];
@@ -850,33 +852,78 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     const int n = a.src_n[p], m = a.tgt_n[p];
     if (n <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if ICP4R_WG_TICKS  // diagnostic build: this pair's source-order start / end (the index stamps' source slots)
+    uint64_t* it = (w.ticks && tid == 0) ? w.ticks + 32 + 12 * (int64_t)gridDim.x + 8 * (int64_t)p + 4 : nullptr;
+    if (it) {
+        it[0] = __builtin_amdgcn_s_memrealtime();
+        it[2] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
+#endif
     const int B = w.leaf;
     const int nb = (m + B - 1) / B;  // <= kKdMaxN / 16
     const uint32_t* kd = w.kdn + (int64_t)p * kKdnStride;
-    for (int k = tid; k < kKdNodes; k += kSoWG) nodes[k] = kd[8 + k];
+    {
+        uint32_t nv[kKdNodes / kSoWG];  // every load before the first store
+#pragma unroll
+        for (int k = 0; k < kKdNodes / kSoWG; ++k) nv[k] = kd[8 + tid + k * kSoWG];
+#pragma unroll
+        for (int k = 0; k < kKdNodes / kSoWG; ++k) nodes[tid + k * kSoWG] = nv[k];
+    }
     if (tid < 6) qz[tid] = __uint_as_float(kd[tid]);
     for (int b = tid; b < kKdMaxN / 16; b += kSoWG) bins[b] = 0u;
     __syncthreads();
     const float lo[3] = {qz[0], qz[1], qz[2]}, sc[3] = {qz[3], qz[4], qz[5]};
     const float4* src = a.src + a.src_off[p];
-    auto leaf_of = [&](const float4 v) {
-        const int k0 = min(kKdBins - 1, max(0, (int)((v.x - lo[0]) * sc[0])));
-        const int k1 = min(kKdBins - 1, max(0, (int)((v.y - lo[1]) * sc[1])));
-        const int k2 = min(kKdBins - 1, max(0, (int)((v.z - lo[2]) * sc[2])));
-        int node = 1, s = 0;
-        while (node < kKdNodes) {
-            const uint32_t nd = nodes[node];
-            if (!(nd >> 31)) break;
-            const int ax = (int)((nd >> 11) & 3u), thr = (int)(nd & 2047u);
-            const int k = ax == 0 ? k0 : (ax == 1 ? k1 : k2);
-            const bool right = k >= thr;
-            s = right ? (int)((nd >> 13) & 0x3fffu) : s;
-            node = 2 * node + (right ? 1 : 0);
+    // Every thread's points (i = tid + e * kSoWG) descend in groups of kSoGrp: their loads all in
+    // flight together and the descents interleaved level by level (independent LDS chains) — a
+    // point-at-a-time loop had waited out a global round trip and 9 dependent LDS reads per point.
+    // The leaves stay in registers (two per dword) for the scatter.
+    constexpr int kSoPer = kKdMaxN / kSoWG, kSoGrp = 8;
+    static_assert(kSoPer % kSoGrp == 0 && kSoPer % 2 == 0, "point groups");
+    uint32_t lv[kSoPer / 2];
+#pragma unroll
+    for (int g = 0; g < kSoPer; g += kSoGrp) {
+        float4 v[kSoGrp];
+#pragma unroll
+        for (int e = 0; e < kSoGrp; ++e) v[e] = src[min(tid + (g + e) * kSoWG, n - 1)];
+        int key3[kSoGrp][3], node[kSoGrp], sp[kSoGrp];
+#pragma unroll
+        for (int e = 0; e < kSoGrp; ++e) {
+            key3[e][0] = min(kKdBins - 1, max(0, (int)((v[e].x - lo[0]) * sc[0])));
+            key3[e][1] = min(kKdBins - 1, max(0, (int)((v[e].y - lo[1]) * sc[1])));
+            key3[e][2] = min(kKdBins - 1, max(0, (int)((v[e].z - lo[2]) * sc[2])));
+            node[e] = 1;
+            sp[e] = 0;
         }
-        return min(s / B, nb - 1);
-    };
-    for (int i = tid; i < n; i += kSoWG) atomicAdd(&bins[leaf_of(src[i])], 1u);
+        for (int lvl = 0; lvl < 11; ++lvl) {  // heap ids < kKdNodes = 2^11
+            uint32_t nd[kSoGrp];  // the group's node reads all issued, then branch-free steps
+#pragma unroll
+            for (int e = 0; e < kSoGrp; ++e) nd[e] = nodes[min(node[e], kKdNodes - 1)];
+#pragma unroll
+            for (int e = 0; e < kSoGrp; ++e) {
+                const bool inner = node[e] < kKdNodes && (nd[e] >> 31);
+                const uint32_t ax = (nd[e] >> 11) & 3u;
+                const int k = ax == 0u ? key3[e][0] : (ax == 1u ? key3[e][1] : key3[e][2]);
+                const bool right = k >= (int)(nd[e] & 2047u);
+                sp[e] = (inner && right) ? (int)((nd[e] >> 13) & 0x3fffu) : sp[e];
+                node[e] = inner ? 2 * node[e] + (right ? 1 : 0) : kKdNodes;  // a leaf: done
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kSoGrp; ++e) {
+            const uint32_t leaf = (uint32_t)min(sp[e] / B, nb - 1);
+            if (tid + (g + e) * kSoWG < n) atomicAdd(&bins[leaf], 1u);
+            if ((e & 1) == 0)
+                lv[(g + e) >> 1] = leaf;
+            else
+                lv[(g + e) >> 1] |= leaf << 16;
+        }
+    }
     __syncthreads();
+#if ICP4R_WG_TICKS
+    if (it) it[3] = __builtin_amdgcn_s_memrealtime();
+#endif
     {  // exclusive scan of the nb bins: thread t owns bins [2t, 2t + 2)
         constexpr int per = kKdMaxN / 16 / kSoWG;
         uint32_t loc[per], run = 0;
@@ -900,15 +947,31 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
         for (int k = 0; k < per; ++k) bins[tid * per + k] = base + incl - run + loc[k];
     }
     __syncthreads();
-    int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
+    int32_t* spm = w.sperm + (int64_t)p * w.x_stride;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const float4* ts = w.tsort + (int64_t)p * w.t_stride;
-    for (int i = tid; i < n; i += kSoWG) {
-        const int b = leaf_of(src[i]);
-        const uint32_t pos = atomicAdd(&bins[b], 1u);
-        sp[pos] = i;
-        key[i] = make_key(INFINITY, __float_as_uint(ts[b * B].w));  // first-pass seed: the leaf's first target
+#pragma unroll
+    for (int g = 0; g < kSoPer; g += kSoGrp) {
+        float sw[kSoGrp];  // the leaves' first targets' index bits (first-pass seeds), loads in flight together
+#pragma unroll
+        for (int e = 0; e < kSoGrp; ++e) {
+            const uint32_t leaf = (lv[(g + e) >> 1] >> (16 * ((g + e) & 1))) & 0xffffu;
+            sw[e] = ts[leaf * B].w;
+        }
+#pragma unroll
+        for (int e = 0; e < kSoGrp; ++e) {
+            const int i = tid + (g + e) * kSoWG;
+            if (i >= n) continue;
+            const uint32_t leaf = (lv[(g + e) >> 1] >> (16 * ((g + e) & 1))) & 0xffffu;
+            const uint32_t pos = atomicAdd(&bins[leaf], 1u);
+            spm[pos] = i;
+            key[i] = make_key(INFINITY, __float_as_uint(sw[e]));  // first-pass seed: the leaf's first target
+        }
     }
+#if ICP4R_WG_TICKS
+    __syncthreads();
+    if (it) it[1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // index_refine_kernel: targets too large for the in-LDS kd build (the C5 scan-to-map submap) are
@@ -2972,7 +3035,10 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 }
 
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
-    hipLaunchKernelGGL(index_kernel, dim3(npairs, 2), dim3(kIdxWG), 0, st, a, w);
+    // every source by the target's tree: launch the target builds alone (a grid with idle source
+    // workgroups left half the CUs without a build)
+    const bool tgt_only = w.src_by_tgt && w.kdn && (w.kd_index & 1) && w.t_stride <= kKdMaxN;
+    hipLaunchKernelGGL(index_kernel, dim3(npairs, tgt_only ? 1 : 2), dim3(kIdxWG), 0, st, a, w);
     if (w.src_by_tgt && w.kdn)
         hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);
     if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))

@@ -297,7 +297,7 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
 
 @pytest.mark.parametrize("npairs", [1, 300])
 def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
-    """Sources ordered by descending their target's kd tree (src_order_kernel, default) or by their
+    """Sources ordered by descending their target's kd tree (src_order_kernel; the batched plan's default) or by their
     own kd tree (ICP4R_SRC_ORDER=0): the order and the first-pass seeds change, the registrations do
     not — bit-identical on the single-pair pruned kernel and the batched LDS search, ragged shapes,
     a lattice (ties) and targets over 8192 points (their sources keep the own-tree path)."""

@@ -56,22 +56,27 @@ def main():
     if lib.icp4r__debug_ticks(ctx._h, buf, k):
         raise RuntimeError(lib.icp4r_last_error())
     raw = np.array(buf[32 + 12 * P:], dtype=np.uint64).reshape(P, 2, 4)  # [pair][tgt, src][start, end, hw, -]
-    t0 = raw[:, :, 0].astype(np.int64).min()
-    st = (raw[:, :, 0].astype(np.int64) - t0) * 0.01
+    have = raw[:, :, 0] > 0  # (clouds built elsewhere, e.g. sources ordered by src_order_kernel, have no stamps)
+    t0 = raw[:, :, 0][have].astype(np.int64).min()
+    st = ((raw[:, :, 0].astype(np.int64) - t0) * 0.01)[have]
     du = (raw[:, :, 1].astype(np.int64) - raw[:, :, 0].astype(np.int64)) * 0.01
-    hw = raw[:, :, 2]
+    hw = raw[:, :, 2][have]
     hid = (hw & np.uint64(0xffffffff)).astype(np.int64)
     xcc = (hw >> np.uint64(32)).astype(np.int64) & 0xf
     cu = (xcc << 16) | (((hid >> 13) & 7) << 8) | (((hid >> 12) & 1) << 4) | ((hid >> 8) & 0xf)
     pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 1) for q in (0, 10, 50, 90, 100)}
     per_cu = {}
-    for c in cu.ravel().tolist():
+    for c in cu.tolist():
         per_cu[c] = per_cu.get(c, 0) + 1
     cnts = list(per_cu.values())
-    out = {"span_us": round(float((raw[:, :, 1].astype(np.int64).max() - t0) * 0.01), 1),
-           "target_build_us": pct(du[:, 0]), "source_build_us": pct(du[:, 1]),
-           "start_us": pct(st.ravel()), "cus": len(per_cu),
+    out = {"span_us": round(float((raw[:, :, 1][have].astype(np.int64).max() - t0) * 0.01), 1),
+           "target_build_us": pct(du[:, 0][have[:, 0]]),
+           "source_build_us": pct(du[:, 1][have[:, 1]]) if have[:, 1].any() else None,
+           "start_us": pct(st), "cus": len(per_cu),
            "builds_per_cu": {str(v): cnts.count(v) for v in sorted(set(cnts))}}
+    ph = (raw[:, 1, 3].astype(np.int64) - raw[:, 1, 0].astype(np.int64)) * 0.01  # src_order: descent + histogram
+    if have[:, 1].any() and (raw[:, 1, 3] > 0).any():
+        out["src_order_phase1_us"] = pct(ph[raw[:, 1, 3] > 0])
     print(json.dumps(out))
     ctx.close()
 
