@@ -1331,6 +1331,30 @@ __device__ __forceinline__ void lds_block(const v4f* tl, int b, v4f (&cs)[16]) {
     for (int t = 0; t < 16; ++t) cs[t] = *(const __attribute__((address_space(3))) v4f*)(uintptr_t)(A ^ ((uint32_t)t << 4));
 }
 
+// An LDS target slot is {key, x, y, z}: the key (original index << 13 | LDS position) first, so a
+// drain's (d², key) pair forms in the aligned register pair of the slot's first two words (d²
+// overwrites x, dead once dx is formed) — with the key last, every evaluation paid a v_mov to pair
+// them (a 64-bit VGPR operand must start on an even register).
+#ifndef ICP4R_TL_KEYFIRST
+#define ICP4R_TL_KEYFIRST 1
+#endif
+__device__ __forceinline__ v4f tl_slot(const v4f t, uint32_t k) {
+    return ICP4R_TL_KEYFIRST ? (v4f){__uint_as_float(k), t.x, t.y, t.z} : (v4f){t.x, t.y, t.z, __uint_as_float(k)};
+}
+__device__ __forceinline__ float tl_x(const v4f c) { return ICP4R_TL_KEYFIRST ? c.y : c.x; }
+__device__ __forceinline__ float tl_y(const v4f c) { return ICP4R_TL_KEYFIRST ? c.z : c.y; }
+__device__ __forceinline__ float tl_z(const v4f c) { return ICP4R_TL_KEYFIRST ? c.w : c.z; }
+__device__ __forceinline__ uint32_t tl_key(const v4f c) { return __float_as_uint(ICP4R_TL_KEYFIRST ? c.x : c.w); }
+
+// The second-smallest d² of a block after one more evaluation: s2 ≥ b (the current best's d²)
+// holds throughout, so min(s2, max(b, d)) — "d below the best: the old best; else min(s2, d)" —
+// is the median of the three (one v_med3_u32; d² bits order as unsigned: never negative).
+__device__ __forceinline__ uint32_t second_d2(uint32_t b, uint32_t d, uint32_t s2) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(d), "v"(s2));
+    return r;
+}
+
 // The batched search's box tests against a bound pre-multiplied by kLbGrow (> 1 / kLbShrink with
 // margin): lb <= bnd·kLbGrow rejects only what lb·kLbShrink <= bnd rejects, one multiply fewer per
 // test.  The per-axis gap v - clamp(v, lo, hi) (a med3) has the magnitude of max(lo - v, v - hi, 0)
@@ -1806,9 +1830,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             for (int k = 0; k < kPerT; ++k) {
                 const int i = tid + k * kLdsWG;
                 if (i < nt) {
-                    v4f t = tv[k];
-                    t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
-                    sh.tl[lds_swz(i)] = t;
+                    sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
                 }
             }
             if (tid < nbx) {
@@ -1873,9 +1895,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                 for (int t = 0; t < kLdsLeaf; ++t) {
                     const v4f c = cs[t];
-                    const float d2 = l2_simple(x, y, z, c.x, c.y, c.z);
-                    const NNKey kn = make_key(d2, __float_as_uint(c.w));
-                    if (CACHE) s2 = kn < lo ? (uint32_t)(lo >> 32) : min(s2, __float_as_uint(d2));
+                    const float d2 = l2_simple(x, y, z, tl_x(c), tl_y(c), tl_z(c));
+                    const NNKey kn = make_key(d2, tl_key(c));
+                    if (CACHE) s2 = second_d2((uint32_t)(lo >> 32), __float_as_uint(d2), s2);
                     lo = kn < lo ? kn : lo;
                 }
                 bestl[lane] = lo;
@@ -1911,7 +1933,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                 const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
                 if (act) {
                     NNKey k1 = ~0ull;
-                    uint32_t s2 = 0x7f800000u;  // second-smallest d² of the block (bits; +inf)
+                    uint32_t s2 = ~0u;  // second-smallest d² of the block (bits; >= k1's throughout)
                     // block b's targets sit XOR-swizzled (lds_swz): at step t lane L reads slot
                     // t ^ (b_L & 15), so lanes on different blocks spread over the 64 banks instead of
                     // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
@@ -1923,9 +1945,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
 #pragma unroll
                     for (int t = 0; t < kLdsLeaf; ++t) {
                         const v4f c = cs[t];
-                        const float d2 = l2_simple(qx, qy, qz, c.x, c.y, c.z);
-                        const NNKey kn = make_key(d2, __float_as_uint(c.w));
-                        if (CACHE) s2 = kn < k1 ? (uint32_t)(k1 >> 32) : min(s2, __float_as_uint(d2));
+                        const float d2 = l2_simple(qx, qy, qz, tl_x(c), tl_y(c), tl_z(c));
+                        const NNKey kn = make_key(d2, tl_key(c));
+                        if (CACHE) s2 = second_d2((uint32_t)(k1 >> 32), __float_as_uint(d2), s2);
                         k1 = kn < k1 ? kn : k1;
                     }
                     if (CACHE) {
@@ -2049,9 +2071,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     const float2 lu = lu_from_sec(__uint_as_float(secl[lane]));
                     X[orig] = make_float4(x, y, z, lu.x);  // .w = L
                     w.nn_u[xs0 + orig] = lu.y;
-                    w.nn_t[xs0 + orig] = make_float4(t.x, t.y, t.z, nt_pack((int)tpos, spos));
+                    w.nn_t[xs0 + orig] = make_float4(tl_x(t), tl_y(t), tl_z(t), nt_pack((int)tpos, spos));
                 } else if (corr) {
-                    write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(t.x, t.y, t.z, 0.f));
+                    write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(tl_x(t), tl_y(t), tl_z(t), 0.f));
                 }
             }
             const uint64_t ck3 = __builtin_readcyclecounter();
@@ -2137,9 +2159,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
         for (int k = 0; k < kPerT; ++k) {
             const int i = tid + k * kLdsWG;
             if (i < nt) {
-                v4f t = tv[k];
-                t.w = __uint_as_float((__float_as_uint(t.w) << kLdsPosBits) | (uint32_t)i);
-                sh.tl[lds_swz(i)] = t;
+                sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
             }
         }
         if (tid < nbx) {
@@ -2190,7 +2210,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
 #pragma unroll
             for (int t = 0; t < kLdsLeaf; ++t) {
                 const v4f c = cs[t];
-                const NNKey kn = make_key(l2_simple(qx, qy, qz, c.x, c.y, c.z), __float_as_uint(c.w));
+                const NNKey kn = make_key(l2_simple(qx, qy, qz, tl_x(c), tl_y(c), tl_z(c)), tl_key(c));
                 k1 = kn < k1 ? kn : k1;
             }
             atomicMin(&bestl[owner], k1);
