@@ -17,7 +17,8 @@ for r in $(seq 1 "$R"); do
 import json, sys
 r = json.loads(sys.argv[2])
 print(f"{sys.argv[1]:36s} value {r['value']:9.0f}  search {r['roofline']['avg_launch_ms']*1e3:6.1f} us  "
-      f"update {r['update_kernel']['avg_launch_ms']*1e3:6.1f} us  batch {r['batch_device_ms']:6.3f} ms  parity {r['parity_ok']}", flush=True)
+      f"update {r['update_kernel']['avg_launch_ms']*1e3:6.1f} us  batch {r['batch_device_ms']:6.3f} ms  "
+      f"hit {r['update_kernel'].get('cache_hit_rate') or 0:.4f}  parity {r['parity_ok']}", flush=True)
 PY
     done
 done
