@@ -391,6 +391,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // does not (C1 0.75 -> 0.80 ms), so the unbatched plans build the source's own tree
     w.src_by_tgt = (pl.pruned && pl.lds) ? (env_int("ICP4R_SRC_ORDER", 1) != 0 ? 1 : 0)
                                          : (pl.pruned && env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0);
+    w.stage_first = (w.src_by_tgt && pl.lds && w.qv && w.qm) ? 1 : 0;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));

@@ -111,6 +111,8 @@ struct WorkArgs {
     int32_t src_by_tgt; // 1: a source whose target gets the kd order is ordered by descending the target's
                         // kd tree (src_order_kernel) instead of by its own tree: queries sorted by the
                         // target leaf they fall in, and that leaf seeds their first search
+    int32_t stage_first;  // 1 (batched plan): src_order_kernel writes the first pass' query records
+                          // (qv / qm, sorted order) itself; 0: the first pass' nn_key seeds
     uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,
                         // [8 + node] internal node (heap order) = 1 << 31 | mid << 13 | axis << 11 | key
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):

@@ -841,6 +841,9 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
 // query runs stay compact, and the leaf's first target seeds the query's first search (nn_key with
 // d² = +inf, read by the first pass).  It replaces the source's own kd build (index_kernel).
 constexpr int kSoWG = 512;
+// query records {index | sorted position << kNtPosShift, ...} and nn_t[i].w (nt_pack, below)
+constexpr int kNtPosShift = 14;
+constexpr int kNtIdxMask = (1 << kNtPosShift) - 1;
 
 __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w) {
     __shared__ uint32_t nodes[kKdNodes];
@@ -950,6 +953,36 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     int32_t* spm = w.sperm + (int64_t)p * w.x_stride;
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const float4* ts = w.tsort + (int64_t)p * w.t_stride;
+    if (w.stage_first) {
+        // The batched search's first-pass query records, in source order: {X_i, U = +inf} and
+        // {i | its position << kNtPosShift, the seed = its leaf's first target position} — the
+        // search takes them as they are instead of gathering X through sperm at every work item
+        // (a chain of dependent global round trips in front of each pair's first search).
+        const float4* X = w.X + (int64_t)p * w.x_stride;
+        float4* qv = w.qv + (int64_t)p * w.x_stride;
+        uint2* qm = w.qm + (int64_t)p * w.x_stride;
+#pragma unroll
+        for (int g = 0; g < kSoPer; g += kSoGrp) {
+            float4 xv[kSoGrp];
+#pragma unroll
+            for (int e = 0; e < kSoGrp; ++e) xv[e] = X[min(tid + (g + e) * kSoWG, n - 1)];
+#pragma unroll
+            for (int e = 0; e < kSoGrp; ++e) {
+                const int i = tid + (g + e) * kSoWG;
+                if (i >= n) continue;
+                const uint32_t leaf = (lv[(g + e) >> 1] >> (16 * ((g + e) & 1))) & 0xffffu;
+                const uint32_t pos = atomicAdd(&bins[leaf], 1u);
+                spm[pos] = i;
+                qv[pos] = make_float4(xv[e].x, xv[e].y, xv[e].z, INFINITY);
+                qm[pos] = make_uint2((uint32_t)i | (pos << kNtPosShift), leaf * (uint32_t)B);
+            }
+        }
+#if ICP4R_WG_TICKS
+        __syncthreads();
+        if (it) it[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+        return;
+    }
 #pragma unroll
     for (int g = 0; g < kSoPer; g += kSoGrp) {
         float sw[kSoGrp];  // the leaves' first targets' index bits (first-pass seeds), loads in flight together
@@ -1303,6 +1336,10 @@ constexpr int kLdsQ = 1;  // queries per lane (2 measured no faster: smaller run
 constexpr int kRing = 128;  // work items per wave (<= 63 pending + 64 appended per query slot)
 constexpr float kCacheMargin = 1.0e-4f;
 constexpr int kNeedWords = kCacheMaxN / 32;  // bitmap words per pair (one bit per Morton position)
+// miss_cnt[p]: the pass' misses, | kMissUnranked when the test left them unplaced (the pair's miss list
+// sq / sm and bitmap, for the search to place) instead of in rank order in qv / qm
+constexpr int32_t kMissUnranked = 1 << 30;
+constexpr int32_t kMissCount = kMissUnranked - 1;
 static_assert(kNeedWords <= kLdsWG, "compaction: one bitmap word per thread");
 
 // An LDS address held in a VGPR: a wave-uniform LDS address otherwise sits in an SGPR and every
@@ -1378,6 +1415,9 @@ __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float 
 #ifndef ICP4R_SKIP_SEED
 #define ICP4R_SKIP_SEED 1  // the lane's seed block (evaluated whole up front) is never queued again
 #endif
+#ifndef ICP4R_SB_EXPAND
+#define ICP4R_SB_EXPAND 1  // a reached superblock's blocks tested for the lanes that reach it only
+#endif
 #ifndef ICP4R_SB_BATCH
 #define ICP4R_SB_BATCH 1  // candidate superblocks tested together per traversal step
 #endif
@@ -1408,8 +1448,6 @@ __device__ __forceinline__ int lds_swz(int p) { return p ^ ((p >> 4) & (kLdsLeaf
 // (bits 14..27): the test reads one record for the miss bitmap's bit and for the search record it
 // writes (sq / sm: the next search's seed is that target position, no index lookup).  Sizes:
 // <= kCacheMaxN = 2^14 sources, <= 8192 targets on the batched plan.
-constexpr int kNtPosShift = 14;
-constexpr int kNtIdxMask = (1 << kNtPosShift) - 1;
 static_assert(kCacheMaxN <= (1 << kNtPosShift) && kLdsTargets <= (1 << kNtPosShift), "nn_t.w packing");
 __device__ __forceinline__ float nt_pack(int tpos, int pos) {
     return __uint_as_float((uint32_t)tpos | ((uint32_t)pos << kNtPosShift));
@@ -1622,13 +1660,13 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
     if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
         unsigned long long t = 0;
         for (int p = tid; p < npairs; p += kOrderWG)
-            t += pass_wants(w.state[p].phase, fitness_pass) ? (unsigned long long)w.miss_cnt[p] : 0ull;
+            t += pass_wants(w.state[p].phase, fitness_pass) ? (unsigned long long)(w.miss_cnt[p] & kMissCount) : 0ull;
         t = wave_sum(t);
         if ((tid & 63) == 0) atomicAdd(&tot_s, t);
     }
     __syncthreads();
     auto work = [&](int p) {
-        return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : w.miss_cnt[p];
+        return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : (w.miss_cnt[p] & kMissCount);
     };
     // a heavy pair's misses are cut into parts of part_size (first pass: one part, all queries), so
     // the few slowly converging pairs with thousands of misses spread over several CUs
@@ -1668,7 +1706,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
 // state: L in X_i.w, U in nn_u[i], the NN's coordinates in nn_t[i] with .w = its index | the query's
 // sorted position << 14 (nt_pack) — the position is what the next test flags a miss at.
 template <bool CACHE>
-__global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+__global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first, int ranked) {
     static_assert(kLdsQ == 1, "one query per lane");
     __shared__ LdsNN sh;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1713,7 +1751,16 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         //    rank in the miss bitmap.  The update kernel clears the bitmap (other parts may still be
         //    reading it).
         int nlist;
-        if (CACHE && !first) {
+        const int mc = (CACHE && !first && ranked) ? uload(w.miss_cnt + p) : kMissUnranked;
+        if (!(mc & kMissUnranked)) {
+            // the fused test put the pair's misses in rank order already (pair_cache_test)
+            const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
+            const int lo = ps > 0 ? part * ps : 0;
+            const int hi = ps > 0 ? lo + ps : (1 << 30);
+            nlist = min(hi, mc) - lo;
+            qv += lo;
+            qm += lo;
+        } else if (CACHE && !first) {
             const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
             const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
             const int lo = ps > 0 ? part * ps : 0;
@@ -1773,6 +1820,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             }
             qv += lo;  // this item's slice, read back by the runs
             qm += lo;
+        } else if (first && w.stage_first && src_by_tgt_tree(a, w, p)) {
+            nlist = n;  // src_order_kernel wrote the records
         } else {
             const int32_t* sperm = w.sperm + xs0;
             const int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
@@ -1882,7 +1931,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                         // -1 on idle lanes (never queue work, never widen the coarse bound)
             const int seed_pos0 = __builtin_amdgcn_readfirstlane(pj);
             const int seed_blk = pj / kLdsLeaf;
-            const uint32_t lane9 = (uint32_t)lane << 9;  // ring item: query lane << 9 | block
+            [[maybe_unused]] const uint32_t lane9 = (uint32_t)lane << 9;  // ring item: query lane << 9 | block
             {
                 // seed: the previous match (first pass: the target at the same relative position)
                 // and the rest of its 16-target block, evaluated up front from LDS — tight initial
@@ -1994,6 +2043,57 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             // the non-empty ones are queued.  A test may use a bound a drain has since tightened:
             // that only queues more work, never loses a target.
             const uint64_t ck1 = __builtin_readcyclecounter();
+#if ICP4R_SB_EXPAND
+            // A superblock some lane may reach has its 8 blocks tested for those lanes only: the c
+            // lanes that passed are compacted (ds_permute: rank k -> lane k), and each round tests 8
+            // of them against the 8 blocks at once — lane L takes passed lane r0 + L / 8 and block
+            // L % 8, with that query's coordinates and bound pulled from its lane (ds_bpermute).  The
+            // (query, block) pairs that pass are queued with one ballot per round.  (Testing all 64
+            // lanes against all 8 blocks spent 80 VALU per superblock on the ~5 lanes that need it.)
+            const int blk8 = lane & (kSuper - 1);
+            for (;;) {
+                const int sb = next_sb();
+                if (sb < 0) break;
+                ++ev_sbv;
+                tests += 64;
+                const auto* sbb = lds_vbase(&sh.sbx[sb][0]);
+                const uint64_t m = __ballot(pt_lb(sbb, x, y, z) <= bnd);
+                if (m == 0) continue;
+                ++ev_sbp;
+                const int c = __builtin_popcountll(m);
+                // this lane's tag: its lane id, and its seed block if that lies in sb (never queued:
+                // it was evaluated whole up front)
+                const int rel = seed_blk - sb * kSuper;
+                const uint32_t tag = (uint32_t)lane | ((ICP4R_SKIP_SEED && (uint32_t)rel < (uint32_t)kSuper) ? (8u | (uint32_t)rel) << 6 : 0u);
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                // passed lanes go to lane rank, the others to distinct lanes >= c (no collisions)
+                const uint32_t dst = lane_select(m, (uint32_t)c + (uint32_t)lane - rk, rk);
+                const uint32_t packed = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)tag);
+                // this lane's block box (8 rows, each read by 8 lanes: broadcast)
+                const auto* brow = lds_vbase(&sh.bx[sb * kSuper + blk8][0]);
+                float bb[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) bb[k] = brow[k];
+                tests += 8 * c;
+                for (int r0 = 0; r0 < c; r0 += 8) {
+                    const int srcl = r0 + (lane >> 3);
+                    const uint32_t tg = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl << 2, (int)packed);
+                    const int owner = (int)(tg & 63u);
+                    const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
+                    const float qb = __shfl(bnd, owner, 64);
+                    const bool ok = srcl < c && (tg >> 6) != (8u | (uint32_t)blk8) && pt_lb(bb, qx, qy, qz) <= qb;
+                    const uint64_t pm = __ballot(ok);
+                    if (pm == 0) continue;
+                    ev_blk += __builtin_popcountll(pm);
+                    const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)pm, tail));
+                    const uint32_t at = lane_select(pm, (uint32_t)(kRing + lane), slot & (kRing - 1));
+                    ring[at] = (uint16_t)(((uint32_t)owner << 9) | (uint32_t)(sb * kSuper + blk8));
+                    tail += (uint32_t)__builtin_popcountll(pm);
+                    if (tail - head >= 64) drain(64);
+                }
+            }
+#else
             for (;;) {
                 uint32_t sbpack = 0, valid = 0;
 #pragma unroll
@@ -2058,6 +2158,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     }
                 }
             }
+#endif
             if (tail != head) drain(tail - head);
             const uint64_t ck2 = __builtin_readcyclecounter();
             // the winner's coordinates come from its LDS slot (the key carries its position)
@@ -2479,9 +2580,12 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 // input point, FROM_SRC); X and U written.  The iteration passes write no key: nothing reads one
 // before the fitness pass — the update folds recompute d² from X and nn_t, and the next search
 // seeds from the record.
+// The miss records stay in LDS (lv / lm, the first lcap of them; the rest go to the pair's global
+// miss list sq / sm) until the rank placement at the end reads them back.
 template <int WG, int kPer, bool FROM_SRC>
 __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
-                                                uint32_t* need, int32_t* mcount, int32_t* wcnt, bool fitness) {
+                                                uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
+                                                int32_t* mcount, int32_t* wcnt, bool fitness, uint64_t* stamp = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t xs = (int64_t)p * w.x_stride;
     float4* X = w.X + xs;
@@ -2541,7 +2645,12 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
             } else if (valid) {
                 const uint32_t sp = nt_pos(t[e].w);
                 atomicOr(&need[sp >> 5], 1u << (sp & 31));
-                put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
+                if (k < lcap) {
+                    lv[k] = make_float4(o.x, o.y, o.z, Lm.y);
+                    lm[k] = make_uint2((uint32_t)i | (nt_tpos(t[e].w) << kNtPosShift), sp);
+                } else {
+                    put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
+                }
                 ++misses;
             }
         }
@@ -2566,13 +2675,82 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
         }
     }
     __syncthreads();
-    uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+    if (stamp && tid == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic: the test's end
+    int tot = 0;
+    for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
+    if (tot == 0) {
+        if (tid == 0) w.miss_cnt[p] = 0;
+        return;
+    }
     const int nwords = (n + 31) >> 5;
-    for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
-    if (tid == 0) {
-        int tot = 0;
-        for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
-        w.miss_cnt[p] = tot;
+    if (tot > lcap) {
+        // more misses than LDS records (the few slowly converging pairs): the whole list goes to
+        // sq / sm and the bitmap to global memory, and the search places it — a read-back of the
+        // overflow here sat on this workgroup's end, which sets the update's launch time
+        for (int k = tid; k < lcap; k += WG) {
+            w.sq[xs + k] = lv[k];
+            w.sm[xs + k] = lm[k];
+        }
+        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+        for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
+        if (tid == 0) w.miss_cnt[p] = tot | kMissUnranked;
+        return;
+    }
+    // Rank placement: the search reads its item's queries in sorted-position order (a run of 64
+    // consecutive ones is a compact box), so every miss record goes to its rank in the bitmap — the
+    // word's prefix + the set bits below it.  Done here, where the workgroup owns the whole bitmap,
+    // instead of in the search, where it put two barriers and three dependent global round trips in
+    // front of every work item.  Word prefixes: wave 0, kNeedWords / 64 words per lane.
+    if (wave == 0) {
+        constexpr int kW = kNeedWords / 64;
+        int c[kW], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            const int wd = lane * kW + j;
+            c[j] = wd < nwords ? __builtin_popcount(need[wd]) : 0;
+            sum += c[j];
+        }
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        int run = incl - sum;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            pre[lane * kW + j] = run;
+            run += c[j];
+        }
+    }
+    if (tid == 0) w.miss_cnt[p] = tot;
+    __syncthreads();
+    float4* qv = w.qv + xs;
+    uint2* qm = w.qm + xs;
+    auto get = [&](int k, float4& r, uint2& m) {  // (tot <= lcap: every record is in LDS)
+        k = min(k, tot - 1);
+        r = lv[k];
+        m = lm[k];
+    };
+    // (unconditional: a slot past the list re-read record tot - 1 and writes its very bytes to its
+    // very rank again)
+    auto put = [&](const float4& r, const uint2& m) {
+        const uint32_t sp = min(m.y, (uint32_t)(n - 1));
+        const int rk = pre[sp >> 5] + __builtin_popcount(need[sp >> 5] & ((1u << (sp & 31)) - 1u));
+        qv[rk] = r;
+        qm[rk] = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
+    };
+    for (int k0 = tid; k0 < tot; k0 += 4 * WG) {
+        float4 r0, r1, r2, r3;  // (named, not an array: an array went to scratch)
+        uint2 m0, m1, m2, m3;
+        get(k0, r0, m0);  // all loads of the round first
+        get(k0 + WG, r1, m1);
+        get(k0 + 2 * WG, r2, m2);
+        get(k0 + 3 * WG, r3, m3);
+        put(r0, m0);
+        put(r1, m1);
+        put(r2, m2);
+        put(r3, m3);
     }
 }
 
@@ -2603,8 +2781,10 @@ constexpr int kFoldChunkP = 512;  // points per LDS chunk of the fold passes
 constexpr int kFoldPad = ICP4R_FOLD_PAD;
 constexpr int kFoldRow = kFoldChunkP + kFoldPad;
 
+// the fused test's LDS miss records (24 B each) after the bitmap and its prefixes, in the fold buffers
+constexpr int kFoldRecs = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4) / 24) & ~15;
 struct FoldShared {
-    float buf[2][9][kFoldRow];
+    alignas(16) float buf[2][9][kFoldRow];
     float res[8];
     int32_t cnt[kFoldWaves];
     int32_t mcount;  // tail: the pair's miss list length so far
@@ -2831,7 +3011,11 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     // its HBM stream overlaps the other workgroups' latency-bound fold chains instead of taking a
     // launch of its own.  The workgroup owns the pair, so the bitmap is built in LDS and stored whole.
     if (tail_test && w.nn_u && sh.s.flag == 0) {
-        uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
+        // the fold buffers are free now: the bitmap, its word prefixes and the LDS miss records
+        uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);
+        int32_t* pre = reinterpret_cast<int32_t*>(need + kNeedWords);
+        float4* lv = reinterpret_cast<float4*>(pre + kNeedWords);
+        uint2* lm = reinterpret_cast<uint2*>(lv + kFoldRecs);
         const int nwords = (n + 31) >> 5;
         for (int k = tid; k < nwords; k += kFoldWG) need[k] = 0u;
         if (tid == 0) sh.mcount = 0;
@@ -2839,7 +3023,13 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
         __syncthreads();
-        pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, &sh.mcount, sh.cnt, false);
+#if ICP4R_WG_TICKS
+        uint64_t* stamp = wt ? wt + 6 : nullptr;
+#else
+        uint64_t* stamp = nullptr;
+#endif
+        pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs, &sh.mcount, sh.cnt,
+                                                        false, stamp);
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(4);
@@ -2902,12 +3092,16 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
 // workgroup (pair_cache_test), instead of as nn_cache_test_kernel after it — one read of X, U, nn_t
 // and the input per point, no launch of its own.
 constexpr int kPrepWG = 256;
+constexpr int kPrepRecs = 1024;  // the fitness test's LDS miss records (the fitness pass misses ~1 %)
 __global__ __launch_bounds__(kPrepWG) void fitness_prep_kernel(PairArgs a, WorkArgs w, int test) {
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     const PairState& st = w.state[p];
     if (st.phase == kPhaseInvalid) return;
     __shared__ float Tf[16];
     __shared__ uint32_t need[kNeedWords];
+    __shared__ int32_t pre[kNeedWords];
+    __shared__ float4 lv[kPrepRecs];
+    __shared__ uint2 lm[kPrepRecs];
     __shared__ int32_t mcount, wcnt[kPrepWG / 64];
     const int n = a.src_n[p];
     if (threadIdx.x < 16) Tf[threadIdx.x] = st.final_T[threadIdx.x];
@@ -2918,7 +3112,7 @@ __global__ __launch_bounds__(kPrepWG) void fitness_prep_kernel(PairArgs a, WorkA
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = Tf[q];
-        pair_cache_test<kPrepWG, 4, true>(a, w, p, n, T, need, &mcount, wcnt, true);
+        pair_cache_test<kPrepWG, 4, true>(a, w, p, n, T, need, pre, lv, lm, kPrepRecs, &mcount, wcnt, true);
         return;
     }
     __syncthreads();
@@ -3086,9 +3280,10 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
     if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
     if (cache)
-        hipLaunchKernelGGL((nn_lds_kernel<true>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+        hipLaunchKernelGGL((nn_lds_kernel<true>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first,
+                           test_fused && !first ? 1 : 0);
     else
-        hipLaunchKernelGGL((nn_lds_kernel<false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first);
+        hipLaunchKernelGGL((nn_lds_kernel<false>), dim3(grid), dim3(kLdsWG), 0, st, a, w, fitness_pass, first, 0);
     if (ev.search_stop && (e = hipEventRecord(ev.search_stop, st)) != hipSuccess) return e;
     return hipGetLastError();
 }

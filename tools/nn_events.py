@@ -52,6 +52,7 @@ def main():
         return np.array(list(buf), np.float64) if lib.icp4r__debug_ticks(ctx._h, buf, 32) == 0 else None
 
     prev = np.zeros(11)
+    prev_it = np.zeros(4)
     total = np.zeros(11)
     tot_ms = 0.0
     for k in range(1, a.iters + 2):  # the last one: the iterations + the fitness pass
@@ -67,6 +68,9 @@ def main():
         d = (t1 - t0)[16:27]
         last = d - prev
         prev = d
+        it = (t1 - t0)[8:12]  # per-item wall (100 MHz): compaction, staging, search (all waves), items
+        it_last = it - prev_it
+        prev_it = it
         total += last
         ms, _ = ctx.kernel_time_ms()
         r = {"pass": "fitness" if fit else k}
@@ -76,6 +80,11 @@ def main():
                         "pushes": last[5] / runs, "drains": last[6] / runs,
                         "cyc_setup": last[8] / runs, "cyc_traverse": last[9] / runs, "cyc_write": last[10] / runs}
         r["cyc_per_sb_visit"] = last[9] / max(last[2], 1)
+        ni = max(it_last[3], 1)
+        r["items"] = {"n": int(it_last[3]), "compact_us": it_last[0] / ni / 100, "stage_us": it_last[1] / ni / 100,
+                      "search_wall_us": it_last[2] / ni / 100,
+                      # wave clocks inside runs / (search wall x 16 waves): the waves' busy share of it
+                      "run_cyc_per_item": (last[8] + last[9] + last[10]) / ni}
         r["registration_kernel_ms"] = ms
         print(json.dumps(r), flush=True)
     runs = max(total[0], 1)

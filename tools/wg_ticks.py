@@ -79,6 +79,10 @@ def main():
     out["start"] = pct(t[:, 0] - t0)
     for j, name in enumerate(["passA", "passB", "solve", "tail"]):
         out[name] = pct(t[:, j + 1] - t[:, j])
+    t6 = raw[ok, 6].astype(np.int64).astype(np.float64) * 0.01
+    if (t6 > 0).all():  # the tail split at the test's end: the test, then the misses' rank placement
+        out["tail_test"] = pct(t6 - t[:, 3])
+        out["tail_place"] = pct(t[:, 4] - t6)
     out["total"] = pct(t[:, 4] - t[:, 0])
     print(json.dumps(out))
     ctx.close()
