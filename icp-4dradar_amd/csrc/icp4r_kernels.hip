@@ -657,7 +657,9 @@ __device__ void index_boxes(const WorkArgs& w, int p, int n) {
 // The source of pair p is ordered by its target's kd tree (src_order_kernel) rather than its own.
 __device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArgs& w, int p) {
     const int m = a.tgt_n[p];
-    return w.src_by_tgt && w.kdn && (w.kd_index & 1) && m > 0 && m <= kKdMaxN && w.t_stride <= kKdMaxN;
+    // (src_order_kernel places at most kKdMaxN sources; a larger source gets its own index)
+    return w.src_by_tgt && w.kdn && (w.kd_index & 1) && m > 0 && m <= kKdMaxN && w.t_stride <= kKdMaxN &&
+           a.src_n[p] <= kKdMaxN;
 }
 
 __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
@@ -850,6 +852,7 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     __shared__ uint32_t bins[kKdMaxN / 16];
     __shared__ uint32_t wsum[kSoWG / 64];
     __shared__ float qz[6];
+    __shared__ uint32_t sl[kKdMaxN];  // stage_first: source index | leaf << kNtPosShift per sorted position
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     if (w.state[p].phase == kPhaseInvalid || !src_by_tgt_tree(a, w, p)) return;
     const int n = a.src_n[p], m = a.tgt_n[p];
@@ -954,27 +957,39 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const float4* ts = w.tsort + (int64_t)p * w.t_stride;
     if (w.stage_first) {
-        // The batched search's first-pass query records, in source order: {X_i, U = +inf} and
+        // The batched search's first-pass query records in sorted order: {X_i, U = +inf} and
         // {i | its position << kNtPosShift, the seed = its leaf's first target position} — the
         // search takes them as they are instead of gathering X through sperm at every work item
-        // (a chain of dependent global round trips in front of each pair's first search).
+        // (a chain of dependent global round trips in front of each pair's first search).  The
+        // scatter goes to LDS (i | leaf << 14 at the position), then every record is written in
+        // position order: scattered 24-B record stores had cost more than the search saved.
+#pragma unroll
+        for (int g = 0; g < kSoPer; ++g) {
+            const int i = tid + g * kSoWG;
+            if (i >= n) continue;
+            const uint32_t leaf = (lv[g >> 1] >> (16 * (g & 1))) & 0xffffu;
+            sl[atomicAdd(&bins[leaf], 1u)] = (uint32_t)i | (leaf << kNtPosShift);
+        }
+        __syncthreads();
         const float4* X = w.X + (int64_t)p * w.x_stride;
         float4* qv = w.qv + (int64_t)p * w.x_stride;
         uint2* qm = w.qm + (int64_t)p * w.x_stride;
 #pragma unroll
         for (int g = 0; g < kSoPer; g += kSoGrp) {
+            uint32_t e8[kSoGrp];
             float4 xv[kSoGrp];
 #pragma unroll
-            for (int e = 0; e < kSoGrp; ++e) xv[e] = X[min(tid + (g + e) * kSoWG, n - 1)];
+            for (int e = 0; e < kSoGrp; ++e) e8[e] = sl[min(tid + (g + e) * kSoWG, n - 1)];
+#pragma unroll
+            for (int e = 0; e < kSoGrp; ++e) xv[e] = X[e8[e] & kNtIdxMask];  // gathers, all in flight
 #pragma unroll
             for (int e = 0; e < kSoGrp; ++e) {
-                const int i = tid + (g + e) * kSoWG;
-                if (i >= n) continue;
-                const uint32_t leaf = (lv[(g + e) >> 1] >> (16 * ((g + e) & 1))) & 0xffffu;
-                const uint32_t pos = atomicAdd(&bins[leaf], 1u);
-                spm[pos] = i;
+                const int pos = tid + (g + e) * kSoWG;
+                if (pos >= n) continue;
+                const uint32_t i = e8[e] & kNtIdxMask, leaf = e8[e] >> kNtPosShift;
+                spm[pos] = (int32_t)i;
                 qv[pos] = make_float4(xv[e].x, xv[e].y, xv[e].z, INFINITY);
-                qm[pos] = make_uint2((uint32_t)i | (pos << kNtPosShift), leaf * (uint32_t)B);
+                qm[pos] = make_uint2(i | ((uint32_t)pos << kNtPosShift), leaf * (uint32_t)B);
             }
         }
 #if ICP4R_WG_TICKS
@@ -3251,7 +3266,7 @@ hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, i
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
     // every source by the target's tree: launch the target builds alone (a grid with idle source
     // workgroups left half the CUs without a build)
-    const bool tgt_only = w.src_by_tgt && w.kdn && (w.kd_index & 1) && w.t_stride <= kKdMaxN;
+    const bool tgt_only = w.src_by_tgt && w.kdn && (w.kd_index & 1) && w.t_stride <= kKdMaxN && w.x_stride <= kKdMaxN;
     hipLaunchKernelGGL(index_kernel, dim3(npairs, tgt_only ? 1 : 2), dim3(kIdxWG), 0, st, a, w);
     if (w.src_by_tgt && w.kdn)
         hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);

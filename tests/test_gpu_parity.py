@@ -177,13 +177,15 @@ def test_target_split_equals_unsplit(gpu_ctx):
 
 
 @pytest.mark.parametrize("lds,cache,tile", [("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")])
-@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map"])
+@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map", "big_src"])
 def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
     """Pruned (LDS target tiles x query parts, the scalar-cache stream, or with the target set in LDS
     and per-query work lists, with or without the cached-neighbour test), brute-force and packed
     searches produce bit-identical registrations (T, fitness, iterations, aligned cloud) — the pruned
     index changes only which targets are evaluated.  dup_map: every target twice, the copies in
-    different tiles of a > 8192-point target, so ties resolve across tiles (lowest index)."""
+    different tiles of a > 8192-point target, so ties resolve across tiles (lowest index).  big_src:
+    a batch mixing sources of more than 8192 points (their own index) with ones ordered by the
+    target's tree."""
     import icp4r
 
     monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
@@ -213,6 +215,9 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
 
         mp = synth.make_map_pair(1)
         pairs = [(mp.src_xyzi()[:4096], mp.tgt_xyzi())]
+    elif case == "big_src":  # sources beyond one kd build (own index, not the target's tree) beside small ones
+        shapes = [(12000, 8000), (16384, 4096), (9000, 8192), (8192, 8192), (500, 300)]
+        pairs = [_pair(350 + k, n, m) for k, (n, m) in enumerate(shapes)]
     else:
         sp, tp = _pair(340, 3000, 6000)
         pairs = [(sp, np.concatenate([tp, tp]))]
