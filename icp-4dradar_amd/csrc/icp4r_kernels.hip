@@ -2067,12 +2067,24 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             // lanes against all 8 blocks spent 80 VALU per superblock on the ~5 lanes that need it.)
             const int blk8 = lane & (kSuper - 1);
             for (;;) {
-                const int sb = next_sb();
-                if (sb < 0) break;
-                ++ev_sbv;
-                tests += 64;
-                const auto* sbb = lds_vbase(&sh.sbx[sb][0]);
-                const uint64_t m = __ballot(pt_lb(sbb, x, y, z) <= bnd);
+                // kSbBatch candidates tested together (independent LDS reads and test chains), then
+                // the ones some lane may reach processed in order
+                int sbs[kSbBatch];
+                uint64_t ms[kSbBatch];
+#pragma unroll
+                for (int j = 0; j < kSbBatch; ++j) sbs[j] = next_sb();
+                if (sbs[0] < 0) break;
+#pragma unroll
+                for (int j = 0; j < kSbBatch; ++j) {
+                    const auto* sbb = lds_vbase(&sh.sbx[sbs[j] < 0 ? 0 : sbs[j]][0]);
+                    ms[j] = sbs[j] < 0 ? 0ull : __ballot(pt_lb(sbb, x, y, z) <= bnd);
+                    ev_sbv += sbs[j] < 0 ? 0 : 1;
+                }
+                tests += 64 * kSbBatch;
+#pragma unroll
+                for (int j = 0; j < kSbBatch; ++j) {
+                const int sb = sbs[j];
+                const uint64_t m = ms[j];
                 if (m == 0) continue;
                 ++ev_sbp;
                 const int c = __builtin_popcountll(m);
@@ -2106,6 +2118,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
                     ring[at] = (uint16_t)(((uint32_t)owner << 9) | (uint32_t)(sb * kSuper + blk8));
                     tail += (uint32_t)__builtin_popcountll(pm);
                     if (tail - head >= 64) drain(64);
+                }
                 }
             }
 #else
