@@ -560,7 +560,10 @@ def run_gpu(args) -> int:
                 "launches": nn_launches,
                 "note": "FP32 VALU work of the exact pruned search kernel (nn_lds_kernel: the queries the "
                         "cached-neighbour test could not resolve), counted on the device: distance evaluations "
-                        "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add); "
+                        "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add) "
+                        "- since round 2 session 4 only the block tests of queries that reach the superblock, "
+                        "which is all the kernel performs (the ~100M per launch it had spent on lanes that "
+                        "could not reach it were counted before, so the fraction fell as the kernel got faster); "
                         "compare/select/ballot/LDS not counted. achieved = that / avg launch time (HIP events on "
                         "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). brute_force_equivalent_"
                         "tflops = n*m*8 per NN pass / search time. See DESIGN.md §5",
