@@ -400,10 +400,21 @@ template <typename Get>  // Get: int -> float4, point i of the cloud
 __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, uint32_t* kdn = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
-    // 1. bounding box -> quantisation
+    // 1. bounding box -> quantisation.  The thread's points (i = tid + k * kIdxWG) are loaded once,
+    // every load in flight together, and kept for the counting sorts: three load-use passes over the
+    // cloud had waited out a global round trip per point and pass (45 us of a build under load).
+    float px[kKdPer], py[kKdPer], pz[kKdPer];  // (xyz only: whole float4s spilled registers)
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {
+        const float4 v = pts(min(tid + k * kIdxWG, n - 1));
+        px[k] = v.x;
+        py[k] = v.y;
+        pz[k] = v.z;
+    }
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts(i);
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {  // (a clamped duplicate of point n - 1 changes no extent)
+        const float4 v = make_float4(px[k], py[k], pz[k], 0.0f);
         mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
         mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
     }
@@ -438,8 +449,10 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
     const float lo[3] = {sh.lo[0], sh.lo[1], sh.lo[2]}, sc[3] = {sh.sc[0], sh.sc[1], sh.sc[2]};
     auto bin = [&](float c, int ax) { return min(kKdBins - 1, max(0, (int)((c - lo[ax]) * sc[ax]))); };
     // 2. three counting sorts at once: histogram, exclusive scan, scatter
-    for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts(i);
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {
+        if (tid + k * kIdxWG >= n) continue;
+        const float4 v = make_float4(px[k], py[k], pz[k], 0.0f);
         atomicAdd(&sh.u.hist[0][bin(v.x, 0)], 1u);
         atomicAdd(&sh.u.hist[1][bin(v.y, 1)], 1u);
         atomicAdd(&sh.u.hist[2][bin(v.z, 2)], 1u);
@@ -475,8 +488,11 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts(i);
+#pragma unroll
+    for (int k = 0; k < kKdPer; ++k) {
+        const int i = tid + k * kIdxWG;
+        if (i >= n) continue;
+        const float4 v = make_float4(px[k], py[k], pz[k], 0.0f);
         const int bx = bin(v.x, 0), by = bin(v.y, 1), bz = bin(v.z, 2);
         sh.L[0][atomicAdd(&sh.u.hist[0][bx], 1u)] = (uint16_t)i;
         sh.L[1][atomicAdd(&sh.u.hist[1][by], 1u)] = (uint16_t)i;
@@ -698,32 +714,50 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
             float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
             const float lastw = __uint_as_float((uint32_t)ord[n - 1]);
             const int B = w.leaf;
-            for (int pos = tid; pos < (int)w.t_stride; pos += kIdxWG) {
-                float4 v = make_float4(INFINITY, INFINITY, INFINITY, lastw);
-                float4 l = v, h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-                if (pos < n) {
-                    const int i = ord[pos];
-                    const float4 c = pts[i];
-                    v = make_float4(c.x, c.y, c.z, __uint_as_float((uint32_t)i));
-                    tinv[i] = pos;
-                    l = v;
-                    h = v;
+            // every gather of the thread's positions in flight together (t_stride <= kKdMaxN here):
+            // a load-use loop had waited out one global round trip per position.  (t_stride is a
+            // multiple of 64, so the position guard is wave-uniform: the shuffles below see every lane.)
+            constexpr int kG = kKdPer / 2;  // two rounds of 8 (16 in flight spilled registers)
+#pragma unroll
+            for (int k0 = 0; k0 < kKdPer; k0 += kG) {
+            float cx[kG], cy[kG], cz[kG];
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                const float4 c = pts[ord[min(tid + (k0 + k) * kIdxWG, n - 1)]];
+                cx[k] = c.x;
+                cy[k] = c.y;
+                cz[k] = c.z;
+            }
+#pragma unroll
+            for (int kk = 0; kk < kG; ++kk) {
+                const int pos = tid + (k0 + kk) * kIdxWG;
+                if (pos < (int)w.t_stride) {
+                    float4 v = make_float4(INFINITY, INFINITY, INFINITY, lastw);
+                    float4 l = v, h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+                    if (pos < n) {
+                        const int i = ord[pos];
+                        v = make_float4(cx[kk], cy[kk], cz[kk], __uint_as_float((uint32_t)i));
+                        tinv[i] = pos;
+                        l = v;
+                        h = v;
+                    }
+                    ts[pos] = v;
+                    for (int off = 1; off < B; off <<= 1) {
+                        l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
+                        l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
+                        l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
+                    }
+                    if ((lane & (B - 1)) == 0) {
+                        const int b = pos / B;
+                        l.w = 0.f;
+                        h.w = 0.f;
+                        tb[2 * b] = l;
+                        tb[2 * b + 1] = h;
+                        shu.kd.u.bbox[2 * b] = l;
+                        shu.kd.u.bbox[2 * b + 1] = h;
+                    }
                 }
-                ts[pos] = v;
-                for (int off = 1; off < B; off <<= 1) {
-                    l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
-                    l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
-                    l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
-                }
-                if ((lane & (B - 1)) == 0) {
-                    const int b = pos / B;
-                    l.w = 0.f;
-                    h.w = 0.f;
-                    tb[2 * b] = l;
-                    tb[2 * b + 1] = h;
-                    shu.kd.u.bbox[2 * b] = l;
-                    shu.kd.u.bbox[2 * b + 1] = h;
-                }
+            }
             }
             __syncthreads();
             float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
