@@ -2644,10 +2644,36 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 // seeds from the record.
 // The miss records stay in LDS (lv / lm, the first lcap of them; the rest go to the pair's global
 // miss list sq / sm) until the rank placement at the end reads them back.
+// The first point group's loads (kPer points per thread: X, the NN record, U) — issued by the update
+// before its solve, so their latency hides behind thread 0's SVD (they do not depend on T_inc).
+template <int kPer>
+struct TailFirst {
+    float4 v[kPer], t[kPer];
+    float U[kPer];
+};
+template <int WG, int kPer>
+__device__ __forceinline__ int tail_group0(int n) {  // first (last-to-first) group's start
+    const int kStep = WG * kPer, ngrp = (n + kStep - 1) / kStep;
+    return (ICP4R_TAIL_REV ? ngrp - 1 : 0) * kStep;
+}
+template <int WG, int kPer>
+__device__ __forceinline__ void tail_prefetch(const WorkArgs& w, int p, int n, TailFirst<kPer>& f) {
+    const int64_t xs = (int64_t)p * w.x_stride;
+    const int i0 = tail_group0<WG, kPer>(n);
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+        const int i = min(i0 + e * WG + (int)threadIdx.x, n - 1);
+        f.v[e] = w.X[xs + i];
+        f.t[e] = w.nn_t[xs + i];
+        f.U[e] = w.nn_u[xs + i];
+    }
+}
+
 template <int WG, int kPer, bool FROM_SRC>
 __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
                                                 uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
-                                                int32_t* mcount, int32_t* wcnt, bool fitness, uint64_t* stamp = nullptr) {
+                                                int32_t* mcount, int32_t* wcnt, bool fitness, uint64_t* stamp = nullptr,
+                                                const TailFirst<kPer>* first = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t xs = (int64_t)p * w.x_stride;
     float4* X = w.X + xs;
@@ -2675,7 +2701,18 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
     // any.)
     const int ngrp = (n + kStep - 1) / kStep;
     auto grp0 = [&](int g) { return (ICP4R_TAIL_REV ? ngrp - 1 - g : g) * kStep; };
-    if (ngrp > 0) load(grp0(0), v, t, U, sv);
+    if (ngrp > 0) {
+        if (first && !FROM_SRC) {
+#pragma unroll
+            for (int e = 0; e < kPer; ++e) {
+                v[e] = first->v[e];
+                t[e] = first->t[e];
+                U[e] = first->U[e];
+            }
+        } else {
+            load(grp0(0), v, t, U, sv);
+        }
+    }
     for (int g = 0; g < ngrp; ++g) {
         const int i0 = grp0(g);
         float4 vn[kPer], tn[kPer], sn[kPer];
@@ -3061,6 +3098,15 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __syncthreads();
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(2);
+    // the fused test's first point group is loaded, and its LDS bitmap cleared, while thread 0 solves
+    const bool tail = tail_test && w.nn_u;
+    TailFirst<ICP4R_TAIL_PER> tf;
+    uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
+    if (tail) {
+        tail_prefetch<kFoldWG, ICP4R_TAIL_PER>(w, p, n, tf);
+        for (int k = tid; k < ((n + 31) >> 5); k += kFoldWG) need[k] = 0u;
+        if (tid == 0) sh.mcount = 0;
+    }
     if (tid == 0) solve_pair<kNumericsPCL>(sh.s, st, kp);
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
@@ -3072,26 +3118,21 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     // transformCloud(T_inc), the bounds moved, the test, hit keys, the miss bitmap — done here, where
     // its HBM stream overlaps the other workgroups' latency-bound fold chains instead of taking a
     // launch of its own.  The workgroup owns the pair, so the bitmap is built in LDS and stored whole.
-    if (tail_test && w.nn_u && sh.s.flag == 0) {
-        // the fold buffers are free now: the bitmap, its word prefixes and the LDS miss records
-        uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);
+    if (tail && sh.s.flag == 0) {
+        // the fold buffers: the bitmap (cleared above), its word prefixes and the LDS miss records
         int32_t* pre = reinterpret_cast<int32_t*>(need + kNeedWords);
         float4* lv = reinterpret_cast<float4*>(pre + kNeedWords);
         uint2* lm = reinterpret_cast<uint2*>(lv + kFoldRecs);
-        const int nwords = (n + 31) >> 5;
-        for (int k = tid; k < nwords; k += kFoldWG) need[k] = 0u;
-        if (tid == 0) sh.mcount = 0;
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
-        __syncthreads();
 #if ICP4R_WG_TICKS
         uint64_t* stamp = wt ? wt + 6 : nullptr;
 #else
         uint64_t* stamp = nullptr;
 #endif
         pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs, &sh.mcount, sh.cnt,
-                                                        false, stamp);
+                                                        false, stamp, &tf);
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(4);
