@@ -2560,19 +2560,34 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
         sh.flag = 1;
         return;
     }
+    // the pair state this serial solve reads, loaded up front (in flight during the SVD): each had
+    // been a dependent global load on thread 0's critical path
+    float F[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) F[k] = st.final_T[k];
+    ConvState cs;
+    cs.prev_mse = st.prev_mse;
+    cs.similar = st.similar;
+    cs.state = st.conv_state;
+    const int32_t iters = st.iterations + 1;
     float* Tinc = sh.T_inc;
     mat4_identity(Tinc);
     double mse;
     if constexpr (NUM == kNumericsPCL) {
         // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (the fold), float SVD,
         // R as Matrix4f, Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean.
-        for (int k = 0; k < 9; ++k) sh.sigmaf[k] = sh.one_over_n * sh.sigmaf[k];
-        umeyama_rotation_f32(sh.sigmaf, sh.svdf);
+        // (in registers: umeyama_rotation_f32_reg is umeyama_rotation_f32 with static indices)
+        float sg[9], R[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) sg[k] = sh.one_over_n * sh.sigmaf[k];
+        umeyama_rotation_f32_reg(sg, R);
+#pragma unroll
         for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) Tinc[j * 4 + i] = sh.svdf.R[i * 3 + j];
-            float rs = sh.svdf.R[i * 3 + 0] * sh.mean[0];
-            rs = sh.svdf.R[i * 3 + 1] * sh.mean[1] + rs;
-            rs = sh.svdf.R[i * 3 + 2] * sh.mean[2] + rs;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Tinc[j * 4 + i] = R[i * 3 + j];
+            float rs = R[i * 3 + 0] * sh.mean[0];
+            rs = R[i * 3 + 1] * sh.mean[1] + rs;
+            rs = R[i * 3 + 2] * sh.mean[2] + rs;
             Tinc[12 + i] = sh.mean[3 + i] - rs;
         }
         mse = sh.mse_sum / (double)cnt;  // calculateMSE: sequential double sum / |C|
@@ -2593,13 +2608,12 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
         mse = sh.mom[MomLayout<kNumericsF64>::MSE] / (double)cnt;
     }
     for (int k = 0; k < 16; ++k) st.T_inc[k] = Tinc[k];
-    mat4_mul_f(Tinc, st.final_T, st.final_T);  // final_transformation_ = transformation_ * final
-    st.iterations += 1;
-    ConvState cs;
-    cs.prev_mse = st.prev_mse;
-    cs.similar = st.similar;
-    cs.state = st.conv_state;
-    const int conv = has_converged(kp.conv, st.iterations, Tinc, mse, cs);
+    float Fn[16];
+    mat4_mul_f(Tinc, F, Fn);  // final_transformation_ = transformation_ * final
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st.final_T[k] = Fn[k];
+    st.iterations = iters;
+    const int conv = has_converged(kp.conv, iters, Tinc, mse, cs);
     st.prev_mse = cs.prev_mse;
     st.similar = cs.similar;
     st.conv_state = cs.state;

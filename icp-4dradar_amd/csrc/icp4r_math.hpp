@@ -298,6 +298,126 @@ __host__ __device__ inline void umeyama_rotation_f32(const float* sigma, SvdWork
         }
 }
 
+// The same float SVD + Umeyama rotation as umeyama_rotation_f32, every operation in the same order,
+// with all indices static so the arrays live in registers: on the device the LDS-resident work
+// struct put a dependent LDS round trip on every access of thread 0's serial solve.
+__device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
+    float W[9], V[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) W[k] = A[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+#pragma nounroll
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        float off = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int p = r == 2 ? 1 : 0, q = r == 0 ? 1 : 2;
+            float al = 0, be = 0, ga = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                al += W[k * 3 + p] * W[k * 3 + p];
+                be += W[k * 3 + q] * W[k * 3 + q];
+                ga += W[k * 3 + p] * W[k * 3 + q];
+            }
+            if (ga == 0) continue;
+            float nrm = sqrtf(al * be);
+            if (nrm == 0) continue;
+            float rel = fabsf(ga) / nrm;
+            if (rel > off) off = rel;
+            if (rel <= 1e-7f) continue;
+            float zeta = (be - al) / (2 * ga);
+            float t = (zeta >= 0 ? 1.0f : -1.0f) / (fabsf(zeta) + sqrtf(1.0f + zeta * zeta));
+            float c = 1.0f / sqrtf(1.0f + t * t);
+            float s = c * t;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float wp = W[k * 3 + p], wq = W[k * 3 + q];
+                W[k * 3 + p] = c * wp - s * wq;
+                W[k * 3 + q] = s * wp + c * wq;
+                float vp = V[k * 3 + p], vq = V[k * 3 + q];
+                V[k * 3 + p] = c * vp - s * vq;
+                V[k * 3 + q] = s * vp + c * vq;
+            }
+        }
+        if (off <= 1e-7f) break;
+    }
+    float sv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        sv[c] = sqrtf(W[0 * 3 + c] * W[0 * 3 + c] + W[1 * 3 + c] * W[1 * 3 + c] + W[2 * 3 + c] * W[2 * 3 + c]);
+    // the column order by descending singular value: the same three compare-and-swaps, on registers
+    int o0 = 0, o1 = 1, o2 = 2;
+    auto svo = [&](int i) { return i == 0 ? sv[0] : (i == 1 ? sv[1] : sv[2]); };
+    if (svo(o1) > svo(o0)) { const int tt = o0; o0 = o1; o1 = tt; }
+    if (svo(o2) > svo(o0)) { const int tt = o0; o0 = o2; o2 = tt; }
+    if (svo(o2) > svo(o1)) { const int tt = o1; o1 = o2; o2 = tt; }
+    const int ord[3] = {o0, o1, o2};
+    auto col = [&](const float (&M)[9], int k, int c) {  // M[k][c] for a runtime column c in 0..2
+        return c == 0 ? M[k * 3 + 0] : (c == 1 ? M[k * 3 + 1] : M[k * 3 + 2]);
+    };
+    float S[3], Vs[9], Ws[9], U[9];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        S[c] = svo(ord[c]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            Vs[k * 3 + c] = col(V, k, ord[c]);
+            Ws[k * 3 + c] = col(W, k, ord[c]);
+        }
+    }
+    int rank = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        if (S[c] > 1e-6f * (S[0] > 0 ? S[0] : 1.0f) && S[c] > 0) rank = c + 1;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) U[k] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        if (c < rank)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) U[k * 3 + c] = Ws[k * 3 + c] / S[c];
+    if (rank == 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) U[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+    } else {
+        if (rank == 1) {
+            int ax = 0;
+            float amin = fabsf(U[0]);
+#pragma unroll
+            for (int k = 1; k < 3; ++k)
+                if (fabsf(U[k * 3]) < amin) {
+                    amin = fabsf(U[k * 3]);
+                    ax = k;
+                }
+            const float e0 = ax == 0 ? 1.0f : 0.0f, e1 = ax == 1 ? 1.0f : 0.0f, e2 = ax == 2 ? 1.0f : 0.0f;
+            float c0 = U[1 * 3] * e2 - U[2 * 3] * e1;
+            float c1 = U[2 * 3] * e0 - U[0 * 3] * e2;
+            float c2 = U[0 * 3] * e1 - U[1 * 3] * e0;
+            float nn = sqrtf(c0 * c0 + c1 * c1 + c2 * c2);
+            U[0 * 3 + 1] = c0 / nn;
+            U[1 * 3 + 1] = c1 / nn;
+            U[2 * 3 + 1] = c2 / nn;
+        }
+        if (rank <= 2) {
+            U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
+            U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
+            U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+        }
+    }
+    float d[3] = {1.0f, 1.0f, 1.0f};
+    if (det3_f32(U) * det3_f32(Vs) < 0) d[2] = -1.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float acc = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc += U[i * 3 + k] * d[k] * Vs[j * 3 + k];
+            R[i * 3 + j] = acc;
+        }
+}
+
 // ---- convergence: DefaultConvergenceCriteria<float>::hasConverged ------------------------------
 struct ConvParams {
     int32_t max_iterations;
