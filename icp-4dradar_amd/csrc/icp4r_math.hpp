@@ -301,7 +301,7 @@ __host__ __device__ inline void umeyama_rotation_f32(const float* sigma, SvdWork
 // The same float SVD + Umeyama rotation as umeyama_rotation_f32, every operation in the same order,
 // with all indices static so the arrays live in registers: on the device the LDS-resident work
 // struct put a dependent LDS round trip on every access of thread 0's serial solve.
-__device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
+__host__ __device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
     float W[9], V[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) W[k] = A[k];
