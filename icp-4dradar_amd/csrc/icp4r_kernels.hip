@@ -2745,10 +2745,10 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
             o.w = Lm.x;
             const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
             const bool hit = valid & cache_hit(Lm.x, d2);
-            if (valid) {
-                X[i] = o;
-                uu[i] = Lm.y;
-            }
+            // (the fitness pass: no later pass reads the bounds, and X only for the aligned output —
+            // the misses' search records carry their own coordinates)
+            if (valid && (!fitness || a.aligned)) X[i] = o;
+            if (valid && !fitness) uu[i] = Lm.y;
             const int k = wave_append(valid && !hit, mcount);
             if (hit) {
                 // the fitness pass' keys are read for their d² only (finish_kernel): a hit's index
