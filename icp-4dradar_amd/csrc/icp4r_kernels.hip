@@ -2646,18 +2646,19 @@ __device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_
 // The cached-neighbour test of one pair by one workgroup of WG threads (the update's fused tail, and
 // the fitness pass inside fitness_prep_kernel): the same work as nn_cache_test_kernel for the pair —
 // X_i's new position (FROM_SRC: T·input_i, the fitness pass' final·input; else T·X_i, the deferred
-// transformCloud(T_inc)), the bounds moved by |new − old|, the test against the cached NN, a miss's
-// bit in the pair's bitmap (built in LDS: `need`, zeroed by the caller) and its search record
-// appended to the pair's miss list; the fitness pass also writes a hit's key (finish_kernel's
-// fitness reads them).  kPer points per thread per group, software-pipelined: the next group's
-// loads are issued before this group's stores, so the stores drain while the loads are in flight (a
-// load issued after a store would wait behind it on vmcnt).
+// transformCloud(T_inc)), the bounds moved by |new − old|, the test against the cached NN; a miss
+// sets its bit in the pair's bitmap (built in LDS: `need`, zeroed by the caller) and appends its
+// search record; the fitness pass also writes a hit's key (finish_kernel's fitness reads them).
+// kPer points per thread per group, software-pipelined: the next group's loads are issued before
+// this group's stores, so the stores drain while the loads are in flight (a load issued after a store
+// would wait behind it on vmcnt).
 // Per point: X (.w = L) and nn_t (.w = target position | sorted position) read, U read (and the
-// input point, FROM_SRC); X and U written.  The iteration passes write no key: nothing reads one
-// before the fitness pass — the update folds recompute d² from X and nn_t, and the next search
-// seeds from the record.
-// The miss records stay in LDS (lv / lm, the first lcap of them; the rest go to the pair's global
-// miss list sq / sm) until the rank placement at the end reads them back.
+// input point, FROM_SRC); X and U written (the fitness pass: neither bounds nor X, unless the aligned
+// cloud is asked for).  The iteration passes write no key: nothing reads one before the fitness pass
+// — the update folds recompute d² from X and nn_t, and the next search seeds from the record.
+// The miss records stay in LDS (lv / lm, the first lcap of them) and are placed at their ranks in the
+// pair's query list (qv / qm) at the end; a pair with more misses than lcap leaves its whole list in
+// sq / sm with its bitmap, flagged kMissUnranked, for the search to place.
 // The first point group's loads (kPer points per thread: X, the NN record, U) — issued by the update
 // before its solve, so their latency hides behind thread 0's SVD (they do not depend on T_inc).
 template <int kPer>
