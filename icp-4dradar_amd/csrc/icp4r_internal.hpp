@@ -139,7 +139,8 @@ struct WorkArgs {
     uint2* qm;          // ... {source index | sorted position << 14, seed's sorted target position}
     uint32_t* need;     // [npairs * need_stride] per pair: bit s = the query at Morton position s missed
     int64_t need_stride;
-    int32_t* miss_cnt;  // [npairs] misses of the current pass (cleared by the search)
+    int32_t* miss_cnt;  // [npairs] misses of the current pass (cleared by the update); | kMissUnranked when
+                        // the fused test left them unplaced (sq / sm + bitmap) for the search to place
     // Batched search (nn_lds_kernel): the pass's pair work list, heaviest first, and its queue
     int32_t* plist;     // [npairs * ceil(x_stride / 64)] items (pair << 10 | part)
     int32_t* plist_n;   // [4]: items, (queue), the pass's part size (nn_order_kernel)
