@@ -20,10 +20,13 @@ against the oracle) are the TIMED run's, copied before any diagnostic rerun.
 Beside the headline: ``incl_upload`` (the same steps with each batch's H2D upload from pinned host
 memory inside the timed region, overlapped with the previous batch on a copy stream), ``gather``
 (the all-gather timed alone), ``roofline`` (the dominant kernel, the batched search, from the
-library's HIP events on its launch stream), ``c5`` (the scan-to-map config, priced against HBM) and
-``cpu_baseline`` (the oracle — the C restatement of the reference CPU path — on one pinned core,
-with median / p90 per pair, and on all the process's cores, both running the node's two fitness
-passes, ``iterative_closest_point.cpp:516,:520``).
+library's HIP events on its launch stream; ``traffic`` from the committed PMC passes of the same
+library build, matched by sha256), ``c1`` / ``c2`` / ``c5`` (BASELINE.json's single-pair configs:
+2k/2k PCL defaults, 8k/8k 20 iterations, and the 8k-scan-vs-65k-map registration, one pair per call,
+each with its own roofline, oracle check and single-core CPU baseline) and ``cpu_baseline`` (the
+oracle — the C restatement of the reference CPU path — on one pinned core, with median / p90 per
+pair, and on all the process's cores, both running the node's two fitness passes,
+``iterative_closest_point.cpp:516,:520``).
 
 ``--dry-run`` exercises the launcher, the sharding and the gather on CPU (gloo, no GPU, no
 registration): every rank fills its result rows with their global pair index, and rank 0 checks the
@@ -62,7 +65,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-all-seconds", type=float, default=8.0, help="all-cores CPU-baseline budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-upload", action="store_true", help="skip the incl-upload figure")
-    ap.add_argument("--no-c5", action="store_true", help="skip the scan-to-map (C5) figure")
+    ap.add_argument("--configs", default="C1,C2,C5", help="single-pair configs reported beside the headline "
+                                                          "(rank 0, N=1): C1, C2, C5; '' for none")
+    ap.add_argument("--no-c5", action="store_true", help="drop C5 from --configs")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 headline (profiling the single-pair configs)")
+    ap.add_argument("--config-cpu-seconds", type=float, default=3.0, help="CPU-baseline budget per single-pair config")
     ap.add_argument("--check", type=int, default=8, help="pairs of the timed run checked against the oracle "
                                                          "(N=1; with N>1 two per rank)")
     ap.add_argument("--dry-run", action="store_true", help="launcher/shard/gather only, gloo on CPU (tests)")
@@ -216,44 +223,182 @@ def cpu_baseline(src, tgt, iters: int, budget_s: float, all_budget_s: float) -> 
                                     f"share for one GPU)"}}
 
 
-# ------------------------------------------------------------------------------------------ C5
-def c5_measure(ctx, dev, iters: int = 20, reps: int = 10) -> dict:
-    """C5: 8,192-point scan vs a 65,540-point map (10 accumulated scans), 20 iterations,
-    one GPU.  The NN pass is priced against HBM with §8(d)'s formula on the work the device counts:
-    per launch N x (16 B query in + 8 B key out) + 16 B per examined target (sum_q K_q) + 24 B per
-    box test (lo/hi xyz) — every examination priced as a fresh read, never the re-reads beyond that
-    (DESIGN.md §6e)."""
-    import icp4r
-    from icp4r import synth
+# ------------------------------------------------------------------------------------------ single pairs
+LIB = os.path.join(ROOT, "icp-4dradar_amd", "icp4r", "_lib", "libicp4r.so")
+PMC_PATH = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
-    mp = synth.make_map_pair(0)
-    src, tgt = mp.src_xyzi(), mp.tgt_xyzi()
+
+def library_sha256() -> str | None:
+    """Hash of the library this run loads: a committed PMC figure is used only for the very build it
+    was measured on (profiles/pmc_traffic.json records the hash of the build tools/profile_round.sh
+    profiled); after any rebuild `traffic` is null until the profile is re-taken."""
+    import hashlib
+
+    try:
+        with open(os.environ.get("ICP4R_LIBRARY", LIB), "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
+def pmc_traffic(config: str, kernel: str, sha: str | None):
+    """(HBM bytes per launch of `kernel` in `config` from the committed FETCH_SIZE (x2, gfx950) +
+    WRITE_SIZE passes, or None, and a note saying why)."""
+    try:
+        with open(PMC_PATH) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None, "no profiles/pmc_traffic.json"
+    if not sha or pmc.get("library_sha256") != sha:
+        return None, "profiles/pmc_traffic.json was measured on another build of the library (sha256 differs)"
+    row = pmc.get("configs", {}).get(config, {}).get(kernel)
+    if not row or "hbm_bytes_per_launch" not in row:
+        return None, f"no PMC row for {kernel} in {config}"
+    return row["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({pmc.get('tag')}), same library build"
+
+
+# The sequential float folds of the PCL-numerics update (SURVEY App. A.4: Eigen's rowwise().sum() and
+# the cross-covariance, in correspondence order) are one dependent add chain per sum: two passes of n
+# dependent adds per iteration.  Measured cost per dependent add with the fold's LDS prefetch:
+# 6.4-6.7 cycles (tools/chain_bench.hip, DESIGN.md §5) at the 2.4 GHz max clock.
+CHAIN_CYCLES_PER_ADD = 6.4
+CLOCK_GHZ = 2.4
+
+
+def single_pair_cpu(src, tgt, oparams: dict, budget_s: float, fitness_passes: int) -> dict:
+    """The oracle on one pinned core, the node's call: align (+ its getFitnessScore) and, for the
+    icp4radar node, the second getFitnessScore (`iterative_closest_point.cpp:516,:520`)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / CPU baseline only
+
+    allowed = sorted(os.sched_getaffinity(0))
+    core = allowed[0]
+    os.sched_setaffinity(0, {core})
+    try:
+        o = oracle.align(src, tgt, **oparams)  # warm-up
+        per, t0 = [], time.perf_counter()
+        while (time.perf_counter() - t0) < budget_s and len(per) < 2000:
+            t1 = time.perf_counter()
+            o = oracle.align(src, tgt, **oparams)
+            if fitness_passes > 1:
+                oracle.fitness(src, tgt, o["T"])
+            per.append(time.perf_counter() - t1)
+        dt = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, set(allowed))
+    per_ms = np.array(per) * 1e3
+    return {"value": len(per) / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "per_pair_ms_median": float(np.median(per_ms)), "per_pair_ms_p90": float(np.percentile(per_ms, 90)),
+            "fitness_passes": fitness_passes,
+            "sample": f"the same pair registered {len(per)} times ({len(src)}/{len(tgt)} pts) by oracle/icp_oracle.c "
+                      f"(FLANN-style kd-tree NN + float Umeyama, -O2), 1 thread pinned to CPU {core}, {dt:.1f} s on "
+                      f"{_cpu_model()}"}
+
+
+def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams: dict, sha: str | None,
+                        reps: int, cpu_budget_s: float | None, fitness_passes: int, check: bool,
+                        hbm_formula: bool = False) -> dict:
+    """One pair per call (`iterative_closest_point.cpp:510-521` is one pair per frame; C5 the node's
+    scan-to-map call, `radar_odometry.cpp:386-411`), synchronous icp4r_align from host buffers.
+    value = registrations/s of the device time (HIP events around the whole launch sequence);
+    wall = the synchronous call incl. both clouds' PCIe upload and the result download.
+    roofline: the NN search kernel (nn_tile_kernel), FP32 VALU work counted on the device (evaluations
+    x 8 + box tests x 11 FLOP) over its average launch time (HIP events on its stream); for C5 also
+    priced against HBM with SURVEY §8(d)'s hash-grid byte formula.  The update's bound is the
+    sequential float fold chain (2 x n dependent adds per iteration), reported as `chain_floor_ms`."""
+    import icp4r
+
     n, m = len(src), len(tgt)
-    p = icp4r.default_params(max_iterations=iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-    r, _ = ctx.align(src, tgt, p)  # warm-up + result
+    r, _ = ctx.align(src, tgt, params)  # warm-up
     ctx.reset_timers()
-    t0 = time.perf_counter()
+    walls = []
     for _ in range(reps):
-        ctx.align(src, tgt, p)
-    wall_ms = (time.perf_counter() - t0) / reps * 1e3
-    batch_ms, _ = ctx.batch_time_ms()
+        t0 = time.perf_counter()
+        r, _ = ctx.align(src, tgt, params)
+        walls.append(time.perf_counter() - t0)
+    dev_ms, calls = ctx.batch_time_ms()
     nn_ms, nn_launches = ctx.kernel_time_ms()
+    upd_ms, upd_launches = ctx.stage_time_ms(icp4r.STAGE_UPDATE)
     st = ctx.nn_stats()
     evals = st["evaluations"] / max(nn_launches, 1)
     tests = st["box_tests"] / max(nn_launches, 1)
-    # algorithmic bytes per NN launch: queries in (16 B) + key out (8 B) + every examined target read
-    # once per examination (16 B, sum_q K_q) + the boxes tested (24 B: lo/hi xyz)
-    bytes_per_launch = n * (16 + 8) + 16 * evals + 24 * tests
-    achieved = bytes_per_launch / (nn_ms * 1e-3) / 1e9 if nn_ms > 0 else 0.0
-    return {"workload": f"C5: {n}-pt scan vs {m}-pt map (10 scans), {iters} iterations fixed + fitness, 1 GPU",
-            "registration_device_ms": batch_ms, "registration_wall_ms_incl_pcie": wall_ms,
-            "pairs_per_s": 1e3 / batch_ms if batch_ms > 0 else None,
-            "status": int(r.status), "iterations": int(r.iterations),
-            "roofline": {"bound": "hbm", "kernel": "nn (scan-to-map pass)", "avg_launch_ms": nn_ms,
-                         "launches_per_registration": nn_launches / reps, "examined_targets_per_launch": evals,
-                         "box_tests_per_launch": tests, "bytes_per_launch": bytes_per_launch,
-                         "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS},
-            "_src": src, "_tgt": tgt, "_T": r.matrix(), "_params": dict(max_iterations=iters)}
+    plan = icp4r.plan(1, n, m)
+    kernel = "nn_tile_kernel" if plan["pruned"] and not plan["lds"] else "nn_kernel"
+    flops = evals * FLOP_PER_PAIR_EVAL + tests * FLOP_PER_BOX_TEST
+    tflops = flops / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
+    traffic, traffic_note = pmc_traffic(name, kernel, sha)
+    roof = {"bound": "valu", "kernel": kernel, "achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": tflops / PEAK_FP32_TFLOPS, "traffic": traffic, "traffic_source": traffic_note,
+            "library_sha256": sha, "avg_launch_ms": nn_ms, "launches_per_registration": nn_launches / max(calls, 1),
+            "evaluations_per_launch": evals, "box_tests_per_launch": tests, "flop_per_launch": flops,
+            "evaluated_fraction_of_brute_force": evals / (n * m)}
+    if traffic is not None and nn_ms > 0:
+        roof["traffic_gbs"] = traffic / (nn_ms * 1e-3) / 1e9
+    if hbm_formula:
+        # SURVEY §8(d) hash-grid formula per NN launch: queries in (16 B) + key out (8 B) + 16 B per
+        # examined target (sum_q K_q) + 24 B per box tested (lo/hi xyz) — every examination priced as a
+        # fresh read.  nn_tile_kernel stages each target tile in LDS once per workgroup, so these are
+        # algorithmic bytes, not traffic: `traffic` above is the measured HBM bytes.
+        b = n * (16 + 8) + 16 * evals + 24 * tests
+        a = b / (nn_ms * 1e-3) / 1e9 if nn_ms > 0 else 0.0
+        roof["hbm_formula"] = {"bytes_per_launch": b, "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": a / PEAK_HBM_GBS}
+    iters = int(r.iterations)
+    floor_ms = 2 * n * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
+    out = {"workload": workload, "value": 1e3 / dev_ms if dev_ms > 0 else None, "unit": "pairs/s",
+           "registration_device_ms": dev_ms, "registration_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
+           "status": int(r.status), "iterations": iters, "plan": plan, "roofline": roof,
+           "update_kernel": {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms,
+                             "launches_per_registration": upd_launches / max(calls, 1),
+                             "bound": "latency: sequential float fold chains (PCL's summation order)",
+                             "chain_floor_ms": floor_ms, "frac_of_floor": floor_ms / upd_ms if upd_ms > 0 else None},
+           "nn_plus_update_share_of_device_time": (nn_ms * nn_launches + upd_ms * upd_launches) / max(calls, 1) / dev_ms
+           if dev_ms > 0 else None}
+    if check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker only: the registration above was timed without it
+
+        o = oracle.align(src, tgt, aligned=True, **oparams)
+        r2, al = ctx.align(src, tgt, params, want_aligned=True)  # (untimed: the aligned cloud too)
+        out["bit_exact_vs_oracle"] = bool((r.matrix() == o["T"]).all() and r.fitness == o["fitness"] and
+                                          iters == o["iterations"] and bytes(r2) == bytes(r) and
+                                          (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all())
+    if cpu_budget_s:
+        cpu = single_pair_cpu(src, tgt, oparams, cpu_budget_s, fitness_passes)
+        out["cpu_baseline"] = cpu
+        out["speedup_vs_cpu"] = out["value"] / cpu["value"] if out["value"] else None
+    return out
+
+
+def single_pair_configs(ctx, which: list[str], sha, cpu_s: float | None, check: bool) -> dict:
+    """C1, C2, C5 of BASELINE.json: one pair per call on one GPU."""
+    import icp4r
+    from icp4r import synth
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # parameters of the checker / CPU baseline only
+
+    fixed = dict(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    out = {}
+    if "C1" in which:  # the reference-default CPU config: PCL defaults (10 iterations, early stops live)
+        p = synth.make_pair(0, 2048)
+        out["c1"] = single_pair_measure(
+            ctx, "C1", "C1: 1 pair, 2048/2048-pt scans, PCL defaults (10 iterations max, early stops live) + fitness",
+            p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(), {"numerics": oracle.NUM_F32}, sha, reps=50,
+            cpu_budget_s=cpu_s, fitness_passes=2, check=check)
+    if "C2" in which:  # single 8k pair, 20 iterations
+        p = synth.make_pair(1, 8192)
+        out["c2"] = single_pair_measure(
+            ctx, "C2", "C2: 1 pair, 8192/8192-pt scans, 20 ICP iterations (fixed) + fitness",
+            p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed), sha,
+            reps=20, cpu_budget_s=cpu_s, fitness_passes=2, check=check)
+    if "C5" in which:  # 8k scan vs the 65,540-pt map of 10 accumulated scans (radar_odometry.cpp:386-411)
+        p = synth.make_map_pair(0)
+        out["c5"] = single_pair_measure(
+            ctx, "C5", "C5: 8192-pt scan vs 65540-pt map (10 accumulated scans), 20 iterations (fixed) + fitness",
+            p.src_xyzi(), p.tgt_xyzi(), icp4r.default_params(**fixed), dict(numerics=oracle.NUM_F32, **fixed), sha,
+            reps=10, cpu_budget_s=cpu_s, fitness_passes=1, check=check, hbm_formula=True)
+    return out
 
 
 # ------------------------------------------------------------------------------------------ GPU run
@@ -273,6 +418,18 @@ def run_gpu(args) -> int:
 
     import icp4r
     from icp4r import dist as idist
+
+    sha = library_sha256()
+    which = [c for c in args.configs.split(",") if c and not (args.no_c5 and c == "C5")]
+    if args.no_c3:  # the single-pair configs alone (tools/profile_round.sh profiles them this way)
+        ctx = icp4r.Context(dev.index)
+        out = single_pair_configs(ctx, which, sha, None if args.no_cpu else args.config_cpu_seconds, args.check > 0)
+        ctx.close()
+        if rank == 0:
+            print(json.dumps({"metric": _metric(), "configs_only": True, "library_sha256": sha, **out}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
     n = args.points
     P = args.pairs
@@ -428,10 +585,11 @@ def run_gpu(args) -> int:
     plan = icp4r.plan(P, n, n)
     kernel = "nn_lds_kernel" if plan["lds"] else "nn_pruned_kernel" if plan["pruned"] else "nn_kernel"
 
-    # C5 (rank 0 only; one GPU)
-    c5 = None
-    if rank == 0 and not args.no_c5:
-        c5 = c5_measure(ctx, dev)
+    # the single-pair configs C1, C2, C5 (rank 0 at N=1: one GPU each; their CPU baselines too)
+    configs = {}
+    if rank == 0 and world == 1 and which:
+        configs = single_pair_configs(ctx, which, sha, None if args.no_cpu else args.config_cpu_seconds,
+                                      args.check > 0)
 
     # checks on the TIMED results: statuses, iteration counts, and pairs of every rank / both pair
     # groups against the oracle (rank 0 regenerates those pairs' inputs from their seeds)
@@ -462,13 +620,7 @@ def run_gpu(args) -> int:
             check.append({"pair": int(g), "rank": int(g // P), "group": int((g % P) >= P // 2), "dt_m": dt, "dr_rad": dr,
                           "bit_exact": bool((T == o["T"]).all() and res[g]["fitness"] == o["fitness"])})
         ok = ok and all(c["dt_m"] <= 1e-4 and c["dr_rad"] <= 1e-4 for c in check)
-        if c5 is not None:
-            o = oracle.align(c5["_src"], c5["_tgt"], numerics=oracle.NUM_F32, mse_threshold_absolute=-1.0,
-                             transformation_epsilon=-1.0, **c5["_params"])
-            c5["bit_exact_vs_oracle"] = bool((c5["_T"] == o["T"]).all())
-    if c5 is not None:
-        for k in ("_src", "_tgt", "_T", "_params"):
-            c5.pop(k)
+    ok = ok and all(c.get("bit_exact_vs_oracle", True) and c["status"] == 0 for c in configs.values())
 
     total_pairs = world * P * args.steps
     value = total_pairs / elapsed
@@ -478,16 +630,9 @@ def run_gpu(args) -> int:
     flops_per_launch = evals_per_launch * FLOP_PER_PAIR_EVAL + tests_per_launch * FLOP_PER_BOX_TEST
     achieved_tflops = flops_per_launch / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     brute_equiv_tflops = P * n * n * FLOP_PER_PAIR_EVAL / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    traffic = None  # HBM bytes per launch from the committed PMC passes of THIS kernel and shape
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            if pmc.get("pairs") == P and pmc.get("points") == n and pmc.get("kernel") == kernel:
-                traffic = pmc.get("hbm_bytes_per_nn_launch")
-        except (OSError, ValueError):
-            traffic = None
+    # HBM bytes per launch from the committed PMC passes of THIS kernel, shape and library build
+    traffic, traffic_note = (pmc_traffic("C3", kernel, sha) if (P, n, args.iters) == (1024, 8192, 20)
+                             else (None, "profiles cover the default C3 shape only"))
 
     # cached-neighbour test kernel (HBM-bound; by default only the fitness pass's test runs here, the
     # iteration passes' tests are fused into fold_update_kernel's tail): per tested query X (16, .w =
@@ -550,6 +695,9 @@ def run_gpu(args) -> int:
                 "unit": "TFLOP/s",
                 "frac": achieved_tflops / PEAK_FP32_TFLOPS,
                 "traffic": traffic,
+                "traffic_source": traffic_note,
+                "traffic_gbs": traffic / (nn_ms * 1e-3) / 1e9 if traffic and nn_ms > 0 else None,
+                "library_sha256": sha,
                 "kernel": kernel,
                 "flop_per_launch": flops_per_launch,
                 "evaluations_per_launch": evals_per_launch,
@@ -572,7 +720,7 @@ def run_gpu(args) -> int:
             "gather": {"ms": gather_ms, "bytes": world * P * 96} if world > 1 else None,
             "cache_test_kernel": cache_test,
             "update_kernel": update,
-            "c5": c5,
+            **configs,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
             "batch_device_ms": batch_ms,

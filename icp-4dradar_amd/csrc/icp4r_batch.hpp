@@ -27,8 +27,10 @@ struct Plan {
 };
 
 int env_int(const char* name, int dflt);
-// Geometry of the NN pass for a batch shape.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO);
+// Geometry of the NN pass for a batch shape.  allow_lds = false keeps the batched LDS search out (a
+// caller whose index strides exceed what it stages, icp4r_gicp.cpp), so every other field of the
+// plan is the one of the plan that runs.
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO, bool allow_lds = true);
 // icp4r_params -> the kernels' KParams (validates).
 int make_kparams(const icp4r_params* p, icp4r::KParams* kp);
 // Size the context's workspace for a plan and fill WorkArgs.

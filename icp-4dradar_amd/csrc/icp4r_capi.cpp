@@ -96,7 +96,7 @@ int env_int(const char* name, int dflt) {
 //    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
 //    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/tune_sweep.py, profiles/tune_r01.jsonl).
 // Tuning overrides (tools/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
@@ -130,15 +130,17 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode) {
         pl.chunk_sb = cs;
         pl.chunks = nsb > 0 ? (nsb + cs - 1) / cs : 1;
         pl.blocks *= pl.chunks;
-        // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides)
+        // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides).  Its
+        // query records pack the source index and sorted position in 14 bits each (kLdsMaxSources),
+        // so larger sources take the tiled search instead.
         const int lds = env_int("ICP4R_NN_LDS", -1);
-        const bool fits = pl.leaf == 16 && max_m <= kLdsMaxTargets;
+        const bool fits = allow_lds && pl.leaf == 16 && max_m <= kLdsMaxTargets && max_n <= kLdsMaxSources;
         pl.lds = fits && (lds == 1 || (lds < 0 && npairs >= kLdsMinPairs));
         if (pl.lds) {
             pl.q = 2;
             pl.blocks = npairs;
             pl.chunks = 1;
-            pl.cache = max_n <= kCacheMaxN && env_int("ICP4R_NN_CACHE", 1) != 0;
+            pl.cache = env_int("ICP4R_NN_CACHE", 1) != 0;
         } else {
             // single pairs / small batches: the LDS-tiled search (target tiles of 8192 x query parts)
             pl.tile = pl.leaf == 16 && max_m < (1 << 19) && env_int("ICP4R_NN_TILE", 1) != 0;
@@ -316,10 +318,12 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
         HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev, test_fused));
         return ICP4R_OK;
     }
+    if (pl.tile) {  // the events bracket nn_tile_kernel itself (not its seed / record kernels)
+        HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, st, ne->start, ne->stop));
+        return ICP4R_OK;
+    }
     HIP_TRY(hipEventRecord(ne->start, st));
-    if (pl.tile) {
-        HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, st));
-    } else if (pl.pruned) {
+    if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, pl.chunk_sb, pl.chunks, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));

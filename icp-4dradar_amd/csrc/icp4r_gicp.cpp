@@ -72,13 +72,14 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     if (npairs <= 0) return ICP4R_OK;
     const int mn = max_n > 0 ? max_n : 1;
     const int mm = max_m > 0 ? max_m : 1;
-    Plan pl = make_plan(npairs, mn, max_m, ICP4R_NN_AUTO);
+    // pruned plans index the source too (its k-NN covariances): the index strides fit both clouds,
+    // and the batched search, which stages t_stride targets, only runs when those fit its LDS
+    const int idx_both = max_n > max_m ? max_n : max_m;
+    Plan pl = make_plan(npairs, mn, max_m, ICP4R_NN_AUTO, idx_both <= kLdsMaxTargets);
     pl.cache = false;  // gicp_iter_kernel moves X without maintaining the cached-neighbour bounds
     WorkArgs w;
     int rc;
-    // pruned plans index the source too (its k-NN covariances): the index strides fit both clouds
-    const int idx_m = pl.pruned ? (max_n > max_m ? max_n : max_m) : max_m;
-    if (pl.lds && idx_m > kLdsMaxTargets) pl.lds = false;  // the batched search stages t_stride targets
+    const int idx_m = pl.pruned ? idx_both : max_m;
     if ((rc = setup_work(ctx, pl, npairs, max_n, idx_m, false, st, w))) return rc;
     const int64_t xs = w.x_stride;
     const int64_t ts = mm;

@@ -101,7 +101,10 @@ __host__ __device__ inline int32_t key_idx(NNKey k) { return (int32_t)(uint32_t)
 // Workspace, pair p at [p * stride, ...) of each array.
 struct WorkArgs {
     float4* X;          // input_transformed [npairs * x_stride]
-    NNKey* nn_key;      // per-query NN key   [npairs * x_stride]; splits > 1 merge by atomicMin
+    NNKey* nn_key;      // per-query NN key   [npairs * x_stride]; splits > 1 merge by atomicMin.  After
+                        // a fused fitness pass (pair_cache_test, fitness) a HIT's index bits hold its NN's
+                        // SORTED target position, not the original index: only key_d2 is meaningful
+                        // there (finish_kernel reads d² only; nothing may read key_idx after that pass)
     PairState* state;   // [npairs]
     int64_t x_stride;   // >= max source points per pair
     int32_t splits;     // brute force: target splits per pair (1 for batches; >1 for single-pair latency)
@@ -163,7 +166,7 @@ hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, 
 // the pruned plan's LDS-tiled search: nn_seed_kernel, nn_tile_kernel (target tiles x query parts),
 // corr_kernel (records, when the update reads them)
 hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
-                          int first, hipStream_t st);
+                          int first, hipStream_t st, hipEvent_t tile_start = nullptr, hipEvent_t tile_stop = nullptr);
 // events recorded around the batched NN's stages (any may be null)
 struct NNLdsEvents {
     hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;
@@ -172,6 +175,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
                          int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused = 0);
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
+constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
                          hipStream_t st,
                          int tail_test = 0);

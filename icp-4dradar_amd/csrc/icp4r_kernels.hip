@@ -1497,7 +1497,8 @@ __device__ __forceinline__ int lds_swz(int p) { return p ^ ((p >> 4) & (kLdsLeaf
 // (bits 14..27): the test reads one record for the miss bitmap's bit and for the search record it
 // writes (sq / sm: the next search's seed is that target position, no index lookup).  Sizes:
 // <= kCacheMaxN = 2^14 sources, <= 8192 targets on the batched plan.
-static_assert(kCacheMaxN <= (1 << kNtPosShift) && kLdsTargets <= (1 << kNtPosShift), "nn_t.w packing");
+static_assert(kCacheMaxN <= (1 << kNtPosShift) && kLdsTargets <= (1 << kNtPosShift) && kLdsMaxSources == (1 << kNtPosShift),
+              "nn_t.w / query record packing");
 __device__ __forceinline__ float nt_pack(int tpos, int pos) {
     return __uint_as_float((uint32_t)tpos | ((uint32_t)pos << kNtPosShift));
 }
@@ -3273,7 +3274,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
         auto fill = [&](int c) {
             const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
             for (int o = threadIdx.x - 64; o < len; o += kFinWG - 64) {
-                const float d2 = key_d2(w.nn_key[slot0 + base + o]);
+                const float d2 = key_d2(w.nn_key[slot0 + base + o]);  // (d² only: see WorkArgs::nn_key)
                 const bool in = (double)d2 <= a.kp.fit_max_range;
                 chunk[c & 1][o] = in ? d2 : 0.0f;
                 fcnt += in ? 1 : 0;
@@ -3381,9 +3382,11 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
                          int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused) {
-    if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0) return hipErrorInvalidValue;
+    // (query records: source index and sorted position in kNtPosShift bits each, every mode)
+    if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0 || max_n > (1 << kNtPosShift))
+        return hipErrorInvalidValue;
     const bool cache = w.nn_u != nullptr;
-    if (cache && (w.x_stride > kCacheMaxN || !w.sq || !w.qv || !w.need || !w.miss_cnt || !w.nn_t || !w.defer_xform))
+    if (cache && (max_n > kCacheMaxN || !w.sq || !w.qv || !w.need || !w.miss_cnt || !w.nn_t || !w.defer_xform))
         return hipErrorInvalidValue;
     if (!w.plist || !w.plist_n || !w.queue || !w.qv || !w.qm) return hipErrorInvalidValue;
     hipError_t e;
@@ -3407,12 +3410,15 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
 }
 
 hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
-                          int first, hipStream_t st) {
+                          int first, hipStream_t st, hipEvent_t tile_start, hipEvent_t tile_stop) {
     if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0)
         return hipErrorInvalidValue;
+    hipError_t e;
     hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass, first);
     const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + kLdsWG - 1) / kLdsWG, npairs);
+    if (tile_start && (e = hipEventRecord(tile_start, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass);
+    if (tile_stop && (e = hipEventRecord(tile_stop, st)) != hipSuccess) return e;
     if (w.corr != nullptr && !fitness_pass)  // records from the merged keys
         hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();

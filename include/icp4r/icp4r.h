@@ -160,7 +160,8 @@ int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream);
 
 /* Device-time accounting with HIP events on the launch stream (used by bench.py for the roofline):
  * icp4r_kernel_time_ms: average duration of the NN kernel launches (the dominant kernel: the batched
- *                       search nn_lds_kernel, or the whole NN launch of the other plans)
+ *                       search nn_lds_kernel, the tiled search nn_tile_kernel, or the whole NN
+ *                       launch of the other plans)
  *                       recorded since the last reset, and how many there were;
  * icp4r_batch_time_ms:  average duration of whole registration calls (all launches of a batch). */
 int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
@@ -169,8 +170,8 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx);
 
 /* Average device time of one stage of the registrations since the last reset (HIP events on the
  * launch stream), and how many launches it averages.  ICP4R_STAGE_NN is what icp4r_kernel_time_ms
- * reports: the batched search kernel (nn_lds_kernel) of the LDS plan, the whole NN launch of the
- * others; ICP4R_STAGE_NN_TEST the cached-neighbour test kernel; ICP4R_STAGE_UPDATE the Umeyama /
+ * reports: the batched search kernel (nn_lds_kernel) of the LDS plan, nn_tile_kernel of the tiled
+ * plan, the whole NN launch of the others; ICP4R_STAGE_NN_TEST the cached-neighbour test kernel; ICP4R_STAGE_UPDATE the Umeyama /
  * convergence update (generalized ICP: its Gauss-Newton / LM iteration kernel); ICP4R_STAGE_BATCH a
  * whole registration call; ICP4R_STAGE_GICP_COV the generalized ICP's covariance kernel. */
 typedef enum icp4r_stage {

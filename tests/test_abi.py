@@ -79,7 +79,12 @@ def test_plan_geometry(monkeypatch):
 
     big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
     assert big["pruned"] and big["lds"] and big["q"] == 2 and big["leaf"] == 16 and big["nn_blocks"] == 1024
-    assert big["cache"] and not icp4r.plan(1024, 16385, 8192)["cache"]  # cached-neighbour test: n <= 16384
+    assert big["cache"] and icp4r.plan(1024, 16384, 8192)["lds"]
+    # the batched search's query records hold 14-bit source indices: larger sources take the tiled search
+    assert not icp4r.plan(1024, 16385, 8192)["lds"] and not icp4r.plan(1024, 16385, 8192)["cache"]
+    monkeypatch.setenv("ICP4R_NN_LDS", "1")
+    assert not icp4r.plan(8, 20000, 8192)["lds"]  # ... even when forced
+    monkeypatch.delenv("ICP4R_NN_LDS")
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
     single = icp4r.plan(1, 8192, 8192)  # C2: LDS-tiled search, one target tile x 8 query parts of 1024

@@ -177,7 +177,7 @@ def test_target_split_equals_unsplit(gpu_ctx):
 
 
 @pytest.mark.parametrize("lds,cache,tile", [("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")])
-@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map", "big_src"])
+@pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map", "big_src", "huge_src"])
 def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
     """Pruned (LDS target tiles x query parts, the scalar-cache stream, or with the target set in LDS
     and per-query work lists, with or without the cached-neighbour test), brute-force and packed
@@ -218,6 +218,10 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
     elif case == "big_src":  # sources beyond one kd build (own index, not the target's tree) beside small ones
         shapes = [(12000, 8000), (16384, 4096), (9000, 8192), (8192, 8192), (500, 300)]
         pairs = [_pair(350 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    elif case == "huge_src":  # sources past the batched search's 14-bit query records (tiled search)
+        shapes = [(20000, 8000), (16385, 4096), (16384, 8192), (700, 300)]
+        pairs = [_pair(360 + k, n, m) for k, (n, m) in enumerate(shapes)]
+        assert not icp4r.plan(len(pairs), 20000, 8192)["lds"]
     else:
         sp, tp = _pair(340, 3000, 6000)
         pairs = [(sp, np.concatenate([tp, tp]))]
@@ -532,3 +536,32 @@ def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, monkeypatch):
                              mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
         assert (default[k]["T"].reshape(4, 4).T == o["T"]).all(), k
         assert default[k]["fitness"] == o["fitness"], k
+
+
+@pytest.mark.parametrize("fixed", [True, False])
+def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
+    """BASELINE.json configs[4] at its own size (the scan-to-map registration of
+    /root/reference/src/radar_odometry.cpp:386-411): an 8,192-point scan against a 65,540-point map
+    (10 accumulated scans, synth.make_map_pair(0)), 20 iterations (fixed as the bench runs it, and
+    with PCL's early stops live) plus the fitness pass, through icp4r_align — the tiled search over
+    9 target tiles.  T, fitness, iteration count, convergence state and the aligned cloud bit-equal
+    to the oracle."""
+    import icp4r
+    from icp4r import synth
+
+    mp = synth.make_map_pair(0)
+    src, tgt = mp.src_xyzi(), mp.tgt_xyzi()
+    assert (len(src), len(tgt)) == (8192, 65540)
+    plan = icp4r.plan(1, len(src), len(tgt))
+    assert plan["pruned"] and not plan["lds"]
+    kw = dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0) if fixed else {}
+    r, al = gpu_ctx.align(src, tgt, icp4r.default_params(max_iterations=20, **kw), want_aligned=True)
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=20, aligned=True, **kw)
+    assert r.status == 0 and r.iterations == o["iterations"]
+    if fixed:
+        assert r.iterations == 20
+    assert r.convergence_state == o["convergence_state"] and bool(r.converged) == o["converged"]
+    assert (r.matrix() == o["T"]).all()
+    assert r.fitness == o["fitness"]
+    assert r.n_correspondences == o["n_correspondences"]
+    assert (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all()

@@ -1,115 +1,119 @@
-"""Summarise rocprofv3 output into profiles/ (run on the dev box after gpurun merged gpurun_out/).
+"""Summarise rocprofv3 output of one benchmark config into profiles/ (tools/profile_round.sh runs it).
 
-    python tools/pmc_traffic.py --stats gpurun_out/prof_stats --fetch gpurun_out/prof_fetch \
-        --write gpurun_out/prof_write --pairs 1024 --points 8192 --tag r01
+    python tools/pmc_traffic.py --config C3 --stats DIR --fetch DIR --write DIR --tag round3
 
-* kernel stats (--kernel-trace --stats): per-kernel calls / average duration -> profiles/kernel_stats_<tag>.csv
-* HBM traffic of the NN kernel per launch from the PMC passes, corrected as MI355X_MICROARCH.md §HBM
-  prescribes: FETCH_SIZE reports half the bytes of a wide coalesced streaming read on gfx950, so it
-  is doubled; WRITE_SIZE is taken as-is.  Units: FETCH_SIZE / WRITE_SIZE are in KiB.
-  -> profiles/pmc_traffic.json (read by bench.py for roofline.traffic), with a per-kernel table
-  (`kernels`) for every kernel of --also (fold_update_kernel, index_kernel, ...): mean FETCH
-  (doubled) + WRITE bytes per launch and the average duration
+* kernel stats (--kernel-trace --stats): copied to profiles/<tag>/kernel_stats_<config>.csv
+* HBM traffic per launch of every kernel of --kernels from the PMC passes, corrected as
+  MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE reports half the bytes of a wide coalesced streaming
+  read on gfx950, so it is doubled; WRITE_SIZE is taken as-is.  Units: FETCH_SIZE / WRITE_SIZE are
+  in KiB.  Launches differ per ICP pass: the mean over the launches matches the average launch time.
+  -> profiles/pmc_traffic.json, under configs[<config>][<kernel>], stamped with the sha256 of the
+  library build that was profiled (bench.py uses a row only when its own library has that hash).
 """
 from __future__ import annotations
 
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "icp-4dradar_amd", "icp4r", "_lib", "libicp4r.so")
+OUT = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+KERNELS = ("nn_lds_kernel,nn_tile_kernel,fold_update_kernel,index_kernel,src_order_kernel,index_refine_kernel,"
+           "nn_seed_kernel,nn_cache_test_kernel,nn_order_kernel,init_kernel,fitness_prep_kernel,finish_kernel")
 
 
 def find(d: str, pattern: str) -> list[str]:
     return sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
 
 
-def counters(d: str, name: str, kernel_sub: str) -> list[float]:
+def short(name: str) -> str:
+    """'void icp4r::nn_lds_kernel<true>(icp4r::PairArgs, ...)' -> 'nn_lds_kernel'."""
+    s = name.split("(")[0].split("<")[0]
+    return s.rsplit("::", 1)[-1].replace("void ", "").strip()
+
+
+def counters(d: str, name: str, kernel: str) -> list[float]:
     vals = []
     for path in find(d, "*counter_collection.csv"):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if row.get("Counter_Name") == name and kernel_sub in row.get("Kernel_Name", ""):
+                if row.get("Counter_Name") == name and short(row.get("Kernel_Name", "")) == kernel:
                     vals.append(float(row["Counter_Value"]))
     return vals
 
 
+def stats(d: str) -> dict:
+    out = {}
+    for path in find(d, "*kernel_stats.csv"):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                k = short(r["Name"])
+                out[k] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"]),
+                          "percentage": float(r.get("Percentage", "nan"))}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True, help="C1 / C2 / C3 / C5 (bench.py's config names)")
     ap.add_argument("--stats")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
-    ap.add_argument("--pairs", type=int, default=1024)
-    ap.add_argument("--points", type=int, default=8192)
-    ap.add_argument("--tag", default="round1", help="profiles/<tag>/ receives the kernel stats")
-    ap.add_argument("--kernel", default="nn_lds_kernel", help="kernel name (substring match in the PMC CSV)")
-    ap.add_argument("--also", default="fold_update_kernel,index_kernel,nn_cache_test_kernel,nn_order_kernel,init_kernel,"
-                                      "fitness_prep_kernel,finish_kernel",
-                    help="comma-separated kernels for the per-kernel traffic table")
+    ap.add_argument("--tag", default="round3", help="profiles/<tag>/ receives the kernel stats")
+    ap.add_argument("--kernels", default=KERNELS)
+    ap.add_argument("--library", default=LIB)
     a = ap.parse_args()
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    out = {"pairs": a.pairs, "points": a.points, "kernel": a.kernel, "tag": a.tag}
+    with open(a.library, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    try:
+        with open(OUT) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        doc = {}
+    if doc.get("library_sha256") != sha:  # rows of another build are stale: start over
+        doc = {"library_sha256": sha, "configs": {}}
+    doc["tag"] = a.tag
+    doc["note"] = ("HBM bytes per launch: FETCH_SIZE x 2 (gfx950: FETCH_SIZE reports half of a wide streaming "
+                   "read) + WRITE_SIZE, KiB -> bytes, mean over the launches of the profiled run "
+                   "(MI355X_MICROARCH.md §HBM); avg_ns from the separate --kernel-trace --stats run")
+    st = stats(a.stats) if a.stats else {}
     if a.stats:
-        st = find(a.stats, "*kernel_stats.csv")
-        if st:
-            dst = os.path.join(ROOT, "profiles", a.tag, "kernel_stats.csv")
+        src = find(a.stats, "*kernel_stats.csv")
+        if src:
+            dst = os.path.join(ROOT, "profiles", a.tag, f"kernel_stats_{a.config}.csv")
             os.makedirs(os.path.dirname(dst), exist_ok=True)
-            shutil.copy(st[0], dst)
-            with open(st[0]) as f:
-                for row in csv.DictReader(f):
-                    if a.kernel in row["Name"]:
-                        out.setdefault("stats", []).append({k: row[k] for k in ("Name", "Calls", "AverageNs", "Percentage")
-                                                            if k in row})
-    if a.fetch:
-        fs = counters(a.fetch, "FETCH_SIZE", a.kernel)
-        if fs:
-            kib = statistics.fmean(fs)  # launches differ per ICP pass: the mean matches the avg launch time
-            out["fetch_size_kib_mean"] = kib
-            out["fetch_bytes_corrected"] = 2.0 * kib * 1024
-            out["fetch_dispatches"] = len(fs)
-    if a.write:
-        ws = counters(a.write, "WRITE_SIZE", a.kernel)
-        if ws:
-            kib = statistics.fmean(ws)
-            out["write_size_kib_mean"] = kib
-            out["write_bytes"] = kib * 1024
-            out["write_dispatches"] = len(ws)
-    if "fetch_bytes_corrected" in out and "write_bytes" in out:
-        out["hbm_bytes_per_nn_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
-
+            shutil.copy(src[0], dst)
     table = {}
-    for k in [a.kernel] + [x for x in a.also.split(",") if x]:
+    for k in [x for x in a.kernels.split(",") if x]:
         row = {}
         fs = counters(a.fetch, "FETCH_SIZE", k) if a.fetch else []
         ws = counters(a.write, "WRITE_SIZE", k) if a.write else []
         if fs:
-            row["fetch_bytes_corrected"] = 2.0 * statistics.fmean(fs) * 1024
-            row["dispatches"] = len(fs)
+            row["fetch_size_kib_mean"] = statistics.fmean(fs)
+            row["fetch_bytes_corrected"] = 2.0 * row["fetch_size_kib_mean"] * 1024
+            row["fetch_dispatches"] = len(fs)
         if ws:
-            row["write_bytes"] = statistics.fmean(ws) * 1024
+            row["write_size_kib_mean"] = statistics.fmean(ws)
+            row["write_bytes"] = row["write_size_kib_mean"] * 1024
+            row["write_dispatches"] = len(ws)
         if fs and ws:
             row["hbm_bytes_per_launch"] = row["fetch_bytes_corrected"] + row["write_bytes"]
-        if a.stats:
-            for path in find(a.stats, "*kernel_stats.csv"):
-                with open(path) as f:
-                    for r in csv.DictReader(f):
-                        if k in r["Name"]:
-                            row["avg_ns"] = float(r["AverageNs"])
-                            row["calls"] = int(r["Calls"])
+        if k in st:
+            row.update(st[k])
         if "hbm_bytes_per_launch" in row and "avg_ns" in row:
             row["hbm_gbs"] = row["hbm_bytes_per_launch"] / row["avg_ns"]
         if row:
             table[k] = row
-    out["kernels"] = table
-
-    if a.fetch or a.write:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-            json.dump(out, f, indent=1)
-    print(json.dumps(out, indent=1))
+    doc.setdefault("configs", {})[a.config] = table
+    with open(OUT, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(json.dumps({a.config: table}, indent=1))
 
 
 if __name__ == "__main__":
