@@ -72,6 +72,9 @@ def parse(argv=None):
     ap.add_argument("--config-cpu-seconds", type=float, default=3.0, help="CPU-baseline budget per single-pair config")
     ap.add_argument("--check", type=int, default=8, help="pairs of the timed run checked against the oracle "
                                                          "(N=1; with N>1 two per rank)")
+    ap.add_argument("--gather", choices=("icp4r", "torch"), default="icp4r",
+                    help="N>1: the results' all-gather through the library's RCCL communicator "
+                         "(icp4r_gather_results, include/icp4r/icp4r_multi.h) or torch.distributed's")
     ap.add_argument("--dry-run", action="store_true", help="launcher/shard/gather only, gloo on CPU (tests)")
     return ap.parse_args(argv)
 
@@ -454,9 +457,20 @@ def run_gpu(args) -> int:
     batch = mk_batch(src, tgt)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    comm = None
+    if world > 1 and args.gather == "icp4r":
+        # the library's own RCCL communicator (one rank per GPU); rank 0's id reaches the others over the
+        # torch.distributed store
+        uid = [icp4r.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = icp4r.Comm(ctx, world, rank, uid[0])
+
     def gather():
         if world > 1:
-            idist.gather_results(results, world, out=gathered)
+            if comm is not None:  # icp4r_gather_results: ncclAllGather of the device-written rows
+                comm.gather(results.data_ptr(), world * P, gathered.data_ptr(), stream)
+            else:
+                idist.gather_results(results, world, out=gathered)
 
     def step():
         ctx.align_batch_device(batch, params, results.data_ptr(), stream)
@@ -717,7 +731,9 @@ def run_gpu(args) -> int:
                         "tflops = n*m*8 per NN pass / search time. See DESIGN.md §5",
             },
             "incl_upload": upload,
-            "gather": {"ms": gather_ms, "bytes": world * P * 96} if world > 1 else None,
+            "gather": {"ms": gather_ms, "bytes": world * P * 96,
+                       "via": "icp4r_gather_results (library RCCL communicator, ncclAllGather)" if comm is not None
+                       else "torch.distributed all_gather_into_tensor (RCCL)"} if world > 1 else None,
             "cache_test_kernel": cache_test,
             "update_kernel": update,
             **configs,
@@ -729,6 +745,9 @@ def run_gpu(args) -> int:
             "result_diag": diag,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.check()
+        comm.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

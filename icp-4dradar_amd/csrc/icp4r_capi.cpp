@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -710,17 +711,33 @@ int icp4r_align_batch_host(icp4r_ctx* ctx, const float* src, const int64_t* src_
     if (!ctx || !results || npairs < 0) return fail(ICP4R_E_INVALID, "bad arguments");
     if (npairs == 0) return ICP4R_OK;
     if (!src_off || !src_n || !tgt_off || !tgt_n) return fail(ICP4R_E_INVALID, "NULL offset/count array");
-    int64_t ns = 0, nt = 0;
+    // only the point ranges the pairs cover are uploaded, offsets rebased to them (a shard of a larger
+    // host batch, icp4r_align_batch_multi, uploads its own points only)
+    int64_t s_lo = INT64_MAX, s_hi = 0, t_lo = INT64_MAX, t_hi = 0;
     int32_t max_n = 0, max_m = 0;
     for (int32_t p = 0; p < npairs; ++p) {
         if (src_n[p] < 0 || tgt_n[p] < 0 || src_off[p] < 0 || tgt_off[p] < 0)
             return fail(ICP4R_E_INVALID, "pair %d: negative offset/count", p);
-        if (src_off[p] + src_n[p] > ns) ns = src_off[p] + src_n[p];
-        if (tgt_off[p] + tgt_n[p] > nt) nt = tgt_off[p] + tgt_n[p];
+        if (src_n[p] > 0) {
+            s_lo = std::min<int64_t>(s_lo, src_off[p]);
+            s_hi = std::max<int64_t>(s_hi, src_off[p] + src_n[p]);
+        }
+        if (tgt_n[p] > 0) {
+            t_lo = std::min<int64_t>(t_lo, tgt_off[p]);
+            t_hi = std::max<int64_t>(t_hi, tgt_off[p] + tgt_n[p]);
+        }
         if (src_n[p] > max_n) max_n = src_n[p];
         if (tgt_n[p] > max_m) max_m = tgt_n[p];
     }
+    if (s_lo > s_hi) s_lo = s_hi = 0;
+    if (t_lo > t_hi) t_lo = t_hi = 0;
+    const int64_t ns = s_hi - s_lo, nt = t_hi - t_lo;
     if ((ns > 0 && !src) || (nt > 0 && !tgt)) return fail(ICP4R_E_INVALID, "NULL cloud data");
+    std::vector<int64_t> so((size_t)npairs), to((size_t)npairs);
+    for (int32_t p = 0; p < npairs; ++p) {
+        so[p] = src_n[p] > 0 ? src_off[p] - s_lo : 0;
+        to[p] = tgt_n[p] > 0 ? tgt_off[p] - t_lo : 0;
+    }
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     HIP_TRY(ctx->src.ensure((size_t)(ns > 0 ? ns : 1) * 16));
@@ -731,10 +748,10 @@ int icp4r_align_batch_host(icp4r_ctx* ctx, const float* src, const int64_t* src_
     HIP_TRY(ctx->tgt_n.ensure((size_t)npairs * 4));
     HIP_TRY(ctx->results.ensure((size_t)npairs * sizeof(icp4r_result)));
     if (guess) HIP_TRY(ctx->guess.ensure((size_t)npairs * 64));
-    if (ns > 0) HIP_TRY(hipMemcpyAsync(ctx->src.p, src, (size_t)ns * 16, hipMemcpyHostToDevice, st));
-    if (nt > 0) HIP_TRY(hipMemcpyAsync(ctx->tgt.p, tgt, (size_t)nt * 16, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, src_off, (size_t)npairs * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, tgt_off, (size_t)npairs * 8, hipMemcpyHostToDevice, st));
+    if (ns > 0) HIP_TRY(hipMemcpyAsync(ctx->src.p, src + 4 * s_lo, (size_t)ns * 16, hipMemcpyHostToDevice, st));
+    if (nt > 0) HIP_TRY(hipMemcpyAsync(ctx->tgt.p, tgt + 4 * t_lo, (size_t)nt * 16, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->src_off.p, so.data(), (size_t)npairs * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ctx->tgt_off.p, to.data(), (size_t)npairs * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->src_n.p, src_n, (size_t)npairs * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ctx->tgt_n.p, tgt_n, (size_t)npairs * 4, hipMemcpyHostToDevice, st));
     if (guess) HIP_TRY(hipMemcpyAsync(ctx->guess.p, guess, (size_t)npairs * 64, hipMemcpyHostToDevice, st));

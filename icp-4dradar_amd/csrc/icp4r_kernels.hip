@@ -27,6 +27,7 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "icp4r_device.hpp"
 #include "icp4r_internal.hpp"
@@ -2288,8 +2289,15 @@ struct TileShared {
 };
 constexpr int kTileMaxM = 1 << (32 - kLdsPosBits);  // target indices that fit the local key
 
-__global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w, int fitness_pass) {
+//
+// One tile (every target of the pass fits one tile: C1, C2), `first` >= 0: the workgroup owns its
+// queries' whole search, so the seed (the previous match; first pass: the target at the same
+// relative sorted position — nn_seed_kernel's rule) is evaluated here, the key is stored, not merged,
+// and the correspondence record is written from the winner's LDS slot — one launch per NN pass
+// instead of three (seed, search, records), two kernel boundaries fewer per ICP iteration.
+__global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
     __shared__ TileShared sh;
+    const bool own = first >= 0;  // (single tile: launched with gridDim.x == 1)
     const int tile = blockIdx.x, part = blockIdx.y, p = blockIdx.z;
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
@@ -2343,10 +2351,18 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     uint16_t* ring = sh.items[wave];
     NNKey* key = w.nn_key + xs0;
     const bool live = r0 + lane < n;
-    const int o = w.sperm[xs0 + (live ? r0 + lane : r0)];  // idle lanes shadow the run's first query
+    const int sq = live ? r0 + lane : r0;
+    const int o = w.sperm[xs0 + sq];  // idle lanes shadow the run's first query
     const float4 v = w.X[xs0 + o];
-    const NNKey k0 = key[o];
+    NNKey k0 = key[o];
     const float x = v.x, y = v.y, z = v.z;
+    if (own) {  // the seed (nn_seed_kernel's rule), evaluated at the query's current position
+        const uint32_t j = (first && !seed_key(k0, m))
+                               ? __float_as_uint(w.tsort[(int64_t)p * w.t_stride + ((int64_t)sq * m) / n].w)
+                               : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+        const float4 t = a.tgt[uload(a.tgt_off + p) + j];
+        k0 = make_key(l2_simple(x, y, z, t.x, t.y, t.z), j);
+    }
     // the current key in the tile's encoding, ranked after every real target of the same (d², index)
     const NNKey init = make_key(key_d2(k0), ((uint32_t)key_idx(k0) << kLdsPosBits) | ((1u << kLdsPosBits) - 1));
     bestl[lane] = init;
@@ -2422,7 +2438,23 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     }
     if (tail != head) drain(tail - head);
     const NNKey kb = bestl[lane];
-    if (live && kb < init) atomicMin(&key[o], make_key(key_d2(kb), lk_idx(kb)));
+    if (own) {
+        // the seed target lies in the tile and its block's bound cannot prune it, so the winner is a
+        // real LDS slot; the sentinel position (kb == init) is handled all the same
+        const NNKey ko = kb < init ? make_key(key_d2(kb), lk_idx(kb)) : k0;
+        if (live) {
+            key[o] = ko;
+            if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence records
+                const float4 t = kb < init ? [&] {
+                    const v4f c = sh.tl[lds_swz((int)lk_pos(kb))];
+                    return make_float4(tl_x(c), tl_y(c), tl_z(c), 0.f);
+                }() : a.tgt[uload(a.tgt_off + p) + key_idx(k0)];
+                write_corr_t(w, a, p, o, x, y, z, key_d2(ko), t);
+            }
+        }
+    } else if (live && kb < init) {
+        atomicMin(&key[o], make_key(key_d2(kb), lk_idx(kb)));
+    }
     if (lane == 0) {
         count_add(w.evals, 0, evals);
         count_add(w.evals, 1, tests);
@@ -3414,12 +3446,18 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
     if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0)
         return hipErrorInvalidValue;
     hipError_t e;
-    hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass, first);
     const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + kLdsWG - 1) / kLdsWG, npairs);
+    // one tile: the search kernel seeds, stores and writes the records itself (ICP4R_TILE_OWN=0: the
+    // three-launch form, for A/B)
+    static const int own_env = getenv("ICP4R_TILE_OWN") ? atoi(getenv("ICP4R_TILE_OWN")) : 1;
+    const bool own = grid.x == 1 && own_env != 0;
+    if (!own)
+        hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass,
+                           first);
     if (tile_start && (e = hipEventRecord(tile_start, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass);
+    hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass, own ? first : -1);
     if (tile_stop && (e = hipEventRecord(tile_stop, st)) != hipSuccess) return e;
-    if (w.corr != nullptr && !fitness_pass)  // records from the merged keys
+    if (!own && w.corr != nullptr && !fitness_pass)  // records from the merged keys
         hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();
 }

@@ -17,8 +17,8 @@
 // the 20-frame submap publisher (:577-633) and stdout are not reproduced; the node's RANSAC of the
 // previous scan (:465-493) feeds nothing that is written and is skipped.
 //
-//   icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N]
-//                    [--use-icp-result CSV]
+//   icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--devices D0,D1,...] [--seed S]
+//                    [--max-iterations N] [--use-icp-result CSV]
 //
 // Empty scans (:505 vs :698-699): the node pushes every frame's points onto cloud_src_in /
 // cloud_tar_in and clears them only inside `if (cloud_tar_in->size() && cloud_src_in->size())`.
@@ -40,6 +40,9 @@
 // --batch: every frame's ICP is independent of the poses (identity guess), so all frames are
 // registered in ONE device batch (icp4r_align_batch_host) and composed afterwards — identical output
 // to the per-frame loop (the batch path is bit-identical to single calls), one launch sequence.
+// --devices D0,D1,... (with --batch): the batch sharded over those devices — one context each,
+// contiguous blocks of frames, all shards at once (icp4r_align_batch_multi, include/icp4r/icp4r_multi.h);
+// the output is byte-identical to the one-device batch.
 #include <sys/stat.h>
 
 #include <array>
@@ -58,6 +61,7 @@
 
 #include "icp4r/icp4r.h"
 #include "icp4r/icp4r_ego.h"
+#include "icp4r/icp4r_multi.h"
 #include "icp4r/pcl_compat.hpp"
 
 namespace {
@@ -123,8 +127,8 @@ struct FrameOut {
 };
 
 int usage() {
-    std::fprintf(stderr, "usage: icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--seed S] [--max-iterations N] "
-                         "[--use-icp-result CSV]\n");
+    std::fprintf(stderr, "usage: icp4radar_replay <dataset_folder> [--csv PATH] [--batch] [--devices D0,D1,...] [--seed S] "
+                         "[--max-iterations N] [--use-icp-result CSV]\n");
     return 2;
 }
 
@@ -136,6 +140,7 @@ int main(int argc, char** argv) {
     if (dataset_folder.empty() || dataset_folder.back() != '/') dataset_folder += "/";
     std::string csv = dataset_folder + "output_result.csv";
     bool batch = false;
+    std::vector<int> devices;  // --devices: the batch sharded over these (icp4r_align_batch_multi)
     icp4r_ego_params ep;
     icp4r_ego_params_default(&ep);
     int max_iterations = -1;  // PCL default (10) unless given
@@ -143,6 +148,15 @@ int main(int argc, char** argv) {
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--csv") && i + 1 < argc) csv = argv[++i];
         else if (!std::strcmp(argv[i], "--batch")) batch = true;
+        else if (!std::strcmp(argv[i], "--devices") && i + 1 < argc) {
+            devices.clear();
+            for (const char* c = argv[++i]; *c;) {
+                char* end = nullptr;
+                devices.push_back((int)std::strtol(c, &end, 10));
+                if (end == c) return usage();
+                c = *end == ',' ? end + 1 : end;
+            }
+        }
         else if (!std::strcmp(argv[i], "--seed") && i + 1 < argc) ep.seed = std::strtoull(argv[++i], nullptr, 0);
         else if (!std::strcmp(argv[i], "--max-iterations") && i + 1 < argc) max_iterations = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--use-icp-result") && i + 1 < argc) icp_result_csv = argv[++i];
@@ -265,7 +279,19 @@ int main(int argc, char** argv) {
             tgt.insert(tgt.end(), q.tgt.begin(), q.tgt.end());
         }
         std::vector<icp4r_result> res(pairs.size());
-        if (!pairs.empty()) {
+        if (!pairs.empty() && devices.size() > 0) {
+            // one context per listed device, frames sharded in contiguous blocks
+            std::vector<icp4r_ctx*> ctxs(devices.size(), nullptr);
+            int rc = ICP4R_OK;
+            for (size_t d = 0; d < devices.size() && rc == ICP4R_OK; ++d) rc = icp4r_create(&ctxs[d], devices[d]);
+            if (rc == ICP4R_OK)
+                rc = icp4r_align_batch_multi(ctxs.data(), (int32_t)ctxs.size(), src.data(), so.data(), sn.data(),
+                                             tgt.data(), to.data(), tn.data(), (int32_t)pairs.size(), nullptr, &ip,
+                                             res.data());
+            if (rc != ICP4R_OK) std::fprintf(stderr, "icp4r_align_batch_multi: %s\n", icp4r_last_error());
+            for (icp4r_ctx* c : ctxs) icp4r_destroy(c);
+            if (rc != ICP4R_OK) return 1;
+        } else if (!pairs.empty()) {
             int rc = icp4r_align_batch_host(ctx, src.data(), so.data(), sn.data(), tgt.data(), to.data(), tn.data(),
                                             (int32_t)pairs.size(), nullptr, &ip, res.data());
             if (rc != ICP4R_OK) {

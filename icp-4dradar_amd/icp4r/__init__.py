@@ -23,7 +23,8 @@ import numpy as np
 
 __all__ = [
     "ICP4RError", "Params", "Result", "Batch", "Context", "IterativeClosestPoint", "library_path", "load",
-    "default_params", "NUMERICS_PCL", "NUMERICS_F64", "status_name", "EXPORTED_SYMBOLS",
+    "default_params", "NUMERICS_PCL", "NUMERICS_F64", "status_name", "EXPORTED_SYMBOLS", "Comm", "shard",
+    "align_batch_multi",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -55,6 +56,11 @@ EGO_EXPORTED_SYMBOLS = [
 # include/icp4r/icp4r_gicp.h (generalized ICP; icp4r.gicp)
 GICP_EXPORTED_SYMBOLS = [
     "icp4r_gicp_params_default", "icp4r_gicp_align", "icp4r_gicp_align_batch_device", "icp4r_gicp_covariances",
+]
+# include/icp4r/icp4r_multi.h (the batched multi-GPU mode: shards, multi-device batch, RCCL gather)
+MULTI_EXPORTED_SYMBOLS = [
+    "icp4r_shard", "icp4r_align_batch_multi", "icp4r_comm_unique_id", "icp4r_comm_create", "icp4r_comm_destroy",
+    "icp4r_comm_rank", "icp4r_comm_check", "icp4r_gather_results", "icp4r_align_batch_sharded",
 ]
 # include/icp4r/icp4r_map.h (scan-to-map store; icp4r.mapstore)
 MAP_EXPORTED_SYMBOLS = [
@@ -177,6 +183,17 @@ def load():
         "icp4r_map_points_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(i64)]),
         "icp4r_map_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_map_time_reset": (C.c_int, [vp]),
+        # icp4r_multi.h
+        "icp4r_shard": (C.c_int, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
+        "icp4r_align_batch_multi": (C.c_int, [C.POINTER(vp), i32, vp, vp, vp, vp, vp, vp, i32, vp, C.POINTER(Params),
+                                              vp]),
+        "icp4r_comm_unique_id": (C.c_int, [C.c_char_p]),
+        "icp4r_comm_create": (C.c_int, [C.POINTER(vp), vp, i32, i32, C.c_char_p]),
+        "icp4r_comm_destroy": (C.c_int, [vp]),
+        "icp4r_comm_rank": (C.c_int, [vp, C.POINTER(i32), C.POINTER(i32)]),
+        "icp4r_comm_check": (C.c_int, [vp]),
+        "icp4r_gather_results": (C.c_int, [vp, vp, i32, vp, vp]),
+        "icp4r_align_batch_sharded": (C.c_int, [vp, C.POINTER(Batch), i32, C.POINTER(Params), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -443,3 +460,85 @@ class IterativeClosestPoint:
 
     def nr_iterations(self) -> int:
         return 0 if self._result is None else self._result.iterations
+
+
+# ---------------------------------------------------------------------------------------------------
+# Batched multi-GPU mode (include/icp4r/icp4r_multi.h).
+
+COMM_ID_BYTES = 128
+
+
+def shard(npairs: int, nranks: int, rank: int) -> range:
+    """icp4r_shard: the contiguous, balanced block of global pairs rank `rank` of `nranks` owns."""
+    f, c = C.c_int32(), C.c_int32()
+    _check(load().icp4r_shard(npairs, nranks, rank, C.byref(f), C.byref(c)), "icp4r_shard")
+    return range(f.value, f.value + c.value)
+
+
+def align_batch_multi(ctxs, src, src_off, src_n, tgt, tgt_off, tgt_n, params: Params | None = None,
+                      guess=None) -> np.ndarray:
+    """icp4r_align_batch_multi: one process, one context per device, shard k on context k (host threads);
+    returns the results of every pair in global order (RESULT_DTYPE)."""
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 4)
+    tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 4)
+    so = np.ascontiguousarray(src_off, np.int64)
+    sn = np.ascontiguousarray(src_n, np.int32)
+    to = np.ascontiguousarray(tgt_off, np.int64)
+    tn = np.ascontiguousarray(tgt_n, np.int32)
+    npairs = len(sn)
+    res = np.zeros(npairs, RESULT_DTYPE)
+    g = None
+    if guess is not None:
+        g = np.ascontiguousarray(np.asarray(guess, np.float32).transpose(0, 2, 1).reshape(npairs, 16))
+    handles = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    p = params if params is not None else default_params()
+    _check(load().icp4r_align_batch_multi(handles, len(ctxs), _ptr(src), _ptr(so), _ptr(sn), _ptr(tgt), _ptr(to),
+                                          _ptr(tn), npairs, _ptr(g) if g is not None else None, C.byref(p),
+                                          res.ctypes.data), "icp4r_align_batch_multi")
+    return res
+
+
+class Comm:
+    """One rank of an RCCL communicator on a context's device (icp4r_comm_create): the one-process-per-GPU
+    form of the batched mode.  Rank 0 makes the id (Comm.unique_id()) and hands it to the others."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _check(load().icp4r_comm_unique_id(buf), "icp4r_comm_unique_id")
+        return buf.raw
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise ICP4RError(E_INVALID, f"unique id must be {COMM_ID_BYTES} bytes")
+        self._lib = load()
+        self._h = C.c_void_p()
+        self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        _check(self._lib.icp4r_comm_create(C.byref(self._h), ctx.handle, nranks, rank, uid), "icp4r_comm_create")
+
+    def close(self):
+        if self._h:
+            self._lib.icp4r_comm_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self):
+        _check(self._lib.icp4r_comm_check(self._h), "icp4r_comm_check")
+
+    def gather(self, shard_rows_ptr: int, npairs: int, gathered_ptr: int, stream: int | None = None):
+        """icp4r_gather_results: this rank's rows (device) into every rank's gathered[npairs] (device)."""
+        _check(self._lib.icp4r_gather_results(self._h, C.c_void_p(shard_rows_ptr), npairs, C.c_void_p(gathered_ptr),
+                                              C.c_void_p(stream) if stream else None), "icp4r_gather_results")
+
+    def align_batch_sharded(self, batch: Batch, npairs_total: int, params: Params, shard_results_ptr: int,
+                            gathered_ptr: int, stream: int | None = None):
+        """icp4r_align_batch_sharded: register this rank's shard, then gather every rank's rows."""
+        _check(self._lib.icp4r_align_batch_sharded(self._h, C.byref(batch), npairs_total, C.byref(params),
+                                                   C.c_void_p(shard_results_ptr), C.c_void_p(gathered_ptr),
+                                                   C.c_void_p(stream) if stream else None),
+               "icp4r_align_batch_sharded")

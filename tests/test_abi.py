@@ -14,10 +14,11 @@ HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r.h")
 MAP_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_map.h")
 EGO_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_ego.h")
 GICP_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_gicp.h")
+MULTI_HEADER = os.path.join(ROOT, "include", "icp4r", "icp4r_multi.h")
 
 
 def header_functions(path=None):
-    paths = [path] if path else [HEADER, MAP_HEADER, EGO_HEADER, GICP_HEADER]
+    paths = [path] if path else [HEADER, MAP_HEADER, EGO_HEADER, GICP_HEADER, MULTI_HEADER]
     names = set()
     for p in paths:
         names |= set(re.findall(r"^\s*(?:const\s+char\s*\*|int|void)\s+(icp4r_\w+)\s*\(", open(p).read(), re.M))
@@ -36,6 +37,20 @@ def test_library_exports_every_declared_symbol():
     assert sorted(icp4r.MAP_EXPORTED_SYMBOLS) == header_functions(MAP_HEADER)
     assert sorted(icp4r.EGO_EXPORTED_SYMBOLS) == header_functions(EGO_HEADER)
     assert sorted(icp4r.GICP_EXPORTED_SYMBOLS) == header_functions(GICP_HEADER)
+    assert sorted(icp4r.MULTI_EXPORTED_SYMBOLS) == header_functions(MULTI_HEADER)
+
+
+def test_shard_ranges_match_split_even():
+    """icp4r_shard (C ABI) is the contiguous balanced split of icp4r.dist.split_even, every pair once."""
+    import icp4r
+    from icp4r import dist as idist
+
+    for P, N in ((8192, 8), (7, 3), (3, 5), (0, 2), (1024, 1)):
+        blocks = [icp4r.shard(P, N, r) for r in range(N)]
+        assert blocks == [idist.split_even(P, r, N) for r in range(N)]
+        assert [i for b in blocks for i in b] == list(range(P))
+    with pytest.raises(icp4r.ICP4RError):
+        icp4r.shard(8, 2, 2)
 
 
 def test_nm_shows_c_linkage():

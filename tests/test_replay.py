@@ -110,6 +110,10 @@ def test_replay_matches_oracle_loop(tmp_path, oracle_mod):
             for mode in ("frame", "batch")}
     assert outs["frame"] == outs["batch"]  # one device batch == the per-frame loop, byte for byte
     _check_against_oracle(outs["batch"], tmp_path, oracle_mod, seed, v)
+    # the batch sharded over several contexts (icp4r_align_batch_multi; one device here, listed three
+    # times: three contexts, three streams, three host threads) — byte-identical
+    multi = _run_replay(tmp_path, seed, True, tmp_path / "out_multi.csv", ["--devices", "0,0,0"])
+    assert multi == outs["batch"]
 
 
 @pytest.mark.gpu
