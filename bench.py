@@ -263,7 +263,7 @@ def pmc_traffic(config: str, kernel: str, sha: str | None):
 # The sequential float folds of the PCL-numerics update (Eigen's rowwise().sum() and
 # the cross-covariance, in correspondence order) are one dependent add chain per sum: two passes of n
 # dependent adds per iteration.  Measured cost per dependent add with the fold's LDS prefetch:
-# 6.4-6.7 cycles (tools/chain_bench.hip) at the 2.4 GHz max clock.
+# 6.4-6.7 cycles (tools/experiments/chain_bench.hip) at the 2.4 GHz max clock.
 CHAIN_CYCLES_PER_ADD = 6.4
 CLOCK_GHZ = 2.4
 

@@ -38,7 +38,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
                icp4r::WorkArgs& w);
 // One NN pass over every pair the pass wants (timed with the context's NN events).
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const icp4r::PairArgs& a, const icp4r::WorkArgs& w, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st, int ncu = 0, int test_fused = 0);
+            int fitness_pass, int first, hipStream_t st, int ncu = 0, int test_fused = 0, int pass = -1);
 int next_event(std::vector<icp4r_host::EventPair>& v, size_t& used, icp4r_host::EventPair** out);
 
 }  // namespace icp4r_pipe

@@ -95,8 +95,8 @@ int env_int(const char* name, int dflt) {
 //    (a single 8k pair runs at Q = 1: 128 waves), leaf = 16 targets per block.
 //  * brute force: Q queries per lane (fewer when pairs are few, so the grid still fills 256 CUs),
 //    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
-//    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/tune_sweep.py, profiles/tune_r01.jsonl).
-// Tuning overrides (tools/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
+//    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/experiments/tune_sweep.py, profiles/tune_r01.jsonl).
+// Tuning overrides (tools/experiments/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
 Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
@@ -231,7 +231,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
     if (env_int("ICP4R_PHASE_TICKS", 0)) {
-        const size_t nt = 32 + 20 * (size_t)npairs;  // (see the kernels' debug tick slots)
+        // (see the kernels' debug tick slots; then kPassTickSlots per NN pass)
+        const size_t nt = (size_t)pass_tick_base(npairs) + (size_t)kMaxTickPasses * kPassTickSlots;
         if (ctx->ticks.cap < nt * sizeof(uint64_t)) {
             HIP_TRY(ctx->ticks.ensure(nt * sizeof(uint64_t)));
             HIP_TRY(hipMemsetAsync(ctx->ticks.p, 0, nt * sizeof(uint64_t), st));
@@ -301,10 +302,14 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
 
 // One NN pass over every active pair, timed with events: the roofline's kernel is the batched
 // search (nn_lds_kernel) or, for the other plans, the NN launch itself.
-int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st, int ncu, int test_fused) {
+int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w0, int npairs, int max_n,
+            int fitness_pass, int first, hipStream_t st, int ncu, int test_fused, int pass) {
     EventPair* ne;
     int r;
+    WorkArgs w = w0;  // debug: the pass' own event slots (ICP4R_PHASE_TICKS=1)
+    w.pass_ticks = (w0.ticks && pass >= 0 && pass < kMaxTickPasses)
+                       ? w0.ticks + pass_tick_base(npairs) + (int64_t)pass * kPassTickSlots
+                       : nullptr;
     if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
     if (pl.lds) {
         NNLdsEvents ev;
@@ -436,7 +441,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     const bool fuse = pl.lds && pl.cache && pcl && env_int("ICP4R_FUSE_TEST", 1) != 0;
     for (int it = 0; it < iters; ++it) {
         for (int g = 0; g < groups; ++g) {
-            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0)))
+            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0, it)))
                 return rc;
             EventPair* ue;
             if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
@@ -449,7 +454,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
         // the fitness pass' cached-neighbour test runs inside fitness_prep_kernel when fused
         const int ftest = fuse && a.kp.compute_fitness ? 1 : 0;
         if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g], ftest));
-        if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu, ftest)))
+        if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu, ftest, iters)))
             return rc;
         HIP_TRY(launch_finish(ag[g], wg[g], gn[g], gs[g]));
     }
@@ -503,7 +508,7 @@ int nearest_keys(icp4r_ctx* ctx, const float* query, int32_t n, int32_t qstride,
     if ((rc = setup_work(ctx, pl, 1, n, m, false, st, w))) return rc;
     HIP_TRY(launch_init(a, w, 1, st));
     if (pl.pruned) HIP_TRY(launch_index(a, w, 1, st));
-    if ((rc = nn_pass(ctx, pl, a, w, 1, n, 0, 1, st))) return rc;
+    if ((rc = nn_pass(ctx, pl, a, w, 1, n, 0, 1, st, 0, 0, -1))) return rc;
     PairState ps;
     keys.resize((size_t)n);
     HIP_TRY(hipMemcpyAsync(&ps, w.state, sizeof(ps), hipMemcpyDeviceToHost, st));

@@ -154,7 +154,13 @@ struct WorkArgs {
                                 // cached-neighbour hits (count_add; the host sums the slots)
     uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
                         // boundaries of pair 0 — start, pass A, pass B, solve, transform
+    uint64_t* pass_ticks;  // debug (ICP4R_PHASE_TICKS=1): this NN pass' own slots [kPassTickSlots] of the
+                           // batched search's event counts / clocks (tools/nn_events.py), or nullptr
 };
+constexpr int kPassTickSlots = 16;  // per NN pass: 11 event counters / clocks + 4 per-item walls
+constexpr int kMaxTickPasses = 64;  // passes with their own slots (later passes: none)
+// first per-pass slot of a batch of npairs (after the pair-0 stamps and the per-pair debug slots)
+inline int64_t pass_tick_base(int npairs) { return 32 + 20 * (int64_t)npairs; }
 
 hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,

@@ -354,7 +354,7 @@ struct MortonShared {
 };
 
 #ifndef ICP4R_WG_TICKS
-#define ICP4R_WG_TICKS 0  // diagnostic builds: per-workgroup phase stamps (tools/wg_ticks.py)
+#define ICP4R_WG_TICKS 0  // diagnostic builds: per-workgroup phase stamps (tools/experiments/wg_ticks.py)
 #endif
 
 union IndexShared {
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     const float4* pts = is_tgt ? a.tgt + a.tgt_off[p] : a.src + a.src_off[p];
     if (!is_tgt && src_by_tgt_tree(a, w, p)) return;  // src_order_kernel orders it
     if ((w.kd_index & (is_tgt ? 1 : 2)) && n <= kKdMaxN && (!is_tgt || w.t_stride <= kKdMaxN)) {
-#if ICP4R_WG_TICKS  // diagnostic build: every cloud's build start / end and XCC / CU (tools/idx_ticks.py)
+#if ICP4R_WG_TICKS  // diagnostic build: every cloud's build start / end and XCC / CU (tools/experiments/idx_ticks.py)
         uint64_t* it = (w.ticks && tid == 0) ? w.ticks + 32 + 12 * (int64_t)gridDim.x + 8 * (int64_t)p + (is_tgt ? 0 : 4) : nullptr;
         if (it) {
             it[0] = __builtin_amdgcn_s_memrealtime();
@@ -1728,7 +1728,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
     auto heavy_size = [&](int c, int k) { return min(ps, c - k * ps); };
     for (int p = tid; p < npairs; p += kOrderWG) {
         const int c = work(p);
-        if (w.ticks) w.ticks[32 + p] = (uint64_t)c;  // debug: this pass' work per pair (tools/miss_hist.py)
+        if (w.ticks) w.ticks[32 + p] = (uint64_t)c;  // debug: this pass' work per pair (tools/experiments/miss_hist.py)
         if (c <= 0) continue;
         for (int k = 0, np = heavy_parts(c); k < np; ++k) atomicAdd(&bcnt[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1);
     }
@@ -1767,8 +1767,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
     unsigned long long evals = 0, tests = 0;
-    // debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1, ticks[16..26];
-    // tools/nn_events.py): wave-uniform adds, stored once at the end
+    // debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1: summed over the
+    // registration in ticks[16..26], and per pass in pass_ticks[0..10]; tools/nn_events.py):
+    // wave-uniform adds, stored once at the end
     uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
     uint64_t ck_setup = 0, ck_trav = 0, ck_write = 0;
     for (;;) {
@@ -2253,6 +2254,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             atomicAdd(tt + 9, (unsigned long long)(tk2 - tk1));
             atomicAdd(tt + 10, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tk2));
             atomicAdd(tt + 11, 1ull);
+            if (w.pass_ticks) {  // the same walls in this pass' own slots
+                unsigned long long* pt = reinterpret_cast<unsigned long long*>(w.pass_ticks);
+                atomicAdd(pt + 11, (unsigned long long)(tk1 - tk0));
+                atomicAdd(pt + 12, (unsigned long long)(tk2 - tk1));
+                atomicAdd(pt + 13, (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tk2));
+                atomicAdd(pt + 14, 1ull);
+            }
         }
     }
     if (lane == 0) {
@@ -2263,6 +2271,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             const unsigned long long ev[11] = {ev_runs, ev_q,  ev_sbv,  ev_sbp,   ev_blk,  ev_push,
                                                ev_drain, ev_items, ck_setup, ck_trav, ck_write};
             for (int k = 0; k < 11; ++k) atomicAdd(tt + 16 + k, ev[k]);
+            if (w.pass_ticks)
+                for (int k = 0; k < 11; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(w.pass_ticks) + k, ev[k]);
         }
     }
 }
@@ -2491,7 +2501,7 @@ __device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
     int k = 0;
     if (ICP4R_FOLD_AHEAD >= 2 && len >= 96) {
         // three register groups in rotation, two loads in flight while a group is summed: 6.4-6.7
-        // cycles per dependent add on gfx950 vs 7.6-9.0 with one group ahead (tools/chain_bench.hip)
+        // cycles per dependent add on gfx950 vs 7.6-9.0 with one group ahead (tools/experiments/chain_bench.hip)
         float4 a[8], b[8], c[8];
         load_group(a, f);
         load_group(b, f + 32);
@@ -2979,7 +2989,7 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
 
     const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
     if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
-#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/wg_ticks.py)
+#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/experiments/wg_ticks.py)
     uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
                                                               : nullptr;
     if (wt) {

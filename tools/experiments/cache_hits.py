@@ -1,6 +1,6 @@
 """Per-pass hit rate of the cached-neighbour test on the benchmark workload (diagnostic).
 
-    python tools/cache_hits.py [--pairs 256] [--iters 20]
+    python tools/experiments/cache_hits.py [--pairs 256] [--iters 20]
 
 Runs the batch with max_iterations = 1..iters (fitness pass off) and differences the device hit
 counter, so row k is the share of queries whose NN pass k resolved without a search; the last row
@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 

@@ -1,5 +1,5 @@
 // Microbenchmark: cycles per dependent float add of a sequential fold (the update's PCL-order sums).
-//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -o _var/chain_bench tools/chain_bench.hip
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -o _var/chain_bench tools/experiments/chain_bench.hip
 // One workgroup of 64 threads; lanes 0..6 each fold 4096 floats (a) from registers only (pure
 // dependent-add latency), (b) from LDS in groups of 32 read one group ahead (fold_seq's scheme),
 // (c) from LDS with two groups in flight.  Prints cycles per add (s_memtime delta / adds).

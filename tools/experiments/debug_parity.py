@@ -1,6 +1,6 @@
 """Per-iteration GPU-vs-oracle comparison (ULP distance of T) for debugging bit-exactness."""
 import sys, os, json
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for p in ("icp-4dradar_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(ROOT, p))
 import numpy as np

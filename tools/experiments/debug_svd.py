@@ -1,5 +1,5 @@
 import sys, os, ctypes as C
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 for p in ("icp-4dradar_amd", "oracle"):
     sys.path.insert(0, os.path.join(ROOT, p))
 import numpy as np

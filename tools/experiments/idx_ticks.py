@@ -1,7 +1,7 @@
 """Per-cloud timeline of index_kernel in the C3 batch (diagnostic build).
 
     tools/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
-    ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/idx_ticks.py [--pairs 1024]
+    ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/experiments/idx_ticks.py [--pairs 1024]
 
 Every cloud's kd build stamps s_memrealtime (100 MHz) at its start and end, with the CU it ran on.
 Prints the launch span, per-cloud build times (targets / sources) and how many builds each CU ran.
@@ -16,7 +16,7 @@ import sys
 
 os.environ["ICP4R_PHASE_TICKS"] = "1"
 os.environ["ICP4R_GROUPS"] = "1"
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 sys.path.insert(0, ROOT)
 

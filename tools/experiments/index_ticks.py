@@ -1,6 +1,6 @@
 """Phase timing of index_kernel's kd build for pair 0's target (diagnostic; ICP4R_PHASE_TICKS=1).
 
-    python tools/index_ticks.py [--pairs 1024]
+    python tools/experiments/index_ticks.py [--pairs 1024]
 
 s_memrealtime (100 MHz) at: start, after the counting sorts, after the levels, after the scatter and
 boxes — for a single pair and for pair 0 of a batch (where 2 clouds per CU-slot queue up).
@@ -15,7 +15,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 

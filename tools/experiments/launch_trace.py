@@ -1,7 +1,7 @@
 """Ordered kernel launches from a rocprofv3 rocpd database (per-launch durations, e.g. of the NN pass
 of every ICP iteration).
 
-    python tools/launch_trace.py gpurun_out/prof/run_results.db [--last 48] [--match nn_]
+    python tools/experiments/launch_trace.py gpurun_out/prof/run_results.db [--last 48] [--match nn_]
 """
 from __future__ import annotations
 

@@ -1,7 +1,7 @@
 """Per-pass distribution of cached-neighbour misses over the pairs of the benchmark batch
 (diagnostic; ICP4R_PHASE_TICKS=1 makes nn_order_kernel record each pair's work of the last pass).
 
-    python tools/miss_hist.py [--pairs 1024] [--iters 20]
+    python tools/experiments/miss_hist.py [--pairs 1024] [--iters 20]
 """
 from __future__ import annotations
 
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 

@@ -1,6 +1,6 @@
 """Per-pass phase times of the persistent batched search (diagnostic; ICP4R_PHASE_TICKS=1).
 
-    python tools/nn_phases.py [--pairs 1024] [--iters 20]
+    python tools/experiments/nn_phases.py [--pairs 1024] [--iters 20]
 
 For pass k (a run of k iterations minus a run of k-1): pairs searched, and per searched pair the
 wall time of compaction, target staging and the search itself (workgroup thread 0's clock).
@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 

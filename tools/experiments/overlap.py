@@ -2,7 +2,7 @@
 the last registration in order with start / duration, and how much of the batch span each queue was
 busy and both were busy together.
 
-    python tools/overlap.py gpurun_out/<trace dir>
+    python tools/experiments/overlap.py gpurun_out/<trace dir>
 """
 from __future__ import annotations
 

@@ -11,7 +11,7 @@ import os
 import sys
 
 os.environ["ICP4R_PHASE_TICKS"] = "1"
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 import numpy as np  # noqa: E402

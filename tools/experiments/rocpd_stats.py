@@ -1,6 +1,6 @@
 """Per-kernel statistics from a rocprofv3 rocpd database (the image's rocprofv3 writes SQLite).
 
-    python tools/rocpd_stats.py gpurun_out/prof_c3/run_results.db [--csv profiles/kernel_stats_<tag>.csv]
+    python tools/experiments/rocpd_stats.py gpurun_out/prof_c3/run_results.db [--csv profiles/kernel_stats_<tag>.csv]
 
 Prints name, calls, total/avg/min/max duration (ns) and share of GPU kernel time, like rocprofv3's
 --stats kernel_stats.csv (same column names), sorted by total time.

@@ -6,7 +6,7 @@ queries the batched NN pass would have to search:
   blk    + on a miss, the targets of j's 16-point kd leaf are evaluated and the best one is exact when it
          is closer than Lo - |X - X_s|, Lo = nearest target outside that leaf at the search position X_s;
   sb     the same with j's 128-point subtree (superblock).
-    python tools/second_chance_sim.py [pairs] [iters]
+    python tools/experiments/second_chance_sim.py [pairs] [iters]
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ import sys
 import numpy as np
 from scipy.spatial import cKDTree
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "icp-4dradar_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "icp-4dradar_amd"))
 from icp4r import synth  # noqa: E402
 
 

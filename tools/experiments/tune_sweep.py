@@ -4,7 +4,7 @@ Prints one JSON line per variant and round: NN kernel average launch time, whole
 distance evaluations per launch, the FP32 roofline fraction, and whether the results are
 bit-identical to the brute-force reference run.
 
-    python tools/tune_sweep.py [--pairs 1024 --points 8192 --rounds 2 --variants pruned:2:16,brute:4:0]
+    python tools/experiments/tune_sweep.py [--pairs 1024 --points 8192 --rounds 2 --variants pruned:2:16,brute:4:0]
 """
 from __future__ import annotations
 
@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 DEFAULT_VARIANTS = "brute:4:0,pruned:1:16,pruned:2:16,pruned:4:16,pruned:1:32,pruned:2:32,pruned:4:32"
 
 

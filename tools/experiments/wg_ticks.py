@@ -1,7 +1,7 @@
 """Per-workgroup phase timeline of fold_update_kernel in the C3 batch (diagnostic build).
 
     tools/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
-    ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/wg_ticks.py [--pairs 1024]
+    ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/experiments/wg_ticks.py [--pairs 1024]
 
 Every pair's workgroup stamps s_memrealtime (100 MHz) at its start, after pass A, pass B, the solve
 and the fused test, in its 10th update (single pair group).  Prints the launch span, the start
@@ -17,7 +17,7 @@ import sys
 
 os.environ["ICP4R_PHASE_TICKS"] = "1"
 os.environ["ICP4R_GROUPS"] = "1"
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 sys.path.insert(0, ROOT)
 

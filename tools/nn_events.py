@@ -3,7 +3,8 @@ ICP4R_PHASE_TICKS=1, ICP4R_GROUPS=1).
 
     python tools/nn_events.py [--pairs 1024] [--iters 20]
 
-For pass k (a run of k iterations minus a run of k-1), summed over every wave of nn_lds_kernel:
+For every NN pass of one registration (each pass adds into its own tick slots), summed over every
+wave of nn_lds_kernel:
 runs (one wave's ≤64-query slice of an item), queries, superblock visits (candidates of the run's
 coarse test), visits that passed the per-query test, candidate blocks, block pushes with at least
 one lane, drains, drained work items; and the wave clocks (s_memtime) of run setup, traversal and
@@ -47,48 +48,39 @@ def main():
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
 
-    def ticks():
-        buf = (C.c_uint64 * 32)()
-        return np.array(list(buf), np.float64) if lib.icp4r__debug_ticks(ctx._h, buf, 32) == 0 else None
+    def ticks(k):
+        buf = (C.c_uint64 * k)()
+        return np.array(list(buf), np.float64) if lib.icp4r__debug_ticks(ctx._h, buf, k) == 0 else None
 
-    prev = np.zeros(11)
-    prev_it = np.zeros(4)
+    # one registration: every NN pass adds into its own slots (pass_tick_base(P) + pass * 16)
+    base, slots, npass = 32 + 20 * P, 16, a.iters + 1
+    t0 = ticks(base + slots * npass)
+    ctx.reset_timers()
+    p = icp4r.default_params(max_iterations=a.iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
+                             compute_fitness=1)
+    ctx.align_batch_host(src, off, cnt, tgt, off, cnt, params=p)
+    t1 = ticks(base + slots * npass)
+    if t0 is None:
+        t0 = np.zeros_like(t1)
+    ms, _ = ctx.kernel_time_ms()
     total = np.zeros(11)
-    tot_ms = 0.0
-    for k in range(1, a.iters + 2):  # the last one: the iterations + the fitness pass
-        fit = k == a.iters + 1
-        p = icp4r.default_params(max_iterations=min(k, a.iters), mse_threshold_absolute=-1.0,
-                                 transformation_epsilon=-1.0, compute_fitness=1 if fit else 0)
-        t0 = ticks()
-        ctx.reset_timers()
-        ctx.align_batch_host(src, off, cnt, tgt, off, cnt, params=p)
-        t1 = ticks()
-        if t0 is None:
-            t0 = np.zeros(32)
-        d = (t1 - t0)[16:27]
-        last = d - prev
-        prev = d
-        it = (t1 - t0)[8:12]  # per-item wall (100 MHz): compaction, staging, search (all waves), items
-        it_last = it - prev_it
-        prev_it = it
+    for k in range(npass):
+        d = (t1 - t0)[base + k * slots: base + (k + 1) * slots]
+        last, it = d[:11], d[11:15]  # per-item walls (100 MHz): compaction, staging, search, items
         total += last
-        ms, _ = ctx.kernel_time_ms()
-        r = {"pass": "fitness" if fit else k}
+        r = {"pass": "fitness" if k == a.iters else k + 1}
         r.update({nm: int(v) for nm, v in zip(NAMES, last)})
         runs = max(last[0], 1)
         r["per_run"] = {"queries": last[1] / runs, "sb_visits": last[2] / runs, "blk_cands": last[4] / runs,
                         "pushes": last[5] / runs, "drains": last[6] / runs,
                         "cyc_setup": last[8] / runs, "cyc_traverse": last[9] / runs, "cyc_write": last[10] / runs}
         r["cyc_per_sb_visit"] = last[9] / max(last[2], 1)
-        ni = max(it_last[3], 1)
-        r["items"] = {"n": int(it_last[3]), "compact_us": it_last[0] / ni / 100, "stage_us": it_last[1] / ni / 100,
-                      "search_wall_us": it_last[2] / ni / 100,
-                      # wave clocks inside runs / (search wall x 16 waves): the waves' busy share of it
-                      "run_cyc_per_item": (last[8] + last[9] + last[10]) / ni}
-        r["registration_kernel_ms"] = ms
+        ni = max(it[3], 1)
+        r["items"] = {"n": int(it[3]), "compact_us": it[0] / ni / 100, "stage_us": it[1] / ni / 100,
+                      "search_wall_us": it[2] / ni / 100, "run_cyc_per_item": (last[8] + last[9] + last[10]) / ni}
         print(json.dumps(r), flush=True)
     runs = max(total[0], 1)
-    print(json.dumps({"pass": "total", **{nm: int(v) for nm, v in zip(NAMES, total)},
+    print(json.dumps({"pass": "total", "registration_kernel_ms": ms, **{nm: int(v) for nm, v in zip(NAMES, total)},
                       "per_run": {nm: total[i] / runs for i, nm in enumerate(NAMES) if i}}), flush=True)
 
 
