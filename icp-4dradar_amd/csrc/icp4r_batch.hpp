@@ -23,6 +23,8 @@ struct Plan {
     int chunks;   // pruned (streamed): target chunks searched by separate waves (merged by atomicMin)
     bool tile;    // pruned, not batched: nn_tile_kernel (LDS target tiles x query parts; ICP4R_NN_TILE=0: the stream)
     int max_m;    // the plan's largest target (tile grid)
+    bool solo;    // run_pairs: the whole registration of each pair in one workgroup (solo_kernel; PCL
+                  // numerics, one target tile, sources <= kCacheMaxN; ICP4R_SOLO=0 disables)
     int64_t blocks;
 };
 
@@ -30,7 +32,9 @@ int env_int(const char* name, int dflt);
 // Geometry of the NN pass for a batch shape.  allow_lds = false keeps the batched LDS search out (a
 // caller whose index strides exceed what it stages, icp4r_gicp.cpp), so every other field of the
 // plan is the one of the plan that runs.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO, bool allow_lds = true);
+// registration = true: the plan of run_pairs for PCL numerics (solo_kernel where it applies).
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO, bool allow_lds = true,
+               bool registration = false);
 // icp4r_params -> the kernels' KParams (validates).
 int make_kparams(const icp4r_params* p, icp4r::KParams* kp);
 // Size the context's workspace for a plan and fill WorkArgs.
@@ -38,7 +42,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
                icp4r::WorkArgs& w);
 // One NN pass over every pair the pass wants (timed with the context's NN events).
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const icp4r::PairArgs& a, const icp4r::WorkArgs& w, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st, int ncu = 0, int test_fused = 0, int pass = -1);
+            int fitness_pass, int first, hipStream_t st, int ncu = 0, int test_fused = 0, int pass = -1,
+            int ordered = 0);
 int next_event(std::vector<icp4r_host::EventPair>& v, size_t& used, icp4r_host::EventPair** out);
 
 }  // namespace icp4r_pipe

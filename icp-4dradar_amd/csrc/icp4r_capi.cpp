@@ -97,7 +97,7 @@ int env_int(const char* name, int dflt) {
 //    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
 //    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/experiments/tune_sweep.py, profiles/tune_r01.jsonl).
 // Tuning overrides (tools/experiments/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds) {
+Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bool registration) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
@@ -108,6 +108,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds) {
     pl.chunk_sb = 64;
     pl.chunks = 1;
     pl.tile = false;
+    pl.solo = false;
     pl.max_m = max_m;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
     pl.q = (qcap == 1 || qcap == 2 || qcap == 4 || qcap == 8 || qcap == 16) ? qcap
@@ -149,6 +150,10 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds) {
                 pl.chunks = (max_m + 8191) / 8192;
                 pl.blocks = (int64_t)npairs * ((max_n + 1023) / 1024) * pl.chunks;
             }
+            // a PCL-numerics registration whose targets fit one LDS tile: the whole registration of
+            // each pair in one workgroup (solo_kernel; ICP4R_SOLO=0: the multi-launch plan)
+            pl.solo = registration && pl.tile && pl.chunks == 1 && max_n <= kCacheMaxN && env_int("ICP4R_SOLO", 1) != 0;
+            if (pl.solo) pl.blocks = npairs;
         }
         return pl;
     }
@@ -262,6 +267,21 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
         HIP_TRY(ctx->kdn.ensure((size_t)npairs * kKdnStride * sizeof(uint32_t)));
         w.kdn = static_cast<uint32_t*>(ctx->kdn.p);
+        if (pl.solo) {  // the query list and the cached-neighbour state (solo_kernel)
+            HIP_TRY(ctx->qv.ensure((size_t)slots * sizeof(float4)));
+            HIP_TRY(ctx->qm.ensure((size_t)slots * sizeof(uint2)));
+            HIP_TRY(ctx->nn_lu.ensure((size_t)slots * sizeof(float)));
+            HIP_TRY(ctx->nn_t.ensure((size_t)slots * sizeof(float4)));
+            HIP_TRY(ctx->sq.ensure((size_t)slots * sizeof(float4)));
+            HIP_TRY(ctx->sm.ensure((size_t)slots * sizeof(uint2)));
+            w.qv = static_cast<float4*>(ctx->qv.p);
+            w.qm = static_cast<uint2*>(ctx->qm.p);
+            w.nn_u = static_cast<float*>(ctx->nn_lu.p);
+            w.nn_t = static_cast<float4*>(ctx->nn_t.p);
+            w.sq = static_cast<float4*>(ctx->sq.p);
+            w.sm = static_cast<uint2*>(ctx->sm.p);
+            w.defer_xform = 1;
+        }
         if (pl.lds) {
             HIP_TRY(ctx->plist.ensure((size_t)npairs * ((x_stride + 63) / 64) * sizeof(int32_t)));
             HIP_TRY(ctx->plist_n.ensure(4 * kMaxGroups * sizeof(int32_t)));  // per group: items, queue, part size
@@ -272,6 +292,10 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.qm = static_cast<uint2*>(ctx->qm.p);
             w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
             w.queue = w.plist_n + 1;
+            // (plist_n[3] of every group: the fused order's arrival counter, from zero per registration)
+            HIP_TRY(hipMemsetAsync(w.plist_n, 0, 4 * kMaxGroups * sizeof(int32_t), st));
+            HIP_TRY(ctx->owork.ensure((size_t)npairs * sizeof(int32_t)));
+            w.owork = static_cast<int32_t*>(ctx->owork.p);
         }
         if (pl.cache) {
             w.need_stride = (x_stride + 31) / 32;
@@ -303,7 +327,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
 // One NN pass over every active pair, timed with events: the roofline's kernel is the batched
 // search (nn_lds_kernel) or, for the other plans, the NN launch itself.
 int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w0, int npairs, int max_n,
-            int fitness_pass, int first, hipStream_t st, int ncu, int test_fused, int pass) {
+            int fitness_pass, int first, hipStream_t st, int ncu, int test_fused, int pass, int ordered) {
     EventPair* ne;
     int r;
     WorkArgs w = w0;  // debug: the pass' own event slots (ICP4R_PHASE_TICKS=1)
@@ -321,7 +345,8 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
             ev.test_start = te->start;
             ev.test_stop = te->stop;
         }
-        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev, test_fused));
+        HIP_TRY(launch_nn_lds(a, w, npairs, max_n, fitness_pass, first, ncu > 0 ? ncu : ctx->ncu, st, ev, test_fused,
+                              ordered));
         return ICP4R_OK;
     }
     if (pl.tile) {  // the events bracket nn_tile_kernel itself (not its seed / record kernels)
@@ -379,6 +404,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.plist += (int64_t)p0 * ((w.x_stride + 63) / 64);
         wg.plist_n += 4 * g;
         wg.queue = wg.plist_n + 1;
+        wg.owork += p0;
     }
     if (g > 0) wg.ticks = nullptr;  // debug slots are pair-0 / global
 }
@@ -391,11 +417,11 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
               int nn_mode, hipStream_t st) {
     if (npairs <= 0) return ICP4R_OK;
     const int mn = max_n > 0 ? max_n : 1;
-    const Plan pl = make_plan(npairs, mn, max_m, nn_mode);
+    const bool pcl = a.kp.numerics == kNumericsPCL;
+    const Plan pl = make_plan(npairs, mn, max_m, nn_mode, true, pcl);
     WorkArgs w;
     int rc;
-    const bool pcl = a.kp.numerics == kNumericsPCL;
-    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl, st, w))) return rc;
+    if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl && !pl.solo, st, w))) return rc;
     // sources ordered by their target's kd tree (src_order_kernel) on the batched plan, where its
     // better first-pass seeds and one kd build per pair pay (C3 +2.9 %); a single pair's extra launch
     // does not (C1 0.75 -> 0.80 ms), so the unbatched plans build the source's own tree
@@ -405,6 +431,17 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
+    if (pl.solo) {  // init, the two kd builds, then every iteration and the fitness pass in one launch
+        HIP_TRY(launch_init(a, w, npairs, st));
+        HIP_TRY(launch_index(a, w, npairs, st));
+        EventPair* ne;
+        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
+        HIP_TRY(hipEventRecord(ne->start, st));
+        HIP_TRY(launch_solo(a, w, npairs, max_n, max_iterations > 0 ? max_iterations : 1, st));
+        HIP_TRY(hipEventRecord(ne->stop, st));
+        HIP_TRY(hipEventRecord(be->stop, st));
+        return ICP4R_OK;
+    }
     int groups = pl.lds ? env_int("ICP4R_GROUPS", kDefaultGroups) : 1;
     if (groups < 1) groups = 1;
     if (groups > kMaxGroups) groups = kMaxGroups;
@@ -439,14 +476,20 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // the cached-neighbour test of iteration passes 2.. runs in the tail of the previous update
     // (fold_update_kernel, PCL numerics; ICP4R_FUSE_TEST=0: its own kernel)
     const bool fuse = pl.lds && pl.cache && pcl && env_int("ICP4R_FUSE_TEST", 1) != 0;
+    // ... and the work list of those passes is built by the update's last workgroup (ICP4R_FUSE_ORDER=0:
+    // nn_order_kernel)
+    const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
     for (int it = 0; it < iters; ++it) {
         for (int g = 0; g < groups; ++g) {
-            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0, it)))
+            const int ncu_g = search_cu > 0 ? search_cu : ctx->ncu;
+            if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0, it,
+                              ford && it > 0)))
                 return rc;
             EventPair* ue;
             if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
             HIP_TRY(hipEventRecord(ue->start, gs[g]));
-            HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g], fuse && it + 1 < iters));
+            HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g], fuse && it + 1 < iters,
+                                  ford && it + 1 < iters ? ncu_g : 0));
             HIP_TRY(hipEventRecord(ue->stop, gs[g]));
         }
     }
@@ -595,7 +638,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
     for (DevBuf* b : {&ctx->src, &ctx->tgt, &ctx->src_off, &ctx->src_n, &ctx->tgt_off, &ctx->tgt_n, &ctx->guess,
                       &ctx->aligned, &ctx->results, &ctx->T, &ctx->X, &ctx->nn_key,
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->kdn, &ctx->sq, &ctx->sm, &ctx->qv, &ctx->qm, &ctx->need,
-                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
+                      &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->owork, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
                       &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active})
         b->release();
@@ -882,8 +925,10 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out) {
     if (npairs <= 0 || max_src_n < 0 || max_tgt_n < 0 || !out) return fail(ICP4R_E_INVALID, "bad shape");
     if (nn_mode < ICP4R_NN_AUTO || nn_mode > ICP4R_NN_PRUNED) return fail(ICP4R_E_INVALID, "unknown nn_mode %d", nn_mode);
-    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode);
+    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode, true, true);
     out->pruned = pl.pruned ? 1 : 0;
+    out->solo = pl.solo ? 1 : 0;
+    out->reserved = 0;
     out->q = pl.q;
     out->splits = pl.splits;
     out->leaf = pl.leaf;

@@ -148,6 +148,8 @@ struct WorkArgs {
     int32_t* plist;     // [npairs * ceil(x_stride / 64)] items (pair << 10 | part)
     int32_t* plist_n;   // [4]: items, (queue), the pass's part size (nn_order_kernel)
     int32_t* queue;     // [1] next work-list index (reset by nn_order_kernel)
+    int32_t* owork;     // [npairs] the next pass' work per pair, published by fold_update_kernel when it
+                        // builds the work list itself (plist_n[3]: its arrival counter)
     int32_t part_size;  // nn_lds_kernel: misses per work item of a heavy pair (0: one item per pair);
                         // plist holds items (pair << 10 | part)
     unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,
@@ -177,14 +179,18 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
 struct NNLdsEvents {
     hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;
 };
+// ordered: the previous fold_update_kernel built the work list (no nn_order_kernel launch)
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused = 0);
+                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused = 0, int ordered = 0);
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
-                         hipStream_t st,
-                         int tail_test = 0);
+                         hipStream_t st, int tail_test = 0,
+                         int order_ncu = 0);  // > 0: the launch also builds the next pass's work list
+// solo_kernel: every iteration and the fitness pass of each pair in one workgroup (PCL numerics,
+// targets <= kLdsMaxTargets, sources <= kCacheMaxN; after launch_init and launch_index)
+hipError_t launch_solo(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int iters, hipStream_t st);
 hipError_t launch_fitness_prep(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st, int test = 0);
 hipError_t launch_finish(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st);

@@ -1700,25 +1700,36 @@ constexpr int kOrderBuckets = 32;
 constexpr int kPartBits = 10;  // work item = pair << kPartBits | part (parts of >= 64 misses)
 static_assert(kCacheMaxN / 64 <= (1 << kPartBits), "part field");
 
-__global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
-                                                            int all, int ncu) {
-    __shared__ int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
-    __shared__ unsigned long long tot_s;
+struct OrderShared {
+    int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
+    unsigned long long tot;
+};
+
+// The work list of a pass, built by WG threads of one workgroup: by nn_order_kernel, or (FUSED) by
+// the last workgroup of the fold_update_kernel launch that ran the pass's cached-neighbour test,
+// from the per-pair work words (owork) the other workgroups published — written and read with
+// agent-scope (L1-bypassing, write-through) accesses only, so no cache can hold a stale copy.
+template <int WG, bool FUSED>
+__device__ void order_items(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int all, int ncu,
+                            OrderShared& sh) {
     const int tid = threadIdx.x;
-    if (tid < kOrderBuckets) bcnt[tid] = 0;
-    if (tid == 0) tot_s = 0;
+    if (tid < kOrderBuckets) sh.bcnt[tid] = 0;
+    if (tid == 0) sh.tot = 0;
     __syncthreads();
-    if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
-        unsigned long long t = 0;
-        for (int p = tid; p < npairs; p += kOrderWG)
-            t += pass_wants(w.state[p].phase, fitness_pass) ? (unsigned long long)(w.miss_cnt[p] & kMissCount) : 0ull;
-        t = wave_sum(t);
-        if ((tid & 63) == 0) atomicAdd(&tot_s, t);
-    }
-    __syncthreads();
-    auto work = [&](int p) {
+    auto work = [&](int p) -> int {
+        if (FUSED) return __hip_atomic_load(w.owork + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMissCount;
         return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : (w.miss_cnt[p] & kMissCount);
     };
+    if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
+        unsigned long long t = 0;
+        for (int p = tid; p < npairs; p += WG) t += (unsigned long long)work(p);
+        t = wave_sum(t);
+        if ((tid & 63) == 0) atomicAdd(&sh.tot, t);
+    }
+    __syncthreads();
+    int32_t* bcnt = sh.bcnt;
+    int32_t* boff = sh.boff;
+    const unsigned long long tot_s = sh.tot;
     // a heavy pair's misses are cut into parts of part_size (first pass: one part, all queries), so
     // the few slowly converging pairs with thousands of misses spread over several CUs
     // (at least part_size, and large enough that the pass has about 2 items per CU: a part costs a
@@ -1726,7 +1737,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
     const int ps = (!all && w.part_size > 0) ? max(w.part_size, (int)((tot_s + 2ull * ncu - 1) / (2ull * ncu))) : (1 << 30);
     auto heavy_parts = [&](int c) { return (c + ps - 1) / ps; };
     auto heavy_size = [&](int c, int k) { return min(ps, c - k * ps); };
-    for (int p = tid; p < npairs; p += kOrderWG) {
+    for (int p = tid; p < npairs; p += WG) {
         const int c = work(p);
         if (w.ticks) w.ticks[32 + p] = (uint64_t)c;  // debug: this pass' work per pair (tools/experiments/miss_hist.py)
         if (c <= 0) continue;
@@ -1744,11 +1755,385 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
         w.plist_n[2] = ps == (1 << 30) ? 0 : ps;  // nn_lds_kernel: misses per part (0: whole pairs)
     }
     __syncthreads();
-    for (int p = tid; p < npairs; p += kOrderWG) {
+    for (int p = tid; p < npairs; p += WG) {
         const int c = work(p);
         if (c > 0)
             for (int k = 0, np = heavy_parts(c); k < np; ++k)
                 w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1)] = (p << kPartBits) | k;
+    }
+}
+
+__global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
+                                                            int all, int ncu) {
+    __shared__ OrderShared sh;
+    order_items<kOrderWG, false>(a, w, npairs, fitness_pass, all, ncu, sh);
+}
+
+// Counters of the LDS search runs (device work counts; per-wave events and clocks for
+// ICP4R_PHASE_TICKS=1 — tools/nn_events.py)
+struct RunStats {
+    unsigned long long evals = 0, tests = 0;
+    uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
+    uint64_t ck_setup = 0, ck_trav = 0, ck_write = 0;
+};
+// The LDS arrays a search reads: one pair's staged targets (.w = original index << 13 | position)
+// and block / superblock boxes (empty: FLT_MAX).
+struct LdsTile {
+    v4f* tl;
+    float (*bx)[6];
+    float (*sbx)[6];
+};
+
+// Stage pair p's sorted targets and boxes for an LDS search (every superblock of the pair: nsb <= 64)
+// and load lane l's superblock box into isl / ish (kept in registers for every run).  Every load is
+// issued before the first store: a load-store loop waited out one global round trip per target (8
+// per thread, ~10-20 us per item under load).  The caller's barrier makes the LDS visible.
+template <int WG>
+__device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w, int p, int nsb, v4f& isl, v4f& ish) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
+    const int nt = nsb * kSuper * kLdsLeaf;
+    constexpr int kPerT = kLdsTargets / WG;
+    static_assert(kLdsTargets % WG == 0, "targets per thread");
+    v4f tv[kPerT];
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * WG, nt - 1)];
+    const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
+    const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+    static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= WG, "one box per thread");
+    const int nbx = nsb * (kSuper + 1);
+    const int bq = min(tid, nbx - 1);
+    const bool blk = bq < nsb * kSuper;
+    const int kb = blk ? bq : bq - nsb * kSuper;
+    const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) {
+        int i = tid + k * WG;
+        // (opaque: the slot addresses are formed here, not hoisted out of a caller's item loop as
+        // invariants — kept live across the search they pushed its other values into scratch)
+        asm volatile("" : "+v"(i));
+        if (i < nt) sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
+    }
+    if (tid < nbx) {
+        const bool empty = !(blo.x <= bhi.x);  // (+inf, -inf): a box no point reaches
+        float* d = blk ? sh.bx[kb] : sh.sbx[kb];
+        d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
+        d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
+    }
+    const int sbl = min(lane, nsb - 1);  // (in flight across the caller's barrier)
+    isl = sbg[2 * sbl];
+    ish = sbg[2 * sbl + 1];
+}
+
+// The exact LDS search of one query list [0, nlist) of pair p (qv / qm: {x, y, z, U}, {source index |
+// sorted position << 14, seed target position}, in sorted-position order) against the staged tile,
+// by the workgroup's kLdsWaves waves (this wave: its runs, with bestl / secl / ring its LDS state).
+// CACHE: the second-nearest distance too (X.w = L, nn_u = U, nn_t = the NN's coordinates | positions);
+// want_key: the (d², index) key; corr: the correspondence record (plans without the cached state).
+template <bool CACHE>
+__device__ __forceinline__ void lds_runs(const LdsTile& sh, unsigned long long* bestl, uint32_t* secl, uint16_t* ring,
+                                         const float4* qv, const uint2* qm, int nlist, int m, int nsb, const v4f isl,
+                                         const v4f ish, const PairArgs& a, const WorkArgs& w, int p, int64_t xs0,
+                                         float4* X, NNKey* key, bool want_key, bool corr, RunStats& rs) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // Queries per wave run: the list is cut into R rounds of kLdsWaves equal position-contiguous
+    // runs of at most 64 (R = ceil(nlist / (kLdsWaves * 64))), so every wave gets the same share —
+    // a short list (the misses of a late pass) spreads over all waves, and the traversal,
+    // latency-bound per wave, runs on small runs whose tight query box prunes most superblocks.
+    const int rounds = max(1, (nlist + kLdsWaves * 64 - 1) / (kLdsWaves * 64));
+    const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
+    const int stride = kLdsWaves * per;
+    // the run's records (idle lanes shadow the run's first query: they never queue work and
+    // never widen the run's box); the next run's are loaded while this one is searched
+    auto fetch = [&](int b, float4& v, uint2& mq) {
+        const int s = (b + lane < min(b + per, nlist)) ? b + lane : b;
+        v = qv[s];
+        mq = qm[s];
+    };
+    float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 nm = make_uint2(0u, 0u);
+    if (wave * per < nlist) fetch(wave * per, nv, nm);
+    for (int base = wave * per; base < nlist; base += stride) {
+        const int cend = min(base + per, nlist);
+        const uint64_t ck0 = __builtin_readcyclecounter();
+        ++rs.ev_runs;
+        rs.ev_q += (uint32_t)(cend - base);
+        const float x = nv.x, y = nv.y, z = nv.z, uu = nv.w;
+        const bool live = base + lane < cend;
+        const int orig = (int)(nm.x & kNtIdxMask);
+        const int spos = (int)(nm.x >> kNtPosShift);
+        const int pj = min((int)nm.y, m - 1);
+        __builtin_amdgcn_sched_barrier(0);  // the current record consumed before the prefetch
+        if (base + stride < nlist) fetch(base + stride, nv, nm);
+        float bnd;  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
+                    // -1 on idle lanes (never queue work, never widen the coarse bound)
+        const int seed_pos0 = __builtin_amdgcn_readfirstlane(pj);
+        const int seed_blk = pj / kLdsLeaf;
+        [[maybe_unused]] const uint32_t lane9 = (uint32_t)lane << 9;  // ring item: query lane << 9 | block
+        {
+            // seed: the previous match (first pass: the target at the same relative position)
+            // and the rest of its 16-target block, evaluated up front from LDS — tight initial
+            // bounds, so the coarse rs.tests below already prune with them
+            NNKey lo = ~0ull;       // the smallest key seen
+            uint32_t s2 = ~0u;      // the smallest d² of every other target seen (bits)
+            v4f cs[kLdsLeaf];
+            lds_block(sh.tl, pj / kLdsLeaf, cs);
+            __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
+#pragma unroll
+            for (int t = 0; t < kLdsLeaf; ++t) {
+                const v4f c = cs[t];
+                const float d2 = l2_simple(x, y, z, tl_x(c), tl_y(c), tl_z(c));
+                const NNKey kn = make_key(d2, tl_key(c));
+                if (CACHE) s2 = second_d2((uint32_t)(lo >> 32), __float_as_uint(d2), s2);
+                lo = kn < lo ? kn : lo;
+            }
+            bestl[lane] = lo;
+            if (CACHE) {
+                // U of the previous search, moved since: an upper bound of the second-nearest
+                // distance even if no evaluated target attains it (all-query passes: +inf)
+                const uint32_t sec0 = min(s2, __float_as_uint(uu * uu * 1.00001f));
+                secl[lane] = sec0;
+                bnd = live ? __uint_as_float(sec0) * kLbGrow : -1.0f;
+            } else {
+                bnd = live ? key_d2(lo) * kLbGrow : -1.0f;
+            }
+            rs.evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
+        }
+        float qlo[3] = {x, y, z}, qhi[3] = {x, y, z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {  // DPP reductions (no LDS round trips), wave-uniform results
+            qlo[k] = wave_minf(qlo[k]);
+            qhi[k] = wave_maxf(qhi[k]);
+        }
+        const float qmax = wave_maxf(bnd);
+
+        // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
+        uint32_t head = 0, tail = 0;
+        auto drain = [&](uint32_t cnt) {
+            ++rs.ev_drain;
+            rs.ev_items += cnt;
+            const bool act = (uint32_t)lane < cnt;
+            const uint32_t it = ring[(head + lane) & (kRing - 1)];
+            const int owner = act ? (int)(it >> 9) : 0;
+            const int b = act ? (int)(it & 0x1ffu) : 0;
+            // the query's coordinates from its owner lane
+            const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
+            if (act) {
+                NNKey k1 = ~0ull;
+                uint32_t s2 = ~0u;  // second-smallest d² of the block (bits; >= k1's throughout)
+                // block b's targets sit XOR-swizzled (lds_swz): at step t lane L reads slot
+                // t ^ (b_L & 15), so lanes on different blocks spread over the 64 banks instead of
+                // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
+                // all 16 reads issued before the first compare (the compiler otherwise keeps two
+                // in flight: 8 dependent LDS round trips per drain)
+                v4f cs[kLdsLeaf];
+                lds_block(sh.tl, b, cs);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < kLdsLeaf; ++t) {
+                    const v4f c = cs[t];
+                    const float d2 = l2_simple(qx, qy, qz, tl_x(c), tl_y(c), tl_z(c));
+                    const NNKey kn = make_key(d2, tl_key(c));
+                    if (CACHE) s2 = second_d2((uint32_t)(k1 >> 32), __float_as_uint(d2), s2);
+                    k1 = kn < k1 ? kn : k1;
+                }
+                if (CACHE) {
+                    // every key but the final winner loses exactly one comparison: keep the smallest loser
+                    const NNKey old = atomicMin(&bestl[owner], k1);
+                    const uint32_t cand =
+                        k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
+                    atomicMin(&secl[owner], cand);
+                } else {
+                    atomicMin(&bestl[owner], k1);
+                }
+            }
+            head += cnt;
+            rs.evals += (unsigned long long)cnt * kLdsLeaf;
+            // tighter bounds for the rs.tests
+            bnd = !live ? -1.0f : (CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane])) * kLbGrow;
+        };
+        // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
+        // sit in the lanes' registers for the whole item (isl / ish)
+        const uint64_t cmask = __ballot(lane < nsb && box_lb(isl, ish, qlo, qhi) <= qmax);
+        rs.tests += nsb;
+        const int sb0 = seed_pos0 / (kLdsLeaf * kSuper);
+        // the candidate superblocks outward from the seed's, alternating up / down (only set bits
+        // of cmask are visited: a scalar loop over all nsb cost ~10 SALU per superblock per run)
+        uint64_t um = sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
+        bool upnext = true;
+        auto next_sb = [&]() -> int {
+            if (!(um | dm)) return -1;
+            int sb;
+            if (um && (upnext || !dm)) {
+                sb = __builtin_ctzll(um);
+                um &= um - 1;
+            } else {
+                sb = 63 - __builtin_clzll(dm);
+                dm &= ~(1ull << sb);
+            }
+            upnext = !upnext;
+            return sb;
+        };
+        // Candidates are taken kSbBatch at a time: their per-query superblock rs.tests run as
+        // independent chains (the traversal is bound by dependent latency, not by issue); then
+        // every superblock some lane may reach has its 8 blocks tested for every lane in one
+        // straight-line sequence (boxes broadcast from LDS, 8 independent rs.tests in flight), and
+        // the non-empty ones are queued.  A test may use a bound a drain has since tightened:
+        // that only queues more work, never loses a target.
+        const uint64_t ck1 = __builtin_readcyclecounter();
+#if ICP4R_SB_EXPAND
+        // A superblock some lane may reach has its 8 blocks tested for those lanes only: the c
+        // lanes that passed are compacted (ds_permute: rank k -> lane k), and each round rs.tests 8
+        // of them against the 8 blocks at once — lane L takes passed lane r0 + L / 8 and block
+        // L % 8, with that query's coordinates and bound pulled from its lane (ds_bpermute).  The
+        // (query, block) pairs that pass are queued with one ballot per round.  (Testing all 64
+        // lanes against all 8 blocks spent 80 VALU per superblock on the ~5 lanes that need it.)
+        const int blk8 = lane & (kSuper - 1);
+        for (;;) {
+            // kSbBatch candidates tested together (independent LDS reads and test chains), then
+            // the ones some lane may reach processed in order
+            int sbs[kSbBatch];
+            uint64_t ms[kSbBatch];
+#pragma unroll
+            for (int j = 0; j < kSbBatch; ++j) sbs[j] = next_sb();
+            if (sbs[0] < 0) break;
+#pragma unroll
+            for (int j = 0; j < kSbBatch; ++j) {
+                const auto* sbb = lds_vbase(&sh.sbx[sbs[j] < 0 ? 0 : sbs[j]][0]);
+                ms[j] = sbs[j] < 0 ? 0ull : __ballot(pt_lb(sbb, x, y, z) <= bnd);
+                rs.ev_sbv += sbs[j] < 0 ? 0 : 1;
+            }
+            rs.tests += 64 * kSbBatch;
+#pragma unroll
+            for (int j = 0; j < kSbBatch; ++j) {
+            const int sb = sbs[j];
+            const uint64_t m = ms[j];
+            if (m == 0) continue;
+            ++rs.ev_sbp;
+            const int c = __builtin_popcountll(m);
+            // this lane's tag: its lane id, and its seed block if that lies in sb (never queued:
+            // it was evaluated whole up front)
+            const int rel = seed_blk - sb * kSuper;
+            const uint32_t tag = (uint32_t)lane | ((ICP4R_SKIP_SEED && (uint32_t)rel < (uint32_t)kSuper) ? (8u | (uint32_t)rel) << 6 : 0u);
+            const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // passed lanes go to lane rank, the others to distinct lanes >= c (no collisions)
+            const uint32_t dst = lane_select(m, (uint32_t)c + (uint32_t)lane - rk, rk);
+            const uint32_t packed = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)tag);
+            // this lane's block box (8 rows, each read by 8 lanes: broadcast)
+            const auto* brow = lds_vbase(&sh.bx[sb * kSuper + blk8][0]);
+            float bb[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) bb[k] = brow[k];
+            rs.tests += 8 * c;
+            for (int r0 = 0; r0 < c; r0 += 8) {
+                const int srcl = r0 + (lane >> 3);
+                const uint32_t tg = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl << 2, (int)packed);
+                const int owner = (int)(tg & 63u);
+                const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
+                const float qb = __shfl(bnd, owner, 64);
+                const bool ok = srcl < c && (tg >> 6) != (8u | (uint32_t)blk8) && pt_lb(bb, qx, qy, qz) <= qb;
+                const uint64_t pm = __ballot(ok);
+                if (pm == 0) continue;
+                rs.ev_blk += __builtin_popcountll(pm);
+                const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)pm, tail));
+                const uint32_t at = lane_select(pm, (uint32_t)(kRing + lane), slot & (kRing - 1));
+                ring[at] = (uint16_t)(((uint32_t)owner << 9) | (uint32_t)(sb * kSuper + blk8));
+                tail += (uint32_t)__builtin_popcountll(pm);
+                if (tail - head >= 64) drain(64);
+            }
+            }
+        }
+#else
+        for (;;) {
+            uint32_t sbpack = 0, valid = 0;
+#pragma unroll
+            for (int j = 0; j < kSbBatch; ++j) {
+                const int sbj = next_sb();
+                if (sbj >= 0) {
+                    sbpack |= (uint32_t)sbj << (6 * j);
+                    valid |= 1u << j;
+                }
+            }
+            if (!valid) break;
+            uint32_t pass = 0;
+#pragma unroll
+            for (int j = 0; j < kSbBatch; ++j) {
+                const int sbj = (sbpack >> (6 * j)) & 63;
+                // the lanes that may reach this superblock (its box broadcast from LDS)
+                const auto* sbb = lds_vbase(&sh.sbx[sbj][0]);
+                if (__ballot(pt_lb(sbb, x, y, z) <= bnd) != 0) pass |= 1u << j;
+            }
+            pass &= valid;
+            const int nv = __builtin_popcount(valid);
+            rs.ev_sbv += nv;
+            rs.tests += 64 * nv;
+            for (; pass; pass &= pass - 1) {
+                const int sb = (sbpack >> (6 * __builtin_ctz(pass))) & 63;
+                ++rs.ev_sbp;
+                // the lane's seed block was evaluated whole up front: never queued again
+                const int rel = seed_blk - sb * kSuper;
+                uint64_t nmk[kSuper];
+#pragma unroll
+                for (int h = 0; h < kSuper; h += 4) {
+                    // 4 rows of 24 B from a multiple of 4 rows (16-B aligned): six ds_read_b128 at
+                    // immediate offsets from one VGPR base
+                    const auto* b4 = (const __attribute__((address_space(3))) v4f*)lds_vbase(&sh.bx[sb * kSuper + h][0]);
+                    v4f r4[6];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) r4[i] = b4[i];
+                    float bb[4][6];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) bb[j][c] = r4[(6 * j + c) >> 2][(6 * j + c) & 3];
+                    // (two ballots: a ballot of the '&&' went through a VGPR select, 3 VALU more)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd) & (ICP4R_SKIP_SEED ? __ballot(rel != h + j) : ~0ull);
+                }
+                rs.tests += 64 * kSuper;
+#pragma unroll
+                for (int k = 0; k < kSuper; ++k) {  // (unrolled: a rolled loop with one drain
+                    const uint64_t mask = nmk[k];  //  copy measured 9 % slower)
+                    if (mask == 0) continue;
+                    ++rs.ev_blk;
+                    // every lane writes (no exec-mask branch): lanes that do not need the block
+                    // write their own spare slot past the ring (the mask itself is the select)
+                    const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, tail));
+                    const uint32_t at = lane_select(mask, (uint32_t)(kRing + lane), slot & (kRing - 1));
+                    ring[at] = (uint16_t)(lane9 | (uint32_t)(sb * kSuper + k));
+                    tail += (uint32_t)__builtin_popcountll(mask);
+                    if (tail - head >= 64) drain(64);
+                }
+            }
+        }
+#endif
+        if (tail != head) drain(tail - head);
+        const uint64_t ck2 = __builtin_readcyclecounter();
+        // the winner's coordinates come from its LDS slot (the key carries its position)
+        const NNKey kb = bestl[lane];
+        const uint32_t tpos = lk_pos(kb);
+        const v4f t = sh.tl[lds_swz((int)tpos)];
+        if (live) {
+            const NNKey ko = make_key(key_d2(kb), lk_idx(kb));  // (d², original index): PCL's answer
+            if (want_key) key[orig] = ko;
+            if (CACHE) {  // the update reads X, nn_t: no correspondence record
+                const float2 lu = lu_from_sec(__uint_as_float(secl[lane]));
+                X[orig] = make_float4(x, y, z, lu.x);  // .w = L
+                w.nn_u[xs0 + orig] = lu.y;
+                w.nn_t[xs0 + orig] = make_float4(tl_x(t), tl_y(t), tl_z(t), nt_pack((int)tpos, spos));
+            } else if (corr) {
+                write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(tl_x(t), tl_y(t), tl_z(t), 0.f));
+            }
+        }
+        const uint64_t ck3 = __builtin_readcyclecounter();
+        rs.ck_setup += ck1 - ck0;
+        rs.ck_trav += ck2 - ck1;
+        rs.ck_write += ck3 - ck2;
     }
 }
 
@@ -1766,12 +2151,10 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     // keys: without the cached-neighbour state the next search's seed and the records read them
     const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
-    unsigned long long evals = 0, tests = 0;
-    // debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1: summed over the
-    // registration in ticks[16..26], and per pass in pass_ticks[0..10]; tools/nn_events.py):
-    // wave-uniform adds, stored once at the end
-    uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
-    uint64_t ck_setup = 0, ck_trav = 0, ck_write = 0;
+    // work counters; debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1:
+    // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
+    // tools/nn_events.py): wave-uniform adds, stored once at the end
+    RunStats rs;
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
@@ -1910,343 +2293,15 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // superblock l's box for every run of the item; nsb <= 64 on this plan).  Every load is issued
         // before the first store: a load-store loop waited out one global round trip per target
         // (8 per thread, ~10-20 us per item under load).
+        const LdsTile tv{sh.tl, sh.bx, sh.sbx};
         v4f isl, ish;
-        {
-            const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
-            const int nt = nsb * kSuper * kLdsLeaf;
-            constexpr int kPerT = kLdsTargets / kLdsWG;
-            static_assert(kLdsTargets % kLdsWG == 0, "targets per thread");
-            v4f tv[kPerT];
-#pragma unroll
-            for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * kLdsWG, nt - 1)];
-            const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
-            const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-            static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= kLdsWG, "one box per thread");
-            const int nbx = nsb * (kSuper + 1);
-            const int bq = min(tid, nbx - 1);
-            const bool blk = bq < nsb * kSuper;
-            const int kb = blk ? bq : bq - nsb * kSuper;
-            const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
-#pragma unroll
-            for (int k = 0; k < kPerT; ++k) {
-                const int i = tid + k * kLdsWG;
-                if (i < nt) {
-                    sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
-                }
-            }
-            if (tid < nbx) {
-                const bool empty = !(blo.x <= bhi.x);  // (+inf, -inf): a box no point reaches
-                float* d = blk ? sh.bx[kb] : sh.sbx[kb];
-                d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
-                d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
-            }
-            const int sbl = min(lane, nsb - 1);  // (in flight across the barrier)
-            isl = sbg[2 * sbl];
-            ish = sbg[2 * sbl + 1];
-        }
+        stage_tile<kLdsWG>(tv, w, p, nsb, isl, ish);
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         unsigned long long* bestl = sh.r.best[wave];
         uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
-
-        // Queries per wave run: the list is cut into R rounds of kLdsWaves equal position-contiguous
-        // runs of at most 64 (R = ceil(nlist / (kLdsWaves * 64))), so every wave gets the same share —
-        // a short list (the misses of a late pass) spreads over all waves, and the traversal,
-        // latency-bound per wave, runs on small runs whose tight query box prunes most superblocks.
-        const int rounds = max(1, (nlist + kLdsWaves * 64 - 1) / (kLdsWaves * 64));
-        const int per = (nlist + kLdsWaves * rounds - 1) / (kLdsWaves * rounds);
-        const int stride = kLdsWaves * per;
-        // the run's records (idle lanes shadow the run's first query: they never queue work and
-        // never widen the run's box); the next run's are loaded while this one is searched
-        auto fetch = [&](int b, float4& v, uint2& mq) {
-            const int s = (b + lane < min(b + per, nlist)) ? b + lane : b;
-            v = qv[s];
-            mq = qm[s];
-        };
-        float4 nv = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint2 nm = make_uint2(0u, 0u);
-        if (wave * per < nlist) fetch(wave * per, nv, nm);
-        for (int base = wave * per; base < nlist; base += stride) {
-            const int cend = min(base + per, nlist);
-            const uint64_t ck0 = __builtin_readcyclecounter();
-            ++ev_runs;
-            ev_q += (uint32_t)(cend - base);
-            const float x = nv.x, y = nv.y, z = nv.z, uu = nv.w;
-            const bool live = base + lane < cend;
-            const int orig = (int)(nm.x & kNtIdxMask);
-            const int spos = (int)(nm.x >> kNtPosShift);
-            const int pj = min((int)nm.y, m - 1);
-            __builtin_amdgcn_sched_barrier(0);  // the current record consumed before the prefetch
-            if (base + stride < nlist) fetch(base + stride, nv, nm);
-            float bnd;  // pruning bound: best d² (plain search) / second-best d² (CACHE search);
-                        // -1 on idle lanes (never queue work, never widen the coarse bound)
-            const int seed_pos0 = __builtin_amdgcn_readfirstlane(pj);
-            const int seed_blk = pj / kLdsLeaf;
-            [[maybe_unused]] const uint32_t lane9 = (uint32_t)lane << 9;  // ring item: query lane << 9 | block
-            {
-                // seed: the previous match (first pass: the target at the same relative position)
-                // and the rest of its 16-target block, evaluated up front from LDS — tight initial
-                // bounds, so the coarse tests below already prune with them
-                NNKey lo = ~0ull;       // the smallest key seen
-                uint32_t s2 = ~0u;      // the smallest d² of every other target seen (bits)
-                v4f cs[kLdsLeaf];
-                lds_block(sh.tl, pj / kLdsLeaf, cs);
-                __builtin_amdgcn_sched_barrier(0);  // all 16 reads in flight before the first use
-#pragma unroll
-                for (int t = 0; t < kLdsLeaf; ++t) {
-                    const v4f c = cs[t];
-                    const float d2 = l2_simple(x, y, z, tl_x(c), tl_y(c), tl_z(c));
-                    const NNKey kn = make_key(d2, tl_key(c));
-                    if (CACHE) s2 = second_d2((uint32_t)(lo >> 32), __float_as_uint(d2), s2);
-                    lo = kn < lo ? kn : lo;
-                }
-                bestl[lane] = lo;
-                if (CACHE) {
-                    // U of the previous search, moved since: an upper bound of the second-nearest
-                    // distance even if no evaluated target attains it (all-query passes: +inf)
-                    const uint32_t sec0 = min(s2, __float_as_uint(uu * uu * 1.00001f));
-                    secl[lane] = sec0;
-                    bnd = live ? __uint_as_float(sec0) * kLbGrow : -1.0f;
-                } else {
-                    bnd = live ? key_d2(lo) * kLbGrow : -1.0f;
-                }
-                evals += 64 * kLdsLeaf;  // the wave's lanes (counted once by lane 0)
-            }
-            float qlo[3] = {x, y, z}, qhi[3] = {x, y, z};
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {  // DPP reductions (no LDS round trips), wave-uniform results
-                qlo[k] = wave_minf(qlo[k]);
-                qhi[k] = wave_maxf(qhi[k]);
-            }
-            const float qmax = wave_maxf(bnd);
-
-            // Evaluate `cnt` (<= 64) queued items from ring[head..]: lane L takes item head + L.
-            uint32_t head = 0, tail = 0;
-            auto drain = [&](uint32_t cnt) {
-                ++ev_drain;
-                ev_items += cnt;
-                const bool act = (uint32_t)lane < cnt;
-                const uint32_t it = ring[(head + lane) & (kRing - 1)];
-                const int owner = act ? (int)(it >> 9) : 0;
-                const int b = act ? (int)(it & 0x1ffu) : 0;
-                // the query's coordinates from its owner lane
-                const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
-                if (act) {
-                    NNKey k1 = ~0ull;
-                    uint32_t s2 = ~0u;  // second-smallest d² of the block (bits; >= k1's throughout)
-                    // block b's targets sit XOR-swizzled (lds_swz): at step t lane L reads slot
-                    // t ^ (b_L & 15), so lanes on different blocks spread over the 64 banks instead of
-                    // all hitting the 4 banks of slot t (a 64-way conflict: every block is 256 B)
-                    // all 16 reads issued before the first compare (the compiler otherwise keeps two
-                    // in flight: 8 dependent LDS round trips per drain)
-                    v4f cs[kLdsLeaf];
-                    lds_block(sh.tl, b, cs);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int t = 0; t < kLdsLeaf; ++t) {
-                        const v4f c = cs[t];
-                        const float d2 = l2_simple(qx, qy, qz, tl_x(c), tl_y(c), tl_z(c));
-                        const NNKey kn = make_key(d2, tl_key(c));
-                        if (CACHE) s2 = second_d2((uint32_t)(k1 >> 32), __float_as_uint(d2), s2);
-                        k1 = kn < k1 ? kn : k1;
-                    }
-                    if (CACHE) {
-                        // every key but the final winner loses exactly one comparison: keep the smallest loser
-                        const NNKey old = atomicMin(&bestl[owner], k1);
-                        const uint32_t cand =
-                            k1 < old ? min((uint32_t)(old >> 32), s2) : (k1 == old ? s2 : (uint32_t)(k1 >> 32));
-                        atomicMin(&secl[owner], cand);
-                    } else {
-                        atomicMin(&bestl[owner], k1);
-                    }
-                }
-                head += cnt;
-                evals += (unsigned long long)cnt * kLdsLeaf;
-                // tighter bounds for the tests
-                bnd = !live ? -1.0f : (CACHE ? __uint_as_float(secl[lane]) : key_d2(bestl[lane])) * kLbGrow;
-            };
-            // coarse test of every superblock at once (lane = superblock; nsb <= 64 here): the boxes
-            // sit in the lanes' registers for the whole item (isl / ish)
-            const uint64_t cmask = __ballot(lane < nsb && box_lb(isl, ish, qlo, qhi) <= qmax);
-            tests += nsb;
-            const int sb0 = seed_pos0 / (kLdsLeaf * kSuper);
-            // the candidate superblocks outward from the seed's, alternating up / down (only set bits
-            // of cmask are visited: a scalar loop over all nsb cost ~10 SALU per superblock per run)
-            uint64_t um = sb0 < 64 ? (cmask >> sb0) << sb0 : 0ull, dm = cmask & ~um;
-            bool upnext = true;
-            auto next_sb = [&]() -> int {
-                if (!(um | dm)) return -1;
-                int sb;
-                if (um && (upnext || !dm)) {
-                    sb = __builtin_ctzll(um);
-                    um &= um - 1;
-                } else {
-                    sb = 63 - __builtin_clzll(dm);
-                    dm &= ~(1ull << sb);
-                }
-                upnext = !upnext;
-                return sb;
-            };
-            // Candidates are taken kSbBatch at a time: their per-query superblock tests run as
-            // independent chains (the traversal is bound by dependent latency, not by issue); then
-            // every superblock some lane may reach has its 8 blocks tested for every lane in one
-            // straight-line sequence (boxes broadcast from LDS, 8 independent tests in flight), and
-            // the non-empty ones are queued.  A test may use a bound a drain has since tightened:
-            // that only queues more work, never loses a target.
-            const uint64_t ck1 = __builtin_readcyclecounter();
-#if ICP4R_SB_EXPAND
-            // A superblock some lane may reach has its 8 blocks tested for those lanes only: the c
-            // lanes that passed are compacted (ds_permute: rank k -> lane k), and each round tests 8
-            // of them against the 8 blocks at once — lane L takes passed lane r0 + L / 8 and block
-            // L % 8, with that query's coordinates and bound pulled from its lane (ds_bpermute).  The
-            // (query, block) pairs that pass are queued with one ballot per round.  (Testing all 64
-            // lanes against all 8 blocks spent 80 VALU per superblock on the ~5 lanes that need it.)
-            const int blk8 = lane & (kSuper - 1);
-            for (;;) {
-                // kSbBatch candidates tested together (independent LDS reads and test chains), then
-                // the ones some lane may reach processed in order
-                int sbs[kSbBatch];
-                uint64_t ms[kSbBatch];
-#pragma unroll
-                for (int j = 0; j < kSbBatch; ++j) sbs[j] = next_sb();
-                if (sbs[0] < 0) break;
-#pragma unroll
-                for (int j = 0; j < kSbBatch; ++j) {
-                    const auto* sbb = lds_vbase(&sh.sbx[sbs[j] < 0 ? 0 : sbs[j]][0]);
-                    ms[j] = sbs[j] < 0 ? 0ull : __ballot(pt_lb(sbb, x, y, z) <= bnd);
-                    ev_sbv += sbs[j] < 0 ? 0 : 1;
-                }
-                tests += 64 * kSbBatch;
-#pragma unroll
-                for (int j = 0; j < kSbBatch; ++j) {
-                const int sb = sbs[j];
-                const uint64_t m = ms[j];
-                if (m == 0) continue;
-                ++ev_sbp;
-                const int c = __builtin_popcountll(m);
-                // this lane's tag: its lane id, and its seed block if that lies in sb (never queued:
-                // it was evaluated whole up front)
-                const int rel = seed_blk - sb * kSuper;
-                const uint32_t tag = (uint32_t)lane | ((ICP4R_SKIP_SEED && (uint32_t)rel < (uint32_t)kSuper) ? (8u | (uint32_t)rel) << 6 : 0u);
-                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                // passed lanes go to lane rank, the others to distinct lanes >= c (no collisions)
-                const uint32_t dst = lane_select(m, (uint32_t)c + (uint32_t)lane - rk, rk);
-                const uint32_t packed = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)tag);
-                // this lane's block box (8 rows, each read by 8 lanes: broadcast)
-                const auto* brow = lds_vbase(&sh.bx[sb * kSuper + blk8][0]);
-                float bb[6];
-#pragma unroll
-                for (int k = 0; k < 6; ++k) bb[k] = brow[k];
-                tests += 8 * c;
-                for (int r0 = 0; r0 < c; r0 += 8) {
-                    const int srcl = r0 + (lane >> 3);
-                    const uint32_t tg = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl << 2, (int)packed);
-                    const int owner = (int)(tg & 63u);
-                    const float qx = __shfl(x, owner, 64), qy = __shfl(y, owner, 64), qz = __shfl(z, owner, 64);
-                    const float qb = __shfl(bnd, owner, 64);
-                    const bool ok = srcl < c && (tg >> 6) != (8u | (uint32_t)blk8) && pt_lb(bb, qx, qy, qz) <= qb;
-                    const uint64_t pm = __ballot(ok);
-                    if (pm == 0) continue;
-                    ev_blk += __builtin_popcountll(pm);
-                    const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)pm, tail));
-                    const uint32_t at = lane_select(pm, (uint32_t)(kRing + lane), slot & (kRing - 1));
-                    ring[at] = (uint16_t)(((uint32_t)owner << 9) | (uint32_t)(sb * kSuper + blk8));
-                    tail += (uint32_t)__builtin_popcountll(pm);
-                    if (tail - head >= 64) drain(64);
-                }
-                }
-            }
-#else
-            for (;;) {
-                uint32_t sbpack = 0, valid = 0;
-#pragma unroll
-                for (int j = 0; j < kSbBatch; ++j) {
-                    const int sbj = next_sb();
-                    if (sbj >= 0) {
-                        sbpack |= (uint32_t)sbj << (6 * j);
-                        valid |= 1u << j;
-                    }
-                }
-                if (!valid) break;
-                uint32_t pass = 0;
-#pragma unroll
-                for (int j = 0; j < kSbBatch; ++j) {
-                    const int sbj = (sbpack >> (6 * j)) & 63;
-                    // the lanes that may reach this superblock (its box broadcast from LDS)
-                    const auto* sbb = lds_vbase(&sh.sbx[sbj][0]);
-                    if (__ballot(pt_lb(sbb, x, y, z) <= bnd) != 0) pass |= 1u << j;
-                }
-                pass &= valid;
-                const int nv = __builtin_popcount(valid);
-                ev_sbv += nv;
-                tests += 64 * nv;
-                for (; pass; pass &= pass - 1) {
-                    const int sb = (sbpack >> (6 * __builtin_ctz(pass))) & 63;
-                    ++ev_sbp;
-                    // the lane's seed block was evaluated whole up front: never queued again
-                    const int rel = seed_blk - sb * kSuper;
-                    uint64_t nmk[kSuper];
-#pragma unroll
-                    for (int h = 0; h < kSuper; h += 4) {
-                        // 4 rows of 24 B from a multiple of 4 rows (16-B aligned): six ds_read_b128 at
-                        // immediate offsets from one VGPR base
-                        const auto* b4 = (const __attribute__((address_space(3))) v4f*)lds_vbase(&sh.bx[sb * kSuper + h][0]);
-                        v4f r4[6];
-#pragma unroll
-                        for (int i = 0; i < 6; ++i) r4[i] = b4[i];
-                        float bb[4][6];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-#pragma unroll
-                            for (int c = 0; c < 6; ++c) bb[j][c] = r4[(6 * j + c) >> 2][(6 * j + c) & 3];
-                        // (two ballots: a ballot of the '&&' went through a VGPR select, 3 VALU more)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            nmk[h + j] = __ballot(pt_lb(bb[j], x, y, z) <= bnd) & (ICP4R_SKIP_SEED ? __ballot(rel != h + j) : ~0ull);
-                    }
-                    tests += 64 * kSuper;
-#pragma unroll
-                    for (int k = 0; k < kSuper; ++k) {  // (unrolled: a rolled loop with one drain
-                        const uint64_t mask = nmk[k];  //  copy measured 9 % slower)
-                        if (mask == 0) continue;
-                        ++ev_blk;
-                        // every lane writes (no exec-mask branch): lanes that do not need the block
-                        // write their own spare slot past the ring (the mask itself is the select)
-                        const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, tail));
-                        const uint32_t at = lane_select(mask, (uint32_t)(kRing + lane), slot & (kRing - 1));
-                        ring[at] = (uint16_t)(lane9 | (uint32_t)(sb * kSuper + k));
-                        tail += (uint32_t)__builtin_popcountll(mask);
-                        if (tail - head >= 64) drain(64);
-                    }
-                }
-            }
-#endif
-            if (tail != head) drain(tail - head);
-            const uint64_t ck2 = __builtin_readcyclecounter();
-            // the winner's coordinates come from its LDS slot (the key carries its position)
-            const NNKey kb = bestl[lane];
-            const uint32_t tpos = lk_pos(kb);
-            const v4f t = sh.tl[lds_swz((int)tpos)];
-            if (live) {
-                const NNKey ko = make_key(key_d2(kb), lk_idx(kb));  // (d², original index): PCL's answer
-                if (want_key) key[orig] = ko;
-                if (CACHE) {  // the update reads X, nn_t: no correspondence record
-                    const float2 lu = lu_from_sec(__uint_as_float(secl[lane]));
-                    X[orig] = make_float4(x, y, z, lu.x);  // .w = L
-                    w.nn_u[xs0 + orig] = lu.y;
-                    w.nn_t[xs0 + orig] = make_float4(tl_x(t), tl_y(t), tl_z(t), nt_pack((int)tpos, spos));
-                } else if (corr) {
-                    write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(tl_x(t), tl_y(t), tl_z(t), 0.f));
-                }
-            }
-            const uint64_t ck3 = __builtin_readcyclecounter();
-            ck_setup += ck1 - ck0;
-            ck_trav += ck2 - ck1;
-            ck_write += ck3 - ck2;
-        }
+        lds_runs<CACHE>(tv, bestl, secl, ring, qv, qm, nlist, m, nsb, isl, ish, a, w, p, xs0, X, key, want_key, corr, rs);
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
         if (tk) {
             unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
@@ -2264,12 +2319,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         }
     }
     if (lane == 0) {
-        count_add(w.evals, 0, evals);
-        count_add(w.evals, 1, tests);
+        count_add(w.evals, 0, rs.evals);
+        count_add(w.evals, 1, rs.tests);
         if (w.ticks) {
             unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
-            const unsigned long long ev[11] = {ev_runs, ev_q,  ev_sbv,  ev_sbp,   ev_blk,  ev_push,
-                                               ev_drain, ev_items, ck_setup, ck_trav, ck_write};
+            const unsigned long long ev[11] = {rs.ev_runs, rs.ev_q,     rs.ev_sbv,   rs.ev_sbp,  rs.ev_blk,  rs.ev_push,
+                                               rs.ev_drain, rs.ev_items, rs.ck_setup, rs.ck_trav, rs.ck_write};
             for (int k = 0; k < 11; ++k) atomicAdd(tt + 16 + k, ev[k]);
             if (w.pass_ticks)
                 for (int k = 0; k < 11; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(w.pass_ticks) + k, ev[k]);
@@ -2728,7 +2783,7 @@ __device__ __forceinline__ void tail_prefetch(const WorkArgs& w, int p, int n, T
 }
 
 template <int WG, int kPer, bool FROM_SRC>
-__device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
+__device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
                                                 uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
                                                 int32_t* mcount, int32_t* wcnt, bool fitness, uint64_t* stamp = nullptr,
                                                 const TailFirst<kPer>* first = nullptr) {
@@ -2837,7 +2892,7 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
     for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
     if (tot == 0) {
         if (tid == 0) w.miss_cnt[p] = 0;
-        return;
+        return 0;
     }
     const int nwords = (n + 31) >> 5;
     if (tot > lcap) {
@@ -2851,7 +2906,7 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
         uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
         for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
         if (tid == 0) w.miss_cnt[p] = tot | kMissUnranked;
-        return;
+        return tot;
     }
     // Rank placement: the search reads its item's queries in sorted-position order (a run of 64
     // consecutive ones is a compact box), so every miss record goes to its rank in the bitmap — the
@@ -2909,6 +2964,7 @@ __device__ __forceinline__ void pair_cache_test(const PairArgs& a, const WorkArg
         put(r2, m2);
         put(r3, m3);
     }
+    return tot;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2948,71 +3004,57 @@ struct FoldShared {
     SolveShared s;
 };
 
-__global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test) {
-    __shared__ FoldShared sh;
-    const int p = xcd_remap(blockIdx.x, gridDim.x);
-    PairState& st = w.state[p];
-    if (st.phase != kPhaseActive) return;
+// The correspondences an update folds: the NN kernels' records C ({s.xyz, w}, {d.xyz, d²} per point),
+// or, with the cached-neighbour test (C == nullptr), X_i (the searched point: the transform is
+// deferred) and its NN's coordinates NT[i], d² = l2_simple(X_i, t) — the very expression the NN
+// computed its key with, so the same bits.
+struct FoldIn {
+    const float4* C;
+    const float4* X;
+    const float4* NT;
+    int n;
+};
+
+// Pass A of the PCL-numerics update by a workgroup of WG threads over LDS chunks of CH points
+// (buf: two chunks of 9 rows of ROW floats): wave 0 lanes 0..6 fold Σs, Σd (Eigen 3.3
+// rowwise().sum(): from the first element == from -0.0f; Huber: w·x from +0) and Σw; wave 1 lane 0
+// the double MSE chain when an MSE criterion is live (else it fills); the other waves stage the next
+// chunk.  Leaves |C|, 1/n and the centroids in s.
+template <int WG, int CH, int ROW>
+__device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], float* res,
+                                            int32_t* wcnt, SolveShared& s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = a.src_n[p];
-    clear_need(w, p, n, tid, kFoldWG);
-    const int64_t xs = w.x_stride;
-    const KParams& kp = a.kp;
     const bool weighted = kp.huber_delta < INFINITY;
-    // The correspondence of source point i: {s.xyz, w}, {d.xyz, d²} — the NN kernels' records, or,
-    // with the cached-neighbour test (no records), X_i (the searched point: the transform is
-    // deferred), its NN's coordinates nn_t[i] and d² = l2_simple(X_i, t) — the very expression the
-    // NN computed its key with, so the same bits.
-    const float4* C = w.corr ? w.corr + (int64_t)p * xs * 2 : nullptr;
-    const float4* Xp = w.X + (int64_t)p * xs;
-    const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
     auto rec = [&](int i, float4& r0, float4& r1) {
-        if (C) {
-            r0 = C[2 * i];
-            r1 = C[2 * i + 1];
+        if (f.C) {
+            r0 = f.C[2 * i];
+            r1 = f.C[2 * i + 1];
         } else {
-            r0 = Xp[i];
-            r1 = NT[i];
+            r0 = f.X[i];
+            r1 = f.NT[i];
         }
     };
     auto rec_fix = [&](float4& r0, float4& r1) {
-        if (!C) {
+        if (!f.C) {
             const float d2 = l2_simple(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z);
             r0.w = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
             r1.w = d2;
         }
     };
+    const int n = f.n;
+    const int nch = (n + CH - 1) / CH;
     const bool mse = kp.need_mse != 0;  // wave 1 runs the MSE chain in pass A, else it fills
     const float ident = weighted ? 0.0f : -0.0f;
-    const int nch = (n + kFoldChunkP - 1) / kFoldChunkP;
     const int fill0 = mse ? 128 : 64;  // first filler thread of pass A
-
-    const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
-    if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
-#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/experiments/wg_ticks.py)
-    uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
-                                                              : nullptr;
-    if (wt) {
-        wt[0] = __builtin_amdgcn_s_memrealtime();
-        // where the fold wave (wave 0) runs: HW_ID (SIMD [5:4], CU [11:8], SH [12], SE [15:13]) and XCC_ID
-        wt[5] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
-    }
-#define WG_TICK(k) \
-    if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define WG_TICK(k)
-#endif
-    // ---- pass A
     int cnt = 0;
     // Fillers issue every load of their (at most kPerA) elements before the first LDS store, so a
     // chunk costs one global round trip, not one per element.
-    constexpr int kPerA = (kFoldChunkP + (kFoldWG - 128) - 1) / (kFoldWG - 128);
+    constexpr int kPerA = (CH + (WG - 128) - 1) / (WG - 128);
     // fill: load_a issues the loads of chunk c's records (clamped: at most kPerA per filler),
     // store_a turns them into the chain rows of LDS buffer c & 1.  (Loading two chunks ahead in two
     // register sets was measured: no faster — pass A at 1024 pairs is not waiting on these loads.)
     auto load_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {
-        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
+        const int base = c * CH, len = min(CH, n - base), nf = WG - fill0;
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int i = base + min(tid - fill0 + e * nf, len - 1);
@@ -3020,8 +3062,8 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
         }
     };
     auto store_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {  // waves 2, 3 (and 1 without the MSE chain)
-        float(*b)[kFoldRow] = sh.buf[c & 1];
-        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base), nf = kFoldWG - fill0;
+        float(*b)[ROW] = buf[c & 1];
+        const int base = c * CH, len = min(CH, n - base), nf = WG - fill0;
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int o = tid - fill0 + e * nf;
@@ -3053,12 +3095,12 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     if (wv == 0) {
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], min(kFoldChunkP, n - c * kFoldChunkP), acc);
+            if (lane < 7) acc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), acc);
         }
     } else if (wv * 64 < fill0) {  // the MSE chain
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane == 0) dacc = fold_seq<double>(sh.buf[c & 1][7], min(kFoldChunkP, n - c * kFoldChunkP), dacc);
+            if (lane == 0) dacc = fold_seq<double>(buf[c & 1][7], min(CH, n - c * CH), dacc);
         }
     } else {
         if (nch > 0) {
@@ -3078,29 +3120,53 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     // |C|: exact integer reduction of the fillers' counts
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
-    if (lane == 0) sh.cnt[wave] = cnt;
-    if (wave == 0 && lane < 7) sh.res[lane] = acc;
-    if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
+    if (lane == 0) wcnt[wave] = cnt;
+    if (wave == 0 && lane < 7) res[lane] = acc;
+    if (wave == 1 && lane == 0) s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
     __syncthreads();
-    if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
-    WG_TICK(1);
     if (tid == 0) {
         int total = 0;
-        for (int k = 0; k < kFoldWaves; ++k) total += sh.cnt[k];
-        sh.s.mom[0] = (double)total;
+        for (int k = 0; k < (WG / 64); ++k) total += wcnt[k];
+        s.mom[0] = (double)total;
         // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
-        const float one_over_n = 1.0f / sh.res[6];
-        sh.s.one_over_n = one_over_n;
-        for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
+        const float one_over_n = 1.0f / res[6];
+        s.one_over_n = one_over_n;
+        for (int k = 0; k < 6; ++k) s.mean[k] = res[k] * one_over_n;
     }
     __syncthreads();
+}
 
-    // ---- pass B
-    const float ms[3] = {sh.s.mean[0], sh.s.mean[1], sh.s.mean[2]};
-    const float md[3] = {sh.s.mean[3], sh.s.mean[4], sh.s.mean[5]};
-    constexpr int kFillB = kFoldWG - 64, kPerB = (kFoldChunkP + kFillB - 1) / kFillB;
+// Pass B: the fillers form the 9 products d'_a·s'_b (Huber: (w·d'_a)·s'_b) over the float-demeaned
+// points and wave 0 lanes 0..8 fold them (IEEE addition commutes: p + acc == a·b + acc bit for bit).
+// Leaves sigma (unscaled) in s.sigmaf.
+template <int WG, int CH, int ROW>
+__device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], SolveShared& s) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool weighted = kp.huber_delta < INFINITY;
+    auto rec = [&](int i, float4& r0, float4& r1) {
+        if (f.C) {
+            r0 = f.C[2 * i];
+            r1 = f.C[2 * i + 1];
+        } else {
+            r0 = f.X[i];
+            r1 = f.NT[i];
+        }
+    };
+    auto rec_fix = [&](float4& r0, float4& r1) {
+        if (!f.C) {
+            const float d2 = l2_simple(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z);
+            r0.w = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
+            r1.w = d2;
+        }
+    };
+    const int n = f.n;
+    const int nch = (n + CH - 1) / CH;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const float ms[3] = {s.mean[0], s.mean[1], s.mean[2]};
+    const float md[3] = {s.mean[3], s.mean[4], s.mean[5]};
+    constexpr int kFillB = WG - 64, kPerB = (CH + kFillB - 1) / kFillB;
     auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
-        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
+        const int base = c * CH, len = min(CH, n - base);
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int i = base + min(tid - 64 + e * kFillB, len - 1);
@@ -3108,8 +3174,8 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
         }
     };
     auto store_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {  // waves 1..3
-        float(*b)[kFoldRow] = sh.buf[c & 1];
-        const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);
+        float(*b)[ROW] = buf[c & 1];
+        const int base = c * CH, len = min(CH, n - base);
 #pragma unroll
         for (int e = 0; e < kPerB; ++e) {
             const int o = tid - 64 + e * kFillB;
@@ -3135,7 +3201,7 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     if (wv == 0) {
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane < 9) sacc = fold_seq<float>(sh.buf[c & 1][lane], min(kFoldChunkP, n - c * kFoldChunkP), sacc);
+            if (lane < 9) sacc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), sacc);
         }
     } else {
         if (nch > 0) {
@@ -3152,12 +3218,51 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
             }
         }
     }
-    if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sacc;
+    if (wave == 0 && lane < 9) s.sigmaf[lane] = sacc;
     __syncthreads();
+}
+
+// The update of pair p; returns the pair's work in the next pass (its misses in the fused test; 0
+// when it is not searched again).
+__device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArgs& w, int tail_test, int p,
+                                                FoldShared& sh) {
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return 0;
+    const int tid = threadIdx.x;
+    const int n = a.src_n[p];
+    clear_need(w, p, n, tid, kFoldWG);
+    const int64_t xs = w.x_stride;
+    const KParams& kp = a.kp;
+    const float4* C = w.corr ? w.corr + (int64_t)p * xs * 2 : nullptr;
+    const float4* Xp = w.X + (int64_t)p * xs;
+    const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
+
+    const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
+    if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
+#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/experiments/wg_ticks.py)
+    uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
+                                                              : nullptr;
+    if (wt) {
+        wt[0] = __builtin_amdgcn_s_memrealtime();
+        // where the fold wave (wave 0) runs: HW_ID (SIMD [5:4], CU [11:8], SH [12], SE [15:13]) and XCC_ID
+        wt[5] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    }
+#define WG_TICK(k) \
+    if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define WG_TICK(k)
+#endif
+    const FoldIn fin{C, Xp, NT, n};
+    fold_pass_a<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
+    if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
+    WG_TICK(1);
+    fold_pass_b<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.s);
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(2);
     // the fused test's first point group is loaded, and its LDS bitmap cleared, while thread 0 solves
     const bool tail = tail_test && w.nn_u;
+    int nwork = 0;
     TailFirst<ICP4R_TAIL_PER> tf;
     uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
     if (tail) {
@@ -3169,7 +3274,7 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(3);
-    if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
+    if (sh.s.flag == 1) return 0;  // error: PCL breaks before transforming
     if (!w.defer_xform) transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
     // The next pass's cached-neighbour test, fused (tail_test: another iteration follows and the pair
     // is still active): the same work as nn_cache_test_kernel for this pair — the deferred
@@ -3189,11 +3294,37 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
 #else
         uint64_t* stamp = nullptr;
 #endif
-        pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs, &sh.mcount, sh.cnt,
-                                                        false, stamp, &tf);
+        nwork = pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs, &sh.mcount,
+                                                                sh.cnt, false, stamp, &tf);
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(4);
+    return nwork;
+}
+
+// order_ncu > 0: the next pass's work list is built here, by the launch's last workgroup (the
+// nn_order_kernel launch and its kernel boundary removed from every iteration pass).  Every
+// workgroup publishes its pair's work word (an agent-scope store: write-through, past every cache),
+// waits for it, then counts itself in with an agent-scope add; the workgroup whose add completes
+// the launch's count reads the words back with agent-scope (L1-bypassing) loads.  The counter only
+// grows (plist_n[3], zeroed per registration): a launch's last add is the one that makes it a
+// multiple of the grid size.
+__global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test, int order_ncu) {
+    __shared__ FoldShared sh;
+    __shared__ OrderShared osh;
+    __shared__ int32_t last;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    const int nwork = fold_update_pair(a, w, tail_test, p, sh);
+    if (order_ncu <= 0) return;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(w.owork + p, nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(w.plist_n + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (old + 1) % (int)gridDim.x == 0 ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    order_items<kFoldWG, true>(a, w, (int)gridDim.x, 0, 0, order_ncu, osh);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3362,6 +3493,266 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// solo_kernel: one pair's whole registration by one 1024-thread workgroup — the unbatched plan for
+// targets of at most kLdsTargets points (C1, C2: the node's per-frame call,
+// iterative_closest_point.cpp:510-521), after init_kernel and index_kernel.  The pair's targets and
+// boxes are staged into LDS once, and every ICP iteration runs inside the launch, separated by
+// workgroup barriers only:
+//   test    the cached-neighbour test of every source in sorted-position order (the deferred
+//           transformCloud(T_inc), the bounds moved, hit or miss), the misses' search records
+//           compacted in that order into the pair's query list — first pass: every source;
+//   search  lds_runs<true> over the list (the batched search's run machinery and arithmetic);
+//   update  fold passes A and B over (X, nn_t) in index order, the Umeyama solve, hasConverged;
+// then the fitness pass (final * input, the test, the misses searched with keys, the sequential
+// double sum of Registration::getFitnessScore) and the result row.  Per iteration this removes the
+// launches, their boundaries and the target staging of the multi-launch plan; every result is
+// bit-identical to it (the same per-query and per-chain arithmetic in the same order).
+constexpr int kSoloWG = kLdsWG;
+constexpr int kSoloChunk = 192;  // fold chunk (points): two 96-float steps of fold_seq per chain
+constexpr int kSoloRow = kSoloChunk + kFoldPad;
+constexpr int kSoloFitChunk = 960;  // fitness chunk: 15 waves fill, wave 0 lane 0 folds
+constexpr int kSoloGrp = 4;         // the test's sorted positions in flight per thread
+struct SoloShared {
+    v4f tl[kLdsTargets];
+    alignas(16) float bx[kLdsTargets / kLdsLeaf][6];
+    float sbx[kLdsTargets / kLdsLeaf / kSuper][6];
+    union {
+        struct {  // the search's per-wave state
+            unsigned long long best[kLdsWaves][64];
+            uint32_t sec[kLdsWaves][64];
+            uint16_t items[kLdsWaves][kRing + 64];
+        } s;
+        struct {  // the update
+            alignas(16) float buf[2][9][kSoloRow];
+            float res[8];
+            int32_t cnt[kLdsWaves];
+            SolveShared sv;
+        } f;
+        alignas(16) float fit[2][kSoloFitChunk];  // the fitness sum's chunks
+    } u;
+    int32_t wtot[kLdsWaves];  // per-wave counts (the test's misses, the fitness count)
+};
+static_assert(sizeof(SoloShared) <= 160 * 1024, "solo LDS");
+
+// The solo plan's cached-neighbour test over sorted positions: thread t takes positions
+// [t * per, (t + 1) * per), 8 at a time with every load in flight, and the misses' records go to the
+// query list at their rank among all misses (a workgroup scan): qv = {x, y, z, U}, qm = {source index
+// | sorted position << 14, the cached NN's sorted target position}.  MODE 0: the first pass — every
+// source, X as init_kernel wrote it, U = +inf, seeded at the target of the same relative sorted
+// position; 1: an iteration pass — X := T_inc X (PCL's transformCloud, deferred), X and U written;
+// 2: the fitness pass — T = final applied to the input, a hit's key (its d² is what the fitness sum
+// reads), the aligned output.  Returns the list length.
+template <int MODE>
+__device__ int solo_test(const PairArgs& a, const WorkArgs& w, int p, int n, int m, const float (&T)[16],
+                         SoloShared& sh) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t xs0 = (int64_t)p * w.x_stride;
+    float4* X = w.X + xs0;
+    float* uu = w.nn_u + xs0;
+    const float4* nt = w.nn_t + xs0;
+    const int32_t* sperm = w.sperm + xs0;
+    float4* qv = w.qv + xs0;
+    uint2* qm = w.qm + xs0;
+    const int per = (n + kSoloWG - 1) / kSoloWG;
+    const int k0 = min(tid * per, n), k1 = min(k0 + per, n);
+    uint32_t missbits = 0;
+    int c = 0;
+    for (int g = k0; g < k1; g += kSoloGrp) {
+        int ii[kSoloGrp];
+#pragma unroll
+        for (int e = 0; e < kSoloGrp; ++e) ii[e] = sperm[min(g + e, k1 - 1)];
+        float4 v[kSoloGrp], t[kSoloGrp], s[kSoloGrp];
+        float U[kSoloGrp];
+#pragma unroll
+        for (int e = 0; e < kSoloGrp; ++e) {
+            v[e] = X[ii[e]];
+            if (MODE != 0) {
+                t[e] = nt[ii[e]];
+                U[e] = uu[ii[e]];
+            }
+            if (MODE == 2) s[e] = a.src[a.src_off[p] + ii[e]];
+        }
+#pragma unroll
+        for (int e = 0; e < kSoloGrp; ++e) {
+            const int k = g + e;
+            if (k >= k1) break;
+            const int i = ii[e];
+            if (MODE == 0) {
+                qv[k] = make_float4(v[e].x, v[e].y, v[e].z, INFINITY);
+                qm[k] = make_uint2((uint32_t)i | ((uint32_t)k << kNtPosShift), (uint32_t)(((int64_t)k * m) / n));
+                continue;
+            }
+            float4 o = v[e];
+            if (MODE == 2)
+                xform_pt(T, s[e].x, s[e].y, s[e].z, o.x, o.y, o.z);  // final * input
+            else
+                xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
+            const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            o.w = Lm.x;
+            const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
+            const bool hit = cache_hit(Lm.x, d2);
+            if (MODE == 1) {
+                X[i] = o;
+                uu[i] = Lm.y;
+            }
+            if (MODE == 2 && a.aligned) a.aligned[a.src_off[p] + i] = make_float4(o.x, o.y, o.z, s[e].w);
+            if (hit) {
+                if (MODE == 2) w.nn_key[xs0 + i] = make_key(d2, nt_tpos(t[e].w));  // (d² only: finish)
+            } else {
+                // the record at its sorted position for now; moved to its rank below
+                w.sq[xs0 + k] = make_float4(o.x, o.y, o.z, Lm.y);
+                w.sm[xs0 + k] = make_uint2((uint32_t)i | ((uint32_t)k << kNtPosShift), nt_tpos(t[e].w));
+                missbits |= 1u << (k - k0);
+                ++c;
+            }
+        }
+    }
+    if (MODE == 0) return n;
+    // cached-neighbour test counters (nn_stats: evaluations, hits, tested)
+    const unsigned long long hits = wave_sum((unsigned long long)(max(k1 - k0, 0) - c));
+    const unsigned long long tested = wave_sum((unsigned long long)max(k1 - k0, 0));
+    if (lane == 0) {
+        count_add(w.evals, 0, hits);
+        count_add(w.evals, 2, hits);
+        count_add(w.evals, 3, tested);
+    }
+    // rank of this thread's first miss: an exclusive scan of the per-thread counts
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) sh.wtot[wave] = incl;
+    __syncthreads();
+    int base = 0, total = 0;
+    for (int v = 0; v < kLdsWaves; ++v) {
+        const int s = sh.wtot[v];
+        base += v < wave ? s : 0;
+        total += s;
+    }
+    int r = base + incl - c;
+    for (uint32_t b = missbits; b; b &= b - 1) {  // (this thread's own records: no barrier needed)
+        const int k = k0 + __builtin_ctz(b);
+        qv[r] = w.sq[xs0 + k];
+        qm[r] = w.sm[xs0 + k];
+        ++r;
+    }
+    return total;
+}
+
+__global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, int iters) {
+    __shared__ SoloShared sh;
+    const int p = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    PairState& st = w.state[p];
+    const KParams& kp = a.kp;
+    const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+    const int64_t xs0 = (int64_t)p * w.x_stride;
+    const bool valid = uload(&st.phase) != kPhaseInvalid;
+    const int nsb = (((m + kLdsLeaf - 1) / kLdsLeaf) + kSuper - 1) / kSuper;
+    const LdsTile tile{sh.tl, sh.bx, sh.sbx};
+    RunStats rs;
+    auto search = [&](int nlist, bool keys) {
+        __syncthreads();  // the list (global, this workgroup's) and the union's previous use
+        const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+        const int sbl = min(lane, nsb - 1);
+        const v4f isl = sbg[2 * sbl], ish = sbg[2 * sbl + 1];
+        lds_runs<true>(tile, sh.u.s.best[wave], sh.u.s.sec[wave], sh.u.s.items[wave], w.qv + xs0, w.qm + xs0, nlist, m,
+                       nsb, isl, ish, a, w, p, xs0, w.X + xs0, w.nn_key + xs0, keys, false, rs);
+        __syncthreads();
+    };
+    if (valid) {
+        v4f isl, ish;
+        stage_tile<kSoloWG>(tile, w, p, nsb, isl, ish);
+        float T[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T[q] = 0.0f;
+        int flag = 0;
+        for (int it = 0; it < iters && flag == 0; ++it) {
+            const int nlist = it == 0 ? solo_test<0>(a, w, p, n, m, T, sh) : solo_test<1>(a, w, p, n, m, T, sh);
+            search(nlist, false);
+            const FoldIn fin{nullptr, w.X + xs0, w.nn_t + xs0, n};
+            fold_pass_a<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, sh.u.f.buf, sh.u.f.res, sh.u.f.cnt, sh.u.f.sv);
+            fold_pass_b<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, sh.u.f.buf, sh.u.f.sv);
+            if (tid == 0) solve_pair<kNumericsPCL>(sh.u.f.sv, st, kp);
+            __syncthreads();
+            flag = sh.u.f.sv.flag;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) T[q] = sh.u.f.sv.T_inc[q];  // the next pass's deferred transform
+        }
+        // the fitness pass (getFitnessScore after align) and align's output: final * input
+        if (kp.compute_fitness || a.aligned) {
+            __syncthreads();  // thread 0's final_T
+#pragma unroll
+            for (int q = 0; q < 16; ++q) T[q] = st.final_T[q];
+            if (kp.compute_fitness) {
+                search(solo_test<2>(a, w, p, n, m, T, sh), true);
+            } else {
+                const float4* src = a.src + a.src_off[p];
+                for (int i = tid; i < n; i += kSoloWG) {
+                    const float4 s = src[i];
+                    float4 o = s;
+                    xform_pt(T, s.x, s.y, s.z, o.x, o.y, o.z);
+                    a.aligned[a.src_off[p] + i] = o;  // (.w: the input's intensity)
+                }
+            }
+        }
+    }
+    // Registration::getFitnessScore: the sequential double sum over points with d² <= max_range in
+    // index order (wave 0 lane 0 over LDS chunks the other waves fill; points beyond contribute +0)
+    // and the exact count (finish_kernel's fold, bit for bit)
+    const bool have = valid && kp.compute_fitness && n > 0;
+    double fsum = 0.0;
+    int fcnt = 0;
+    if (have) {
+        const NNKey* key = w.nn_key + xs0;
+        const int nch = (n + kSoloFitChunk - 1) / kSoloFitChunk;
+        auto fill = [&](int c) {
+            const int base = c * kSoloFitChunk, len = min(kSoloFitChunk, n - base);
+            for (int o = tid - 64; o < len; o += kSoloWG - 64) {
+                const float d2 = key_d2(key[base + o]);
+                const bool in = (double)d2 <= kp.fit_max_range;
+                sh.u.fit[c & 1][o] = in ? d2 : 0.0f;
+                fcnt += in ? 1 : 0;
+            }
+        };
+        if (wave >= 1) fill(0);
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (wave == 0) {
+                if (lane == 0) fsum = fold_seq<double>(sh.u.fit[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
+            } else if (c + 1 < nch) {
+                fill(c + 1);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) fcnt += __shfl_xor(fcnt, off, 64);
+        if (lane == 0) sh.wtot[wave] = fcnt;
+        __syncthreads();
+        fcnt = 0;
+        for (int k = 0; k < kLdsWaves; ++k) fcnt += sh.wtot[k];
+    }
+    if (tid == 0) {
+        Result r;
+        for (int k = 0; k < 16; ++k) r.T[k] = st.final_T[k];
+        r.fitness = (have && fcnt > 0) ? fsum / fcnt : DBL_MAX;
+        r.iterations = st.iterations;
+        r.converged = st.phase == kPhaseConverged ? 1 : 0;
+        r.status = st.status;
+        r.convergence_state = st.conv_state;
+        r.n_correspondences = st.ncorr;
+        r.reserved = 0;
+        a.results[p] = r;
+    }
+    if (lane == 0) {
+        count_add(w.evals, 0, rs.evals);
+        count_add(w.evals, 1, rs.tests);
+    }
+}
+
 // Test hook: the device float Umeyama rotation for k sigma matrices (one thread each).
 __global__ void rot_f32_kernel(const float* sigma, float* R, int k) {
     __shared__ SvdWorkF ws[64];
@@ -3423,7 +3814,7 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
 }
 
 hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int fitness_pass, int first,
-                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused) {
+                         int ncu, hipStream_t st, const NNLdsEvents& ev, int test_fused, int ordered) {
     // (query records: source index and sorted position in kNtPosShift bits each, every mode)
     if (w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || npairs <= 0 || max_n > (1 << kNtPosShift))
         return hipErrorInvalidValue;
@@ -3438,8 +3829,10 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
         hipLaunchKernelGGL(nn_cache_test_kernel, dim3(chunks, npairs), dim3(kTestWG), 0, st, a, w, fitness_pass);
         if (ev.test_stop && (e = hipEventRecord(ev.test_stop, st)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(nn_order_kernel, dim3(1), dim3(kOrderWG), 0, st, a, w, npairs, fitness_pass,
-                       (first || !cache) ? 1 : 0, ncu);
+    if (ordered && (first || !cache || fitness_pass || !test_fused)) return hipErrorInvalidValue;
+    if (!ordered)
+        hipLaunchKernelGGL(nn_order_kernel, dim3(1), dim3(kOrderWG), 0, st, a, w, npairs, fitness_pass,
+                           (first || !cache) ? 1 : 0, ncu);
     const int grid = npairs < ncu ? npairs : ncu;  // persistent: one workgroup per CU (LDS-bound)
     if (ev.search_start && (e = hipEventRecord(ev.search_start, st)) != hipSuccess) return e;
     if (cache)
@@ -3505,14 +3898,25 @@ hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, 
 }
 
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr, hipStream_t st,
-                         int tail_test) {
+                         int tail_test, int order_ncu) {
+    if (order_ncu > 0 && (!tail_test || !w.owork || !w.plist || !w.plist_n || !w.nn_u || a.kp.numerics != kNumericsPCL))
+        return hipErrorInvalidValue;
     if (a.kp.numerics == kNumericsPCL) {
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
-        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test);
+        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test, order_ncu);
     } else {
         hipLaunchKernelGGL(update_f64_kernel, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_solo(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int iters, hipStream_t st) {
+    if (a.kp.numerics != kNumericsPCL || w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || max_n > kCacheMaxN ||
+        w.x_stride > kCacheMaxN || !w.tsort || !w.tbox || !w.sbox || !w.sperm || !w.nn_u || !w.nn_t || !w.qv ||
+        !w.qm || !w.sq || !w.sm || npairs <= 0 || iters <= 0)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(solo_kernel, dim3(npairs), dim3(kSoloWG), 0, st, a, w, iters);
     return hipGetLastError();
 }
 

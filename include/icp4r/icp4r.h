@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ICP4R_ABI_VERSION 2
+#define ICP4R_ABI_VERSION 3
 
 typedef enum icp4r_status {
     ICP4R_OK = 0,
@@ -220,6 +220,10 @@ typedef struct icp4r_plan_info {
                            without a search when a second-nearest bound proves it;
                            exact); off with ICP4R_NN_CACHE=0                          */
     int64_t nn_blocks;  /* workgroups of one NN launch                               */
+    int32_t solo;       /* 1: a PCL-numerics registration of this shape runs whole in one
+                           workgroup per pair (solo_kernel: targets <= 8192, sources <=
+                           16384, fewer than 256 pairs); off with ICP4R_SOLO=0        */
+    int32_t reserved;
 } icp4r_plan_info;
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);
 

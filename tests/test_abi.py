@@ -77,7 +77,7 @@ def test_params_default_matches_pcl():
     assert math.isinf(p.huber_delta)
     assert p.fitness_max_range == sys.float_info.max
     L = icp4r.load()
-    assert L.icp4r_abi_version() == 2
+    assert L.icp4r_abi_version() == 3
     assert b"gfx950" in L.icp4r_version()
 
 
@@ -102,10 +102,16 @@ def test_plan_geometry(monkeypatch):
     monkeypatch.delenv("ICP4R_NN_LDS")
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
-    single = icp4r.plan(1, 8192, 8192)  # C2: LDS-tiled search, one target tile x 8 query parts of 1024
-    assert single["pruned"] and not single["lds"] and single["nn_blocks"] == 8
+    single = icp4r.plan(1, 8192, 8192)  # C2: the whole registration in one workgroup (solo_kernel)
+    assert single["pruned"] and not single["lds"] and single["solo"] and single["nn_blocks"] == 1
+    assert icp4r.plan(200, 16384, 8192)["solo"] and not icp4r.plan(200, 16385, 8192)["solo"]
+    assert not big["solo"] and not icp4r.plan(1, 8192, 8193)["solo"]
+    monkeypatch.setenv("ICP4R_SOLO", "0")  # the multi-launch plan: one target tile x 8 query parts of 1024
+    single = icp4r.plan(1, 8192, 8192)
+    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 8
+    monkeypatch.delenv("ICP4R_SOLO")
     c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 8 query parts
-    assert c5["pruned"] and not c5["lds"] and c5["nn_blocks"] == 8 * 9
+    assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 8 * 9
     monkeypatch.setenv("ICP4R_NN_TILE", "0")  # the streamed kernel instead
     single = icp4r.plan(1, 8192, 8192)  # one query per lane, the target in 4 chunks
     assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32 * 4

@@ -176,21 +176,23 @@ def test_target_split_equals_unsplit(gpu_ctx):
         assert (res[k]["T"] == np.array(r.T, np.float32)).all()
 
 
-@pytest.mark.parametrize("lds,cache,tile", [("0", "1", "1"), ("0", "1", "0"), ("1", "0", "1"), ("1", "1", "1")])
+@pytest.mark.parametrize("lds,cache,tile,solo", [("0", "1", "1", "1"), ("0", "1", "1", "0"), ("0", "1", "0", "0"),
+                                                ("1", "0", "1", "1"), ("1", "1", "1", "1")])
 @pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map", "big_src", "huge_src"])
-def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, monkeypatch):
-    """Pruned (LDS target tiles x query parts, the scalar-cache stream, or with the target set in LDS
-    and per-query work lists, with or without the cached-neighbour test), brute-force and packed
-    searches produce bit-identical registrations (T, fitness, iterations, aligned cloud) — the pruned
-    index changes only which targets are evaluated.  dup_map: every target twice, the copies in
-    different tiles of a > 8192-point target, so ties resolve across tiles (lowest index).  big_src:
-    a batch mixing sources of more than 8192 points (their own index) with ones ordered by the
-    target's tree."""
+def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, monkeypatch):
+    """Pruned (the whole registration per workgroup, LDS target tiles x query parts, the scalar-cache
+    stream, or with the target set in LDS and per-query work lists, with or without the
+    cached-neighbour test), brute-force and packed searches produce bit-identical registrations (T,
+    fitness, iterations, aligned cloud) — the pruned index changes only which targets are evaluated.
+    dup_map: every target twice, the copies in different tiles of a > 8192-point target, so ties
+    resolve across tiles (lowest index).  big_src: a batch mixing sources of more than 8192 points
+    (their own index) with ones ordered by the target's tree."""
     import icp4r
 
     monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
     monkeypatch.setenv("ICP4R_NN_CACHE", cache)
     monkeypatch.setenv("ICP4R_NN_TILE", tile)  # 0: the scalar-cache stream for the unbatched plan
+    monkeypatch.setenv("ICP4R_SOLO", solo)  # 0: the multi-launch unbatched plan (solo_kernel off)
     guess = None
     if case == "c2":
         pairs = [_pair(310, 8192)]
@@ -288,13 +290,18 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
     kw = {} if early else dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     p = icp4r.default_params(max_iterations=20, **kw)
     out = {}
-    for fuse in ("0", "1"):
+    # (ICP4R_FUSE_ORDER=1, the default: the update's last workgroup also builds the next search's
+    # work list from the words the other workgroups publish; 0: nn_order_kernel does)
+    for fuse, order in (("0", "1"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("ICP4R_FUSE_TEST", fuse)
+        monkeypatch.setenv("ICP4R_FUSE_ORDER", order)
         gpu_ctx.reset_timers()
-        out[fuse] = gpu_ctx.align_batch_host(*args, params=p)
+        out[fuse + order] = gpu_ctx.align_batch_host(*args, params=p)
         st = gpu_ctx.nn_stats()
         assert (st["tested_in_update"] > 0) == (fuse == "1")
-    assert out["1"].tobytes() == out["0"].tobytes()
+    assert out["10"].tobytes() == out["01"].tobytes()
+    assert out["11"].tobytes() == out["01"].tobytes()
+    out["1"] = out["11"]
     assert (out["1"]["status"] == 0).all()
     if early:
         assert len(set(out["1"]["iterations"].tolist())) > 1  # pairs stop at different iterations
