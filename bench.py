@@ -326,6 +326,10 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
     evals = st["evaluations"] / max(nn_launches, 1)
     tests = st["box_tests"] / max(nn_launches, 1)
     plan = icp4r.plan(1, n, m)
+    iters = int(r.iterations)
+    if plan["solo"]:
+        return _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_ms, calls, nn_ms,
+                             nn_launches, st, plan, cpu_budget_s, fitness_passes, check)
     kernel = "nn_tile_kernel" if plan["pruned"] and not plan["lds"] else "nn_kernel"
     flops = evals * FLOP_PER_PAIR_EVAL + tests * FLOP_PER_BOX_TEST
     tflops = flops / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
@@ -346,7 +350,6 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
         a = b / (nn_ms * 1e-3) / 1e9 if nn_ms > 0 else 0.0
         roof["hbm_formula"] = {"bytes_per_launch": b, "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": a / PEAK_HBM_GBS}
-    iters = int(r.iterations)
     floor_ms = 2 * n * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
     out = {"workload": workload, "value": 1e3 / dev_ms if dev_ms > 0 else None, "unit": "pairs/s",
            "registration_device_ms": dev_ms, "registration_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
@@ -357,6 +360,11 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
                              "chain_floor_ms": floor_ms, "frac_of_floor": floor_ms / upd_ms if upd_ms > 0 else None},
            "nn_plus_update_share_of_device_time": (nn_ms * nn_launches + upd_ms * upd_launches) / max(calls, 1) / dev_ms
            if dev_ms > 0 else None}
+    _check_and_cpu(ctx, out, r, src, tgt, params, oparams, cpu_budget_s, fitness_passes, check)
+    return out
+
+
+def _check_and_cpu(ctx, out: dict, r, src, tgt, params, oparams: dict, cpu_budget_s, fitness_passes: int, check: bool):
     if check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # checker only: the registration above was timed without it
@@ -364,12 +372,47 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
         o = oracle.align(src, tgt, aligned=True, **oparams)
         r2, al = ctx.align(src, tgt, params, want_aligned=True)  # (untimed: the aligned cloud too)
         out["bit_exact_vs_oracle"] = bool((r.matrix() == o["T"]).all() and r.fitness == o["fitness"] and
-                                          iters == o["iterations"] and bytes(r2) == bytes(r) and
+                                          int(r.iterations) == o["iterations"] and bytes(r2) == bytes(r) and
                                           (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all())
     if cpu_budget_s:
         cpu = single_pair_cpu(src, tgt, oparams, cpu_budget_s, fitness_passes)
         out["cpu_baseline"] = cpu
         out["speedup_vs_cpu"] = out["value"] / cpu["value"] if out["value"] else None
+
+
+def _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_ms, calls, solo_ms, solo_launches, st,
+                  plan, cpu_budget_s, fitness_passes, check) -> dict:
+    """The solo plan (solo_kernel: every ICP iteration and the fitness pass of the pair in one
+    1024-thread workgroup, after init_kernel and index_kernel).  Its bound is latency: the
+    registration is a dependent chain — per iteration the cached-neighbour test, the search of the
+    misses, then PCL's sequential float folds (2 x n dependent adds: pass A's centroids before pass B's
+    cross-covariance) and the serial 3x3 solve; the fitness pass ends in a sequential double sum of n
+    terms.  `chain_floor_ms` is those fold chains alone at the dependent-add latency measured for
+    them (CHAIN_CYCLES_PER_ADD, tools/experiments/chain_bench.hip); frac = floor / kernel time.  The
+    FP32 VALU figures of the search beside it are the device-counted evaluations and box tests of the
+    whole registration over the kernel time."""
+    n, m = len(src), len(tgt)
+    iters = int(r.iterations)
+    per = max(solo_launches, 1)
+    evals = st["evaluations"] / per
+    tests = st["box_tests"] / per
+    flops = evals * FLOP_PER_PAIR_EVAL + tests * FLOP_PER_BOX_TEST
+    floor_ms = (2 * n * iters + n) * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
+    tflops = flops / (solo_ms * 1e-3) / 1e12 if solo_ms > 0 else 0.0
+    roof = {"bound": "latency", "kernel": "solo_kernel", "achieved": floor_ms, "peak": solo_ms, "unit": "ms",
+            "frac": floor_ms / solo_ms if solo_ms > 0 else None, "chain_floor_ms": floor_ms,
+            "avg_launch_ms": solo_ms, "launches_per_registration": solo_launches / max(calls, 1),
+            "kernel_share_of_device_time": solo_ms * solo_launches / max(calls, 1) / dev_ms if dev_ms > 0 else None,
+            "valu": {"achieved": tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tflops / PEAK_FP32_TFLOPS,
+                     "evaluations_per_registration": evals, "box_tests_per_registration": tests,
+                     "evaluated_fraction_of_brute_force": evals / (n * m * (iters + 1))},
+            "cache_hit_rate": st["cache_hits"] / st["cache_tested"] if st["cache_tested"] else None,
+            "note": "achieved / peak here = the fold-chain floor / the kernel's time (latency-bound: PCL's "
+                    "sequential summation order); see DESIGN.md §5 solo_kernel"}
+    out = {"workload": workload, "value": 1e3 / dev_ms if dev_ms > 0 else None, "unit": "pairs/s",
+           "registration_device_ms": dev_ms, "registration_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
+           "status": int(r.status), "iterations": iters, "plan": plan, "roofline": roof}
+    _check_and_cpu(ctx, out, r, src, tgt, params, oparams, cpu_budget_s, fitness_passes, check)
     return out
 
 

@@ -280,6 +280,12 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.nn_t = static_cast<float4*>(ctx->nn_t.p);
             w.sq = static_cast<float4*>(ctx->sq.p);
             w.sm = static_cast<uint2*>(ctx->sm.p);
+            // (the test's per-pair count and, for an overflowing miss list, its bitmap: written only)
+            w.need_stride = (x_stride + 31) / 32;
+            HIP_TRY(ctx->need.ensure((size_t)npairs * w.need_stride * sizeof(uint32_t)));
+            HIP_TRY(ctx->miss_cnt.ensure((size_t)npairs * sizeof(int32_t)));
+            w.need = static_cast<uint32_t*>(ctx->need.p);
+            w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
             w.defer_xform = 1;
         }
         if (pl.lds) {
@@ -427,7 +433,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // does not (C1 0.75 -> 0.80 ms), so the unbatched plans build the source's own tree
     w.src_by_tgt = (pl.pruned && pl.lds) ? (env_int("ICP4R_SRC_ORDER", 1) != 0 ? 1 : 0)
                                          : (pl.pruned && env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0);
-    w.stage_first = (w.src_by_tgt && pl.lds && w.qv && w.qm) ? 1 : 0;
+    w.stage_first = (w.src_by_tgt && (pl.lds || pl.solo) && w.qv && w.qm) ? 1 : 0;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));

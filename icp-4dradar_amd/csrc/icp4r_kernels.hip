@@ -329,6 +329,10 @@ typedef uint32_t kd_flag_t;
 #else
 typedef uint8_t kd_flag_t;
 #endif
+#ifndef ICP4R_IDX_TOUCH
+#define ICP4R_IDX_TOUCH 1  // index_kernel: the cloud's lines touched (coalesced) before the sorted gather
+#endif
+
 struct KdShared {
     uint16_t L[3][kKdMaxN];  // per axis: the point indices, sorted by that axis inside every segment
     union {
@@ -719,6 +723,18 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
             // a load-use loop had waited out one global round trip per position.  (t_stride is a
             // multiple of 64, so the position guard is wave-uniform: the shuffles below see every lane.)
             constexpr int kG = kKdPer / 2;  // two rounds of 8 (16 in flight spilled registers)
+#if ICP4R_IDX_TOUCH
+            // Every 128-B line of the cloud touched first (one dword each, coalesced): the gather below
+            // reads it in sorted order, 16 B per line visit, and the ~100 us of levels since the
+            // bounding-box read let the other builds on this XCD (two per CU, 8 MB of clouds against a
+            // 4-MB L2) evict it — each scattered 16-B load then refetched its whole line.
+            {
+                const uint32_t* pw = reinterpret_cast<const uint32_t*>(pts);
+                uint32_t acc = 0;
+                for (int l = tid; l < (n * 16 + 127) / 128; l += kIdxWG) acc ^= pw[l * 32];
+                asm volatile("" ::"v"(acc));
+            }
+#endif
 #pragma unroll
             for (int k0 = 0; k0 < kKdPer; k0 += kG) {
             float cx[kG], cy[kG], cz[kG];
@@ -3509,137 +3525,129 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
 // launches, their boundaries and the target staging of the multi-launch plan; every result is
 // bit-identical to it (the same per-query and per-chain arithmetic in the same order).
 constexpr int kSoloWG = kLdsWG;
-constexpr int kSoloChunk = 192;  // fold chunk (points): two 96-float steps of fold_seq per chain
-constexpr int kSoloRow = kSoloChunk + kFoldPad;
 constexpr int kSoloFitChunk = 960;  // fitness chunk: 15 waves fill, wave 0 lane 0 folds
-constexpr int kSoloGrp = 4;         // the test's sorted positions in flight per thread
+constexpr int kSoloGrp = 4;         // the first pass' sorted positions in flight per thread
+// the test's LDS miss records (24 B each) in the tile's region, after the bitmap and its prefixes
+constexpr int kSoloRecs = ((int)(sizeof(v4f) * kLdsTargets + 4 * 6 * (kLdsTargets / kLdsLeaf) * 9 / 8) -
+                           8 * kNeedWords) / 24 & ~15;
+// LDS: the target tile (search) and the update's fold buffers (fold_update_kernel's 512-point
+// double buffer: a chunk's fold outlasts its fillers' L2 round trip) take turns in one region — the
+// tile is restaged from the L2 for each search (~128 KB of this XCD's L2 per iteration; smaller
+// chunks beside a resident tile left the fold chains waiting on their fillers); the search's
+// per-wave state has its own.
 struct SoloShared {
-    v4f tl[kLdsTargets];
-    alignas(16) float bx[kLdsTargets / kLdsLeaf][6];
-    float sbx[kLdsTargets / kLdsLeaf / kSuper][6];
     union {
-        struct {  // the search's per-wave state
-            unsigned long long best[kLdsWaves][64];
-            uint32_t sec[kLdsWaves][64];
-            uint16_t items[kLdsWaves][kRing + 64];
-        } s;
+        struct {  // the search
+            v4f tl[kLdsTargets];
+            alignas(16) float bx[kLdsTargets / kLdsLeaf][6];
+            float sbx[kLdsTargets / kLdsLeaf / kSuper][6];
+        } t;
         struct {  // the update
-            alignas(16) float buf[2][9][kSoloRow];
+            alignas(16) float buf[2][9][kFoldRow];
             float res[8];
             int32_t cnt[kLdsWaves];
             SolveShared sv;
         } f;
         alignas(16) float fit[2][kSoloFitChunk];  // the fitness sum's chunks
-    } u;
+        struct {  // the cached-neighbour test: the miss bitmap, its word prefixes, the miss records
+            uint32_t need[kNeedWords];
+            int32_t pre[kNeedWords];
+            float4 lv[kSoloRecs];
+            uint2 lm[kSoloRecs];
+        } c;
+    } a;
+    struct {  // the search's per-wave state
+        unsigned long long best[kLdsWaves][64];
+        uint32_t sec[kLdsWaves][64];
+        uint16_t items[kLdsWaves][kRing + 64];
+    } s;
     int32_t wtot[kLdsWaves];  // per-wave counts (the test's misses, the fitness count)
+    int32_t mcount;           // the test's LDS record count
 };
 static_assert(sizeof(SoloShared) <= 160 * 1024, "solo LDS");
 
-// The solo plan's cached-neighbour test over sorted positions: thread t takes positions
-// [t * per, (t + 1) * per), 8 at a time with every load in flight, and the misses' records go to the
-// query list at their rank among all misses (a workgroup scan): qv = {x, y, z, U}, qm = {source index
-// | sorted position << 14, the cached NN's sorted target position}.  MODE 0: the first pass — every
-// source, X as init_kernel wrote it, U = +inf, seeded at the target of the same relative sorted
-// position; 1: an iteration pass — X := T_inc X (PCL's transformCloud, deferred), X and U written;
-// 2: the fitness pass — T = final applied to the input, a hit's key (its d² is what the fitness sum
-// reads), the aligned output.  Returns the list length.
-template <int MODE>
-__device__ int solo_test(const PairArgs& a, const WorkArgs& w, int p, int n, int m, const float (&T)[16],
-                         SoloShared& sh) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// The first pass' query list of the solo plan: every source in sorted-position order (thread t takes
+// positions [t * per, (t + 1) * per), kSoloGrp at a time with every load in flight): qv = {X_i as
+// init_kernel wrote it, U = +inf}, qm = {source index | sorted position << 14, the target at the same
+// relative sorted position — the seed}.  Returns n.
+__device__ int solo_first_list(const PairArgs& a, const WorkArgs& w, int p, int n, int m) {
+    const int tid = threadIdx.x;
     const int64_t xs0 = (int64_t)p * w.x_stride;
-    float4* X = w.X + xs0;
-    float* uu = w.nn_u + xs0;
-    const float4* nt = w.nn_t + xs0;
+    const float4* X = w.X + xs0;
     const int32_t* sperm = w.sperm + xs0;
     float4* qv = w.qv + xs0;
     uint2* qm = w.qm + xs0;
     const int per = (n + kSoloWG - 1) / kSoloWG;
     const int k0 = min(tid * per, n), k1 = min(k0 + per, n);
-    uint32_t missbits = 0;
-    int c = 0;
     for (int g = k0; g < k1; g += kSoloGrp) {
         int ii[kSoloGrp];
+        float4 v[kSoloGrp];
 #pragma unroll
         for (int e = 0; e < kSoloGrp; ++e) ii[e] = sperm[min(g + e, k1 - 1)];
-        float4 v[kSoloGrp], t[kSoloGrp], s[kSoloGrp];
-        float U[kSoloGrp];
 #pragma unroll
-        for (int e = 0; e < kSoloGrp; ++e) {
-            v[e] = X[ii[e]];
-            if (MODE != 0) {
-                t[e] = nt[ii[e]];
-                U[e] = uu[ii[e]];
-            }
-            if (MODE == 2) s[e] = a.src[a.src_off[p] + ii[e]];
-        }
+        for (int e = 0; e < kSoloGrp; ++e) v[e] = X[ii[e]];
 #pragma unroll
         for (int e = 0; e < kSoloGrp; ++e) {
             const int k = g + e;
             if (k >= k1) break;
-            const int i = ii[e];
-            if (MODE == 0) {
-                qv[k] = make_float4(v[e].x, v[e].y, v[e].z, INFINITY);
-                qm[k] = make_uint2((uint32_t)i | ((uint32_t)k << kNtPosShift), (uint32_t)(((int64_t)k * m) / n));
-                continue;
-            }
-            float4 o = v[e];
-            if (MODE == 2)
-                xform_pt(T, s[e].x, s[e].y, s[e].z, o.x, o.y, o.z);  // final * input
-            else
-                xform_pt(T, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);  // PCL transformCloud, in place
-            const float2 Lm = move_lu(make_float2(v[e].w, U[e]), v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
-            o.w = Lm.x;
-            const float d2 = l2_simple(o.x, o.y, o.z, t[e].x, t[e].y, t[e].z);
-            const bool hit = cache_hit(Lm.x, d2);
-            if (MODE == 1) {
-                X[i] = o;
-                uu[i] = Lm.y;
-            }
-            if (MODE == 2 && a.aligned) a.aligned[a.src_off[p] + i] = make_float4(o.x, o.y, o.z, s[e].w);
-            if (hit) {
-                if (MODE == 2) w.nn_key[xs0 + i] = make_key(d2, nt_tpos(t[e].w));  // (d² only: finish)
-            } else {
-                // the record at its sorted position for now; moved to its rank below
-                w.sq[xs0 + k] = make_float4(o.x, o.y, o.z, Lm.y);
-                w.sm[xs0 + k] = make_uint2((uint32_t)i | ((uint32_t)k << kNtPosShift), nt_tpos(t[e].w));
-                missbits |= 1u << (k - k0);
-                ++c;
-            }
+            qv[k] = make_float4(v[e].x, v[e].y, v[e].z, INFINITY);
+            qm[k] = make_uint2((uint32_t)ii[e] | ((uint32_t)k << kNtPosShift), (uint32_t)(((int64_t)k * m) / n));
         }
     }
-    if (MODE == 0) return n;
-    // cached-neighbour test counters (nn_stats: evaluations, hits, tested)
-    const unsigned long long hits = wave_sum((unsigned long long)(max(k1 - k0, 0) - c));
-    const unsigned long long tested = wave_sum((unsigned long long)max(k1 - k0, 0));
-    if (lane == 0) {
-        count_add(w.evals, 0, hits);
-        count_add(w.evals, 2, hits);
-        count_add(w.evals, 3, tested);
-    }
-    // rank of this thread's first miss: an exclusive scan of the per-thread counts
-    int incl = c;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-    }
-    if (lane == 63) sh.wtot[wave] = incl;
+    return n;
+}
+
+// The cached-neighbour test of an iteration pass (FROM_SRC = false: X := T_inc X, deferred) or of
+// the fitness pass (FROM_SRC: T = final applied to the input): pair_cache_test by the whole
+// workgroup, its records in the tile's LDS region; when they overflow it (a pair far from
+// converged), the records left in sq / sm are placed at their ranks here.  Returns the list length.
+template <bool FROM_SRC>
+__device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
+                               SoloShared& sh) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwords = (n + 31) >> 5;
+    for (int k = tid; k < nwords; k += kSoloWG) sh.a.c.need[k] = 0u;
+    if (tid == 0) sh.mcount = 0;
     __syncthreads();
-    int base = 0, total = 0;
-    for (int v = 0; v < kLdsWaves; ++v) {
-        const int s = sh.wtot[v];
-        base += v < wave ? s : 0;
-        total += s;
+    const int tot = pair_cache_test<kSoloWG, 2, FROM_SRC>(a, w, p, n, T, sh.a.c.need, sh.a.c.pre, sh.a.c.lv,
+                                                         sh.a.c.lm, kSoloRecs, &sh.mcount, sh.wtot, FROM_SRC);
+    if (tot <= kSoloRecs) return tot;
+    // overflow: every record is in sq / sm (test order), the bitmap still in LDS — word prefixes
+    // (wave 0), then each record to its rank
+    __syncthreads();
+    if (wave == 0) {
+        constexpr int kW = kNeedWords / 64;
+        int c[kW], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            const int wd = lane * kW + j;
+            c[j] = wd < nwords ? __builtin_popcount(sh.a.c.need[wd]) : 0;
+            sum += c[j];
+        }
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        int run = incl - sum;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            sh.a.c.pre[lane * kW + j] = run;
+            run += c[j];
+        }
     }
-    int r = base + incl - c;
-    for (uint32_t b = missbits; b; b &= b - 1) {  // (this thread's own records: no barrier needed)
-        const int k = k0 + __builtin_ctz(b);
-        qv[r] = w.sq[xs0 + k];
-        qm[r] = w.sm[xs0 + k];
-        ++r;
+    __syncthreads();
+    const int64_t xs0 = (int64_t)p * w.x_stride;
+    for (int k = tid; k < tot; k += kSoloWG) {
+        const float4 r = w.sq[xs0 + k];
+        const uint2 m = w.sm[xs0 + k];
+        const uint32_t sp = min(m.y, (uint32_t)(n - 1));
+        const int rk = sh.a.c.pre[sp >> 5] + __builtin_popcount(sh.a.c.need[sp >> 5] & ((1u << (sp & 31)) - 1u));
+        w.qv[xs0 + rk] = r;
+        w.qm[xs0 + rk] = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
     }
-    return total;
+    return tot;
 }
 
 __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, int iters) {
@@ -3653,35 +3661,55 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
     const int64_t xs0 = (int64_t)p * w.x_stride;
     const bool valid = uload(&st.phase) != kPhaseInvalid;
     const int nsb = (((m + kLdsLeaf - 1) / kLdsLeaf) + kSuper - 1) / kSuper;
-    const LdsTile tile{sh.tl, sh.bx, sh.sbx};
+    const LdsTile tile{sh.a.t.tl, sh.a.t.bx, sh.a.t.sbx};
     RunStats rs;
     auto search = [&](int nlist, bool keys) {
-        __syncthreads();  // the list (global, this workgroup's) and the union's previous use
-        const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
-        const int sbl = min(lane, nsb - 1);
-        const v4f isl = sbg[2 * sbl], ish = sbg[2 * sbl + 1];
-        lds_runs<true>(tile, sh.u.s.best[wave], sh.u.s.sec[wave], sh.u.s.items[wave], w.qv + xs0, w.qm + xs0, nlist, m,
-                       nsb, isl, ish, a, w, p, xs0, w.X + xs0, w.nn_key + xs0, keys, false, rs);
-        __syncthreads();
-    };
-    if (valid) {
+        __syncthreads();  // the list (global, this workgroup's) and the region's previous use
         v4f isl, ish;
         stage_tile<kSoloWG>(tile, w, p, nsb, isl, ish);
+        __syncthreads();
+        lds_runs<true>(tile, sh.s.best[wave], sh.s.sec[wave], sh.s.items[wave], w.qv + xs0, w.qm + xs0, nlist, m, nsb,
+                       isl, ish, a, w, p, xs0, w.X + xs0, w.nn_key + xs0, keys, false, rs);
+        __syncthreads();
+    };
+    // debug (ICP4R_PHASE_TICKS=1): pair 0's phase walls summed over the registration (s_memrealtime,
+    // 100 MHz) into ticks[0..9]: staging, test, search, pass A, pass B, solve, fitness test, fitness
+    // search, fitness sum, iterations (tools/solo_phases.py)
+    unsigned long long* tk = (w.ticks && p == 0 && tid == 0) ? reinterpret_cast<unsigned long long*>(w.ticks) : nullptr;
+    uint64_t tk_last = tk ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tick = [&](int slot) {
+        if (!tk) return;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        tk[slot] += now - tk_last;
+        tk_last = now;
+    };
+    if (valid) {
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = 0.0f;
         int flag = 0;
+        __syncthreads();
+        tick(0);
         for (int it = 0; it < iters && flag == 0; ++it) {
-            const int nlist = it == 0 ? solo_test<0>(a, w, p, n, m, T, sh) : solo_test<1>(a, w, p, n, m, T, sh);
+            // (first pass: src_order_kernel wrote the records, seeded at the source's kd leaf in the
+            // target's tree, when the sources are ordered by it — ICP4R_SRC_ORDER=1)
+            const int nlist = it > 0 ? solo_cache_test<false>(a, w, p, n, T, sh)
+                              : (w.stage_first && src_by_tgt_tree(a, w, p)) ? n : solo_first_list(a, w, p, n, m);
+            tick(1);
             search(nlist, false);
+            tick(2);
             const FoldIn fin{nullptr, w.X + xs0, w.nn_t + xs0, n};
-            fold_pass_a<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, sh.u.f.buf, sh.u.f.res, sh.u.f.cnt, sh.u.f.sv);
-            fold_pass_b<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, sh.u.f.buf, sh.u.f.sv);
-            if (tid == 0) solve_pair<kNumericsPCL>(sh.u.f.sv, st, kp);
+            fold_pass_a<kSoloWG, kFoldChunkP, kFoldRow>(kp, fin, sh.a.f.buf, sh.a.f.res, sh.a.f.cnt, sh.a.f.sv);
+            tick(3);
+            fold_pass_b<kSoloWG, kFoldChunkP, kFoldRow>(kp, fin, sh.a.f.buf, sh.a.f.sv);
+            tick(4);
+            if (tid == 0) solve_pair<kNumericsPCL>(sh.a.f.sv, st, kp);
             __syncthreads();
-            flag = sh.u.f.sv.flag;
+            tick(5);
+            if (tk) tk[9] += 1;
+            flag = sh.a.f.sv.flag;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) T[q] = sh.u.f.sv.T_inc[q];  // the next pass's deferred transform
+            for (int q = 0; q < 16; ++q) T[q] = sh.a.f.sv.T_inc[q];  // the next pass's deferred transform
         }
         // the fitness pass (getFitnessScore after align) and align's output: final * input
         if (kp.compute_fitness || a.aligned) {
@@ -3689,7 +3717,20 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
 #pragma unroll
             for (int q = 0; q < 16; ++q) T[q] = st.final_T[q];
             if (kp.compute_fitness) {
-                search(solo_test<2>(a, w, p, n, m, T, sh), true);
+                const int nlist = solo_cache_test<true>(a, w, p, n, T, sh);
+                tick(6);
+                search(nlist, true);
+                tick(7);
+                if (a.aligned) {  // X = final * input (the test wrote it, the search rewrote its misses)
+                    __syncthreads();
+                    const float4* src = a.src + a.src_off[p];
+                    const float4* X = w.X + xs0;
+                    for (int i = tid; i < n; i += kSoloWG) {
+                        float4 v = X[i];
+                        v.w = src[i].w;  // intensity copied through
+                        a.aligned[a.src_off[p] + i] = v;
+                    }
+                }
             } else {
                 const float4* src = a.src + a.src_off[p];
                 for (int i = tid; i < n; i += kSoloWG) {
@@ -3715,7 +3756,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
             for (int o = tid - 64; o < len; o += kSoloWG - 64) {
                 const float d2 = key_d2(key[base + o]);
                 const bool in = (double)d2 <= kp.fit_max_range;
-                sh.u.fit[c & 1][o] = in ? d2 : 0.0f;
+                sh.a.fit[c & 1][o] = in ? d2 : 0.0f;
                 fcnt += in ? 1 : 0;
             }
         };
@@ -3723,7 +3764,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
             if (wave == 0) {
-                if (lane == 0) fsum = fold_seq<double>(sh.u.fit[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
+                if (lane == 0) fsum = fold_seq<double>(sh.a.fit[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
             } else if (c + 1 < nch) {
                 fill(c + 1);
             }
@@ -3735,6 +3776,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         fcnt = 0;
         for (int k = 0; k < kLdsWaves; ++k) fcnt += sh.wtot[k];
     }
+    tick(8);
     if (tid == 0) {
         Result r;
         for (int k = 0; k < 16; ++k) r.T[k] = st.final_T[k];
@@ -3914,7 +3956,7 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
 hipError_t launch_solo(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int iters, hipStream_t st) {
     if (a.kp.numerics != kNumericsPCL || w.leaf != kLdsLeaf || w.t_stride > kLdsTargets || max_n > kCacheMaxN ||
         w.x_stride > kCacheMaxN || !w.tsort || !w.tbox || !w.sbox || !w.sperm || !w.nn_u || !w.nn_t || !w.qv ||
-        !w.qm || !w.sq || !w.sm || npairs <= 0 || iters <= 0)
+        !w.qm || !w.sq || !w.sm || !w.need || !w.miss_cnt || npairs <= 0 || iters <= 0)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(solo_kernel, dim3(npairs), dim3(kSoloWG), 0, st, a, w, iters);
     return hipGetLastError();

@@ -437,15 +437,19 @@ def test_pcl_facade_callsite(oracle_mod, golden, exe_name):
     assert float(kv["score"]) == o["fitness"]
 
 
-def test_kernel_timing_api(gpu_ctx):
+@pytest.mark.parametrize("solo", ["1", "0"])
+def test_kernel_timing_api(gpu_ctx, solo, monkeypatch):
+    """The NN kernel timer counts one launch per NN pass (5 iterations + the fitness pass) on the
+    multi-launch plan, and the one solo_kernel launch of the whole registration on the solo plan."""
     import icp4r
 
+    monkeypatch.setenv("ICP4R_SOLO", solo)
     gpu_ctx.reset_timers()
     s, t = _pair(700, 2048)
     gpu_ctx.align(s, t, icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1))
     ms, k = gpu_ctx.kernel_time_ms()
     bms, bk = gpu_ctx.batch_time_ms()
-    assert k == 6 and ms > 0 and bk == 1 and bms >= ms
+    assert k == (1 if solo == "1" else 6) and ms > 0 and bk == 1 and bms >= ms
 
 
 def _brute_nn(q, t):
