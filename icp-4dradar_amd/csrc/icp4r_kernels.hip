@@ -203,12 +203,15 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     const bool id = ident != 0;
     const int nc = min(n, (int)w.x_stride);
     int bad = 0;
-    for (int i0 = 0; i0 < m; i0 += kInitWG * kInitPer) {
-        float4 t[kInitPer];
+    // (the target is only validated: 16 points per thread in flight — a scan-to-map target of 65k
+    // points had taken 64 dependent rounds of 1024, ~65 us of a single registration)
+    constexpr int kTgtPer = 16;
+    for (int i0 = 0; i0 < m; i0 += kInitWG * kTgtPer) {
+        float4 t[kTgtPer];
 #pragma unroll
-        for (int e = 0; e < kInitPer; ++e) t[e] = tgt[min(i0 + e * kInitWG + tid, m - 1)];
+        for (int e = 0; e < kTgtPer; ++e) t[e] = tgt[min(i0 + e * kInitWG + tid, m - 1)];
 #pragma unroll
-        for (int e = 0; e < kInitPer; ++e) bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
+        for (int e = 0; e < kTgtPer; ++e) bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
     }
     for (int i0 = 0; i0 < n; i0 += kInitWG * kInitPer) {
         float4 v[kInitPer];
@@ -804,13 +807,26 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     uint32_t* wsum = shu.mo.wsum;
     float* lo_s = shu.mo.lo_s;
     float* sc_s = shu.mo.sc_s;
+    // Large clouds (the scan-to-map target): every pass over the cloud keeps kMoPer points per thread
+    // in flight (a load-use loop had waited out one round trip per 512 points: 3 x 128 of them for a
+    // 65k-point map, ~140 us of a single registration)
+    constexpr int kMoPer = 8;
+    auto sweep = [&](auto&& f) {
+        for (int i0 = 0; i0 < n; i0 += kIdxWG * kMoPer) {
+            float4 v[kMoPer];
+#pragma unroll
+            for (int e = 0; e < kMoPer; ++e) v[e] = pts[min(i0 + e * kIdxWG + tid, n - 1)];
+#pragma unroll
+            for (int e = 0; e < kMoPer; ++e)
+                if (i0 + e * kIdxWG + tid < n) f(i0 + e * kIdxWG + tid, v[e]);
+        }
+    };
     // 1. bounding box
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts[i];
+    sweep([&](int, const float4& v) {
         mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
         mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
-    }
+    });
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
@@ -838,10 +854,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     __syncthreads();
     float lo[3] = {lo_s[0], lo_s[1], lo_s[2]}, sc[3] = {sc_s[0], sc_s[1], sc_s[2]};
     // 2. histogram of cell codes
-    for (int i = tid; i < n; i += kIdxWG) {
-        const float4 v = pts[i];
-        atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
-    }
+    sweep([&](int, const float4& v) { atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u); });
     __syncthreads();
     // 3. exclusive scan: thread t owns bins [16 t, 16 t + 16)
     constexpr int per = kCellBins / kIdxWG;
@@ -869,20 +882,18 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     if (is_tgt) {
         float4* ts = w.tsort + (int64_t)p * w.t_stride;
         int32_t* tinv = w.tinv + (int64_t)p * w.t_stride;
-        for (int i = tid; i < n; i += kIdxWG) {
-            const float4 v = pts[i];
+        sweep([&](int i, const float4& v) {
             const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
             ts[pos] = make_float4(v.x, v.y, v.z, __uint_as_float((uint32_t)i));
             tinv[i] = (int32_t)pos;
-        }
+        });
         index_boxes(w, p, n);
     } else {
         int32_t* sp = w.sperm + (int64_t)p * w.x_stride;
-        for (int i = tid; i < n; i += kIdxWG) {
-            const float4 v = pts[i];
+        sweep([&](int i, const float4& v) {
             const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
             sp[pos] = i;
-        }
+        });
     }
 }
 
@@ -1732,9 +1743,19 @@ __device__ void order_items(const PairArgs& a, const WorkArgs& w, int npairs, in
     if (tid < kOrderBuckets) sh.bcnt[tid] = 0;
     if (tid == 0) sh.tot = 0;
     __syncthreads();
-    auto work = [&](int p) -> int {
+    auto work_load = [&](int p) -> int {
         if (FUSED) return __hip_atomic_load(w.owork + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kMissCount;
         return !pass_wants(w.state[p].phase, fitness_pass) ? 0 : all ? a.src_n[p] : (w.miss_cnt[p] & kMissCount);
+    };
+    // the thread's first kOrderReg pairs' work loaded once, all in flight (the three passes below
+    // had each waited out their loads: one dependent round trip per pass)
+    constexpr int kOrderReg = 4;
+    int wreg[kOrderReg];
+#pragma unroll
+    for (int k = 0; k < kOrderReg; ++k) wreg[k] = tid + k * WG < npairs ? work_load(tid + k * WG) : 0;
+    auto work = [&](int p) -> int {
+        const int k = (p - tid) / WG;
+        return k < kOrderReg ? wreg[k] : work_load(p);
     };
     if (!all && w.part_size > 0) {  // the pass' total work, for the part size below
         unsigned long long t = 0;
@@ -3527,43 +3548,73 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
 constexpr int kSoloWG = kLdsWG;
 constexpr int kSoloFitChunk = 960;  // fitness chunk: 15 waves fill, wave 0 lane 0 folds
 constexpr int kSoloGrp = 4;         // the first pass' sorted positions in flight per thread
-// the test's LDS miss records (24 B each) in the tile's region, after the bitmap and its prefixes
-constexpr int kSoloRecs = ((int)(sizeof(v4f) * kLdsTargets + 4 * 6 * (kLdsTargets / kLdsLeaf) * 9 / 8) -
-                           8 * kNeedWords) / 24 & ~15;
-// LDS: the target tile (search) and the update's fold buffers (fold_update_kernel's 512-point
-// double buffer: a chunk's fold outlasts its fillers' L2 round trip) take turns in one region — the
-// tile is restaged from the L2 for each search (~128 KB of this XCD's L2 per iteration; smaller
-// chunks beside a resident tile left the fold chains waiting on their fillers); the search's
-// per-wave state has its own.
+// LDS.  ICP4R_SOLO_RESIDENT=1: the pair's target tile stays resident for the whole registration,
+// and the search's per-wave state, the update's fold buffers (192-point chunks), the test's bitmap
+// and records and the fitness chunks take turns in the 18 KB beside it.  0: the tile and the
+// update's 512-point fold buffers (fold_update_kernel's) take turns in one region, the tile
+// restaged from the L2 for each search.
+#ifndef ICP4R_SOLO_RESIDENT
+#define ICP4R_SOLO_RESIDENT 1
+#endif
+constexpr bool kSoloResident = ICP4R_SOLO_RESIDENT != 0;
+struct SoloTile {
+    v4f tl[kLdsTargets];
+    alignas(16) float bx[kLdsTargets / kLdsLeaf][6];
+    float sbx[kLdsTargets / kLdsLeaf / kSuper][6];
+};
+struct SoloSearch {  // the search's per-wave state
+    unsigned long long best[kLdsWaves][64];
+    uint32_t sec[kLdsWaves][64];
+    uint16_t items[kLdsWaves][kRing + 64];
+};
+constexpr int kSoloChunk = kSoloResident ? 192 : kFoldChunkP;  // fold chunk (points)
+constexpr int kSoloRow = kSoloChunk + kFoldPad;
+struct SoloFold {  // the update
+    alignas(16) float buf[2][9][kSoloRow];
+    float res[8];
+    int32_t cnt[kLdsWaves];
+    SolveShared sv;
+};
+// the test's LDS miss records (24 B each), after the bitmap and its prefixes, in the region they share
+constexpr int kSoloRecs = ((int)(kSoloResident ? sizeof(SoloSearch) : sizeof(SoloTile)) - 8 * kNeedWords) / 24 & ~15;
+struct SoloTest {  // the cached-neighbour test: the miss bitmap, its word prefixes, the miss records
+    uint32_t need[kNeedWords];
+    int32_t pre[kNeedWords];
+    float4 lv[kSoloRecs];
+    uint2 lm[kSoloRecs];
+};
+#if ICP4R_SOLO_RESIDENT
 struct SoloShared {
+    SoloTile t;
     union {
-        struct {  // the search
-            v4f tl[kLdsTargets];
-            alignas(16) float bx[kLdsTargets / kLdsLeaf][6];
-            float sbx[kLdsTargets / kLdsLeaf / kSuper][6];
-        } t;
-        struct {  // the update
-            alignas(16) float buf[2][9][kFoldRow];
-            float res[8];
-            int32_t cnt[kLdsWaves];
-            SolveShared sv;
-        } f;
+        SoloSearch s;
+        SoloFold f;
+        SoloTest c;
         alignas(16) float fit[2][kSoloFitChunk];  // the fitness sum's chunks
-        struct {  // the cached-neighbour test: the miss bitmap, its word prefixes, the miss records
-            uint32_t need[kNeedWords];
-            int32_t pre[kNeedWords];
-            float4 lv[kSoloRecs];
-            uint2 lm[kSoloRecs];
-        } c;
-    } a;
-    struct {  // the search's per-wave state
-        unsigned long long best[kLdsWaves][64];
-        uint32_t sec[kLdsWaves][64];
-        uint16_t items[kLdsWaves][kRing + 64];
-    } s;
+    } u;
     int32_t wtot[kLdsWaves];  // per-wave counts (the test's misses, the fitness count)
     int32_t mcount;           // the test's LDS record count
 };
+#define SOLO_T(sh) (sh).t
+#define SOLO_S(sh) (sh).u.s
+#else
+struct SoloShared {
+    union {
+        SoloTile t;
+        SoloFold f;
+        SoloTest c;
+        alignas(16) float fit[2][kSoloFitChunk];
+    } u;
+    SoloSearch s;
+    int32_t wtot[kLdsWaves];
+    int32_t mcount;
+};
+#define SOLO_T(sh) (sh).u.t
+#define SOLO_S(sh) (sh).s
+#endif
+#define SOLO_F(sh) (sh).u.f
+#define SOLO_C(sh) (sh).u.c
+#define SOLO_FIT(sh) (sh).u.fit
 static_assert(sizeof(SoloShared) <= 160 * 1024, "solo LDS");
 
 // The first pass' query list of the solo plan: every source in sorted-position order (thread t takes
@@ -3606,11 +3657,11 @@ __device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int 
                                SoloShared& sh) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nwords = (n + 31) >> 5;
-    for (int k = tid; k < nwords; k += kSoloWG) sh.a.c.need[k] = 0u;
+    for (int k = tid; k < nwords; k += kSoloWG) SOLO_C(sh).need[k] = 0u;
     if (tid == 0) sh.mcount = 0;
     __syncthreads();
-    const int tot = pair_cache_test<kSoloWG, 2, FROM_SRC>(a, w, p, n, T, sh.a.c.need, sh.a.c.pre, sh.a.c.lv,
-                                                         sh.a.c.lm, kSoloRecs, &sh.mcount, sh.wtot, FROM_SRC);
+    const int tot = pair_cache_test<kSoloWG, 2, FROM_SRC>(a, w, p, n, T, SOLO_C(sh).need, SOLO_C(sh).pre, SOLO_C(sh).lv,
+                                                         SOLO_C(sh).lm, kSoloRecs, &sh.mcount, sh.wtot, FROM_SRC);
     if (tot <= kSoloRecs) return tot;
     // overflow: every record is in sq / sm (test order), the bitmap still in LDS — word prefixes
     // (wave 0), then each record to its rank
@@ -3621,7 +3672,7 @@ __device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int 
 #pragma unroll
         for (int j = 0; j < kW; ++j) {
             const int wd = lane * kW + j;
-            c[j] = wd < nwords ? __builtin_popcount(sh.a.c.need[wd]) : 0;
+            c[j] = wd < nwords ? __builtin_popcount(SOLO_C(sh).need[wd]) : 0;
             sum += c[j];
         }
         int incl = sum;
@@ -3633,7 +3684,7 @@ __device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int 
         int run = incl - sum;
 #pragma unroll
         for (int j = 0; j < kW; ++j) {
-            sh.a.c.pre[lane * kW + j] = run;
+            SOLO_C(sh).pre[lane * kW + j] = run;
             run += c[j];
         }
     }
@@ -3643,7 +3694,7 @@ __device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int 
         const float4 r = w.sq[xs0 + k];
         const uint2 m = w.sm[xs0 + k];
         const uint32_t sp = min(m.y, (uint32_t)(n - 1));
-        const int rk = sh.a.c.pre[sp >> 5] + __builtin_popcount(sh.a.c.need[sp >> 5] & ((1u << (sp & 31)) - 1u));
+        const int rk = SOLO_C(sh).pre[sp >> 5] + __builtin_popcount(SOLO_C(sh).need[sp >> 5] & ((1u << (sp & 31)) - 1u));
         w.qv[xs0 + rk] = r;
         w.qm[xs0 + rk] = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
     }
@@ -3661,14 +3712,21 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
     const int64_t xs0 = (int64_t)p * w.x_stride;
     const bool valid = uload(&st.phase) != kPhaseInvalid;
     const int nsb = (((m + kLdsLeaf - 1) / kLdsLeaf) + kSuper - 1) / kSuper;
-    const LdsTile tile{sh.a.t.tl, sh.a.t.bx, sh.a.t.sbx};
+    const LdsTile tile{SOLO_T(sh).tl, SOLO_T(sh).bx, SOLO_T(sh).sbx};
     RunStats rs;
     auto search = [&](int nlist, bool keys) {
         __syncthreads();  // the list (global, this workgroup's) and the region's previous use
         v4f isl, ish;
-        stage_tile<kSoloWG>(tile, w, p, nsb, isl, ish);
-        __syncthreads();
-        lds_runs<true>(tile, sh.s.best[wave], sh.s.sec[wave], sh.s.items[wave], w.qv + xs0, w.qm + xs0, nlist, m, nsb,
+        if (kSoloResident) {
+            const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+            const int sbl = min(lane, nsb - 1);
+            isl = sbg[2 * sbl];
+            ish = sbg[2 * sbl + 1];
+        } else {
+            stage_tile<kSoloWG>(tile, w, p, nsb, isl, ish);
+            __syncthreads();
+        }
+        lds_runs<true>(tile, SOLO_S(sh).best[wave], SOLO_S(sh).sec[wave], SOLO_S(sh).items[wave], w.qv + xs0, w.qm + xs0, nlist, m, nsb,
                        isl, ish, a, w, p, xs0, w.X + xs0, w.nn_key + xs0, keys, false, rs);
         __syncthreads();
     };
@@ -3684,6 +3742,10 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         tk_last = now;
     };
     if (valid) {
+        if (kSoloResident) {
+            v4f isl, ish;
+            stage_tile<kSoloWG>(tile, w, p, nsb, isl, ish);  // (the search reloads its boxes)
+        }
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = 0.0f;
@@ -3699,17 +3761,17 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
             search(nlist, false);
             tick(2);
             const FoldIn fin{nullptr, w.X + xs0, w.nn_t + xs0, n};
-            fold_pass_a<kSoloWG, kFoldChunkP, kFoldRow>(kp, fin, sh.a.f.buf, sh.a.f.res, sh.a.f.cnt, sh.a.f.sv);
+            fold_pass_a<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, SOLO_F(sh).buf, SOLO_F(sh).res, SOLO_F(sh).cnt, SOLO_F(sh).sv);
             tick(3);
-            fold_pass_b<kSoloWG, kFoldChunkP, kFoldRow>(kp, fin, sh.a.f.buf, sh.a.f.sv);
+            fold_pass_b<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, SOLO_F(sh).buf, SOLO_F(sh).sv);
             tick(4);
-            if (tid == 0) solve_pair<kNumericsPCL>(sh.a.f.sv, st, kp);
+            if (tid == 0) solve_pair<kNumericsPCL>(SOLO_F(sh).sv, st, kp);
             __syncthreads();
             tick(5);
             if (tk) tk[9] += 1;
-            flag = sh.a.f.sv.flag;
+            flag = SOLO_F(sh).sv.flag;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) T[q] = sh.a.f.sv.T_inc[q];  // the next pass's deferred transform
+            for (int q = 0; q < 16; ++q) T[q] = SOLO_F(sh).sv.T_inc[q];  // the next pass's deferred transform
         }
         // the fitness pass (getFitnessScore after align) and align's output: final * input
         if (kp.compute_fitness || a.aligned) {
@@ -3756,7 +3818,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
             for (int o = tid - 64; o < len; o += kSoloWG - 64) {
                 const float d2 = key_d2(key[base + o]);
                 const bool in = (double)d2 <= kp.fit_max_range;
-                sh.a.fit[c & 1][o] = in ? d2 : 0.0f;
+                SOLO_FIT(sh)[c & 1][o] = in ? d2 : 0.0f;
                 fcnt += in ? 1 : 0;
             }
         };
@@ -3764,7 +3826,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
             if (wave == 0) {
-                if (lane == 0) fsum = fold_seq<double>(sh.a.fit[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
+                if (lane == 0) fsum = fold_seq<double>(SOLO_FIT(sh)[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
             } else if (c + 1 < nch) {
                 fill(c + 1);
             }
