@@ -329,7 +329,7 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
     iters = int(r.iterations)
     if plan["solo"]:
         return _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_ms, calls, nn_ms,
-                             nn_launches, st, plan, cpu_budget_s, fitness_passes, check)
+                             nn_launches, st, plan, cpu_budget_s, fitness_passes, check, sha)
     kernel = "nn_tile_kernel" if plan["pruned"] and not plan["lds"] else "nn_kernel"
     flops = evals * FLOP_PER_PAIR_EVAL + tests * FLOP_PER_BOX_TEST
     tflops = flops / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
@@ -381,7 +381,7 @@ def _check_and_cpu(ctx, out: dict, r, src, tgt, params, oparams: dict, cpu_budge
 
 
 def _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_ms, calls, solo_ms, solo_launches, st,
-                  plan, cpu_budget_s, fitness_passes, check) -> dict:
+                  plan, cpu_budget_s, fitness_passes, check, sha) -> dict:
     """The solo plan (solo_kernel: every ICP iteration and the fitness pass of the pair in one
     1024-thread workgroup, after init_kernel and index_kernel).  Its bound is latency: the
     registration is a dependent chain — per iteration the cached-neighbour test, the search of the
@@ -407,8 +407,13 @@ def _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_
                      "evaluations_per_registration": evals, "box_tests_per_registration": tests,
                      "evaluated_fraction_of_brute_force": evals / (n * m * (iters + 1))},
             "cache_hit_rate": st["cache_hits"] / st["cache_tested"] if st["cache_tested"] else None,
+            "traffic": None, "traffic_source": None, "library_sha256": sha,
             "note": "achieved / peak here = the fold-chain floor / the kernel's time (latency-bound: PCL's "
                     "sequential summation order); see DESIGN.md §5 solo_kernel"}
+    # HBM bytes of the launch (the whole registration) from the PMC passes of this build, beside its
+    # algorithmic floor: every source and target point read once (16 B each) and the result row
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(name, "solo_kernel", sha)
+    roof["algorithmic_bytes"] = 16 * (n + m) + 96
     out = {"workload": workload, "value": 1e3 / dev_ms if dev_ms > 0 else None, "unit": "pairs/s",
            "registration_device_ms": dev_ms, "registration_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
            "status": int(r.status), "iterations": iters, "plan": plan, "roofline": roof}

@@ -152,7 +152,12 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
             }
             // a PCL-numerics registration whose targets fit one LDS tile: the whole registration of
             // each pair in one workgroup (solo_kernel; ICP4R_SOLO=0: the multi-launch plan)
-            pl.solo = registration && pl.tile && pl.chunks == 1 && max_n <= kCacheMaxN && env_int("ICP4R_SOLO", 1) != 0;
+            // (up to kSoloMaxN sources: beyond, the one CU's test and search of the misses cost more than
+            // the multi-launch plan's boundaries — tools/solo_sweep.py, profiles/round3/solo_sweep.jsonl;
+            // ICP4R_SOLO=1 forces it up to kCacheMaxN, 0 disables it)
+            const int solo_env = env_int("ICP4R_SOLO", -1);
+            pl.solo = registration && pl.tile && pl.chunks == 1 && solo_env != 0 &&
+                      max_n <= (solo_env == 1 ? kCacheMaxN : kSoloMaxN);
             if (pl.solo) pl.blocks = npairs;
         }
         return pl;
@@ -434,6 +439,8 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     w.src_by_tgt = (pl.pruned && pl.lds) ? (env_int("ICP4R_SRC_ORDER", 1) != 0 ? 1 : 0)
                                          : (pl.pruned && env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0);
     w.stage_first = (w.src_by_tgt && (pl.lds || pl.solo) && w.qv && w.qm) ? 1 : 0;
+    // multi-tile plan (the scan-to-map target), PCL numerics: seeds written by the update's transform
+    w.seed_next = (pl.tile && pl.chunks > 1 && pcl && w.corr && env_int("ICP4R_FUSE_SEED", 1) != 0) ? 1 : 0;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));

@@ -115,6 +115,9 @@ struct WorkArgs {
                         // kd tree (src_order_kernel) instead of by its own tree: queries sorted by the
                         // target leaf they fall in, and that leaf seeds their first search
     int32_t stage_first;  // 1 (batched plan): src_order_kernel writes the first pass' query records
+    int32_t seed_next;    // 1 (multi-tile plan, PCL numerics): the update's transform and fitness_prep_kernel
+                          // write the next NN pass's seed keys (the previous NN at the moved point) from the
+                          // correspondence records, so no nn_seed_kernel launch
                           // (qv / qm, sorted order) itself; 0: the first pass' nn_key seeds
     uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,
                         // [8 + node] internal node (heap order) = 1 << 31 | mid << 13 | axis << 11 | key
@@ -185,6 +188,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
+constexpr int kSoloMaxN = 4096;           // solo_kernel by default for single pairs of at most this many sources
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
                          hipStream_t st, int tail_test = 0,
                          int order_ncu = 0);  // > 0: the launch also builds the next pass's work list

@@ -2758,15 +2758,28 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
 
 // transformCloud(*input_transformed, *input_transformed, transformation_) by the whole workgroup.
 // (With the cached-neighbour test the update defers this to the next pass's test kernel.)
+// seed (w.seed_next): the next NN pass's starting key too — the current NN (its coordinates from the
+// correspondence record, its index from the key) at the moved point, as nn_seed_kernel computes it.
 template <int WG>
-__device__ __forceinline__ void transform_pair(float4* X, int n, const float* T_lds) {
+__device__ __forceinline__ void transform_pair(const WorkArgs& w, int p, int n, const float* T_lds, bool seed) {
     float Tl[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) Tl[k] = T_lds[k];
+    const int64_t xs0 = (int64_t)p * w.x_stride;
+    float4* X = w.X + xs0;
+    NNKey* key = w.nn_key + xs0;
+    const float4* C = w.corr + xs0 * 2;
     for (int i = threadIdx.x; i < n; i += WG) {
         float4 s = X[i];
+        float4 t;
+        NNKey k0;
+        if (seed) {
+            t = C[2 * i + 1];
+            k0 = key[i];
+        }
         xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
         X[i] = s;
+        if (seed) key[i] = make_key(l2_simple(s.x, s.y, s.z, t.x, t.y, t.z), (uint32_t)key_idx(k0));
     }
 }
 
@@ -3312,7 +3325,7 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(3);
     if (sh.s.flag == 1) return 0;  // error: PCL breaks before transforming
-    if (!w.defer_xform) transform_pair<kFoldWG>(w.X + (int64_t)p * xs, n, sh.s.T_inc);
+    if (!w.defer_xform) transform_pair<kFoldWG>(w, p, n, sh.s.T_inc, w.seed_next && w.corr);
     // The next pass's cached-neighbour test, fused (tail_test: another iteration follows and the pair
     // is still active): the same work as nn_cache_test_kernel for this pair — the deferred
     // transformCloud(T_inc), the bounds moved, the test, hit keys, the miss bitmap — done here, where
@@ -3412,7 +3425,7 @@ __global__ __launch_bounds__(kUpdWG) void update_f64_kernel(PairArgs a, WorkArgs
     if (tid == 0) solve_pair<kNumericsF64>(sh, st, kp);
     __syncthreads();
     if (sh.flag == 1) return;
-    if (!w.defer_xform) transform_pair<kUpdWG>(X, n, sh.T_inc);
+    if (!w.defer_xform) transform_pair<kUpdWG>(w, p, n, sh.T_inc, false);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3448,10 +3461,18 @@ __global__ __launch_bounds__(kPrepWG) void fitness_prep_kernel(PairArgs a, WorkA
     const float4* src = a.src + a.src_off[p];
     float4* X = w.X + (int64_t)p * w.x_stride;
     float* uu = w.nn_u ? w.nn_u + (int64_t)p * w.x_stride : nullptr;
+    // (w.seed_next: the fitness pass's seed keys too — see transform_pair)
+    const bool seed = w.seed_next && w.corr && a.kp.compute_fitness;
+    NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
+    const float4* C = w.corr ? w.corr + (int64_t)p * w.x_stride * 2 : nullptr;
     for (int i = threadIdx.x; i < n; i += kPrepWG) {
         const float4 s = src[i];
         float4 o = s;
         xform_pt(Tf, s.x, s.y, s.z, o.x, o.y, o.z);
+        if (seed) {
+            const float4 t = C[2 * i + 1];
+            key[i] = make_key(l2_simple(o.x, o.y, o.z, t.x, t.y, t.z), (uint32_t)key_idx(key[i]));
+        }
         if (uu) {  // X still holds the last NN pass's points (a deferred transform never ran), .w = L
             const float4 old = X[i];
             const float2 Lm = move_lu(make_float2(old.w, uu[i]), old.x, old.y, old.z, o.x, o.y, o.z);
@@ -3654,14 +3675,20 @@ __device__ int solo_first_list(const PairArgs& a, const WorkArgs& w, int p, int 
 // converged), the records left in sq / sm are placed at their ranks here.  Returns the list length.
 template <bool FROM_SRC>
 __device__ int solo_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
-                               SoloShared& sh) {
+                               SoloShared& sh, unsigned long long* tk = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nwords = (n + 31) >> 5;
+    const uint64_t t0 = tk ? __builtin_amdgcn_s_memrealtime() : 0;
     for (int k = tid; k < nwords; k += kSoloWG) SOLO_C(sh).need[k] = 0u;
     if (tid == 0) sh.mcount = 0;
     __syncthreads();
     const int tot = pair_cache_test<kSoloWG, 2, FROM_SRC>(a, w, p, n, T, SOLO_C(sh).need, SOLO_C(sh).pre, SOLO_C(sh).lv,
                                                          SOLO_C(sh).lm, kSoloRecs, &sh.mcount, sh.wtot, FROM_SRC);
+    if (tk) {  // debug: the test's own wall, and how many passes overflowed the LDS records
+        tk[27] += __builtin_amdgcn_s_memrealtime() - t0;
+        tk[28] += tot > kSoloRecs ? 1 : 0;
+        tk[29] += tot;
+    }
     if (tot <= kSoloRecs) return tot;
     // overflow: every record is in sq / sm (test order), the bitmap still in LDS — word prefixes
     // (wave 0), then each record to its rank
@@ -3755,7 +3782,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         for (int it = 0; it < iters && flag == 0; ++it) {
             // (first pass: src_order_kernel wrote the records, seeded at the source's kd leaf in the
             // target's tree, when the sources are ordered by it — ICP4R_SRC_ORDER=1)
-            const int nlist = it > 0 ? solo_cache_test<false>(a, w, p, n, T, sh)
+            const int nlist = it > 0 ? solo_cache_test<false>(a, w, p, n, T, sh, tk)
                               : (w.stage_first && src_by_tgt_tree(a, w, p)) ? n : solo_first_list(a, w, p, n, m);
             tick(1);
             search(nlist, false);
@@ -3958,7 +3985,8 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
     // three-launch form, for A/B)
     static const int own_env = getenv("ICP4R_TILE_OWN") ? atoi(getenv("ICP4R_TILE_OWN")) : 1;
     const bool own = grid.x == 1 && own_env != 0;
-    if (!own)
+    // (w.seed_next: the previous update / fitness_prep_kernel wrote the seeds, except for the first pass)
+    if (!own && (first || !w.seed_next))
         hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass,
                            first);
     if (tile_start && (e = hipEventRecord(tile_start, st)) != hipSuccess) return e;

@@ -26,6 +26,7 @@ def main():
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
     fixed = dict(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    os.environ.setdefault("ICP4R_SOLO", "1")  # (C2's 8192 sources are past the default solo size)
     for name, pair, params in (("C1", synth.make_pair(0, 2048), icp4r.default_params()),
                                ("C2", synth.make_pair(1, 8192), icp4r.default_params(**fixed))):
         ctx = icp4r.Context(0)
@@ -33,8 +34,8 @@ def main():
         ctx.align(s, t, params)  # warm-up (allocates the tick slots)
 
         def ticks():
-            buf = (C.c_uint64 * 16)()
-            if lib.icp4r__debug_ticks(ctx._h, buf, 16) != 0:
+            buf = (C.c_uint64 * 32)()
+            if lib.icp4r__debug_ticks(ctx._h, buf, 32) != 0:
                 raise RuntimeError(icp4r.load().icp4r_last_error())
             return np.array(list(buf), np.float64)
 
@@ -46,7 +47,9 @@ def main():
         it = max(d[9], 1)
         out = {"config": name, "iterations": int(r.iterations), "solo_kernel_ms": ms,
                "phases_us": {k: d[i] / 100.0 for i, k in enumerate(NAMES)},
-               "per_iteration_us": {k: d[i] / 100.0 / it for i, k in enumerate(NAMES[1:6], 1)}}
+               "per_iteration_us": {k: d[i] / 100.0 / it for i, k in enumerate(NAMES[1:6], 1)},
+               "test_core_us_per_pass": d[27] / 100.0 / max(it - 1, 1), "test_overflow_passes": int(d[28]),
+               "misses_per_pass": d[29] / max(it - 1, 1)}
         print(json.dumps(out), flush=True)
         ctx.close()
 
