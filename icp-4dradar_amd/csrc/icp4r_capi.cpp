@@ -345,12 +345,21 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
     w.pass_ticks = (w0.ticks && pass >= 0 && pass < kMaxTickPasses)
                        ? w0.ticks + pass_tick_base(npairs) + (int64_t)pass * kPassTickSlots
                        : nullptr;
-    if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
+    // per-kernel events only when asked for (icp4r_set_kernel_timing: each record between two kernels
+    // costs device time); the batch events around a registration are always recorded
+    const bool kev = ctx->kernel_timing;
+    EventPair none;
+    none.start = none.stop = nullptr;
+    if (kev) {
+        if ((r = next_event(ctx->nn_events, ctx->nn_used, &ne))) return r;
+    } else {
+        ne = &none;
+    }
     if (pl.lds) {
         NNLdsEvents ev;
         ev.search_start = ne->start;
         ev.search_stop = ne->stop;
-        if (pl.cache && !first && !test_fused) {
+        if (kev && pl.cache && !first && !test_fused) {
             EventPair* te;
             if ((r = next_event(ctx->test_events, ctx->test_used, &te))) return r;
             ev.test_start = te->start;
@@ -364,14 +373,14 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
         HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, st, ne->start, ne->stop));
         return ICP4R_OK;
     }
-    HIP_TRY(hipEventRecord(ne->start, st));
+    if (kev) HIP_TRY(hipEventRecord(ne->start, st));
     if (pl.pruned) {
         HIP_TRY(launch_nn_pruned(pl.q, pl.chunk_sb, pl.chunks, a, w, npairs, max_n, fitness_pass, first, st));
     } else {
         if (pl.splits > 1) HIP_TRY(hipMemsetAsync(w.nn_key, 0xFF, (size_t)npairs * w.x_stride * sizeof(NNKey), st));
         HIP_TRY(launch_nn(pl.q, pl.packed, a, w, npairs, max_n, fitness_pass, st));
     }
-    HIP_TRY(hipEventRecord(ne->stop, st));
+    if (kev) HIP_TRY(hipEventRecord(ne->stop, st));
     return ICP4R_OK;
 }
 
@@ -447,11 +456,14 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     if (pl.solo) {  // init, the two kd builds, then every iteration and the fitness pass in one launch
         HIP_TRY(launch_init(a, w, npairs, st));
         HIP_TRY(launch_index(a, w, npairs, st));
-        EventPair* ne;
-        if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
-        HIP_TRY(hipEventRecord(ne->start, st));
+        const bool kev = ctx->kernel_timing;
+        EventPair* ne = nullptr;
+        if (kev) {
+            if ((rc = next_event(ctx->nn_events, ctx->nn_used, &ne))) return rc;
+            HIP_TRY(hipEventRecord(ne->start, st));
+        }
         HIP_TRY(launch_solo(a, w, npairs, max_n, max_iterations > 0 ? max_iterations : 1, st));
-        HIP_TRY(hipEventRecord(ne->stop, st));
+        if (kev) HIP_TRY(hipEventRecord(ne->stop, st));
         HIP_TRY(hipEventRecord(be->stop, st));
         return ICP4R_OK;
     }
@@ -492,18 +504,21 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // ... and the work list of those passes is built by the update's last workgroup (ICP4R_FUSE_ORDER=0:
     // nn_order_kernel)
     const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
+    const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
     for (int it = 0; it < iters; ++it) {
         for (int g = 0; g < groups; ++g) {
             const int ncu_g = search_cu > 0 ? search_cu : ctx->ncu;
             if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0, it,
                               ford && it > 0)))
                 return rc;
-            EventPair* ue;
-            if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
-            HIP_TRY(hipEventRecord(ue->start, gs[g]));
+            EventPair* ue = nullptr;
+            if (kev) {
+                if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
+                HIP_TRY(hipEventRecord(ue->start, gs[g]));
+            }
             HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g], fuse && it + 1 < iters,
                                   ford && it + 1 < iters ? ncu_g : 0));
-            HIP_TRY(hipEventRecord(ue->stop, gs[g]));
+            if (kev) HIP_TRY(hipEventRecord(ue->stop, gs[g]));
         }
     }
     for (int g = 0; g < groups; ++g) {
@@ -631,6 +646,7 @@ int icp4r_create(icp4r_ctx** out, int device) {
     c->device = device;
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
+    c->kernel_timing = env_int("ICP4R_KERNEL_EVENTS", 0) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -918,6 +934,12 @@ int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* 
     int rc = events_avg(*v, used, avg_ms);
     if (launches) *launches = (int32_t)used;
     return rc;
+}
+
+int icp4r_set_kernel_timing(icp4r_ctx* ctx, int32_t enable) {
+    if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
+    ctx->kernel_timing = enable != 0;
+    return ICP4R_OK;
 }
 
 int icp4r_kernel_time_reset(icp4r_ctx* ctx) {

@@ -107,11 +107,13 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     HIP_TRY(hipEventRecord(be->start, st));
     HIP_TRY(launch_init(a, w, npairs, st));
     HIP_TRY(launch_gicp_init(a.guess, g.gs, npairs, st));
-    EventPair* ce;
-    if ((rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
+    // per-stage events only with icp4r_set_kernel_timing (each record between kernels costs device time)
+    const bool kev = ctx->kernel_timing;
+    EventPair* ce = nullptr;
+    if (kev && (rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
     double* cs = static_cast<double*>(ctx->gicp_cov_src.p);
     double* ct = static_cast<double*>(ctx->gicp_cov_tgt.p);
-    HIP_TRY(hipEventRecord(ce->start, st));
+    if (kev) HIP_TRY(hipEventRecord(ce->start, st));
     // source covariances first: the target's index (built last) stays for the NN passes
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
                        st)))
@@ -120,15 +122,17 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
                        st)))
         return rc;
     if (pl.pruned && icp4r_pipe::env_int("ICP4R_GICP_COV_BRUTE", 0)) HIP_TRY(launch_index(a, w, npairs, st));
-    HIP_TRY(hipEventRecord(ce->stop, st));
+    if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
     for (int it = 0; it < gp.max_iterations; ++it) {
         if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
-        EventPair* ue;
-        if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
-        HIP_TRY(hipEventRecord(ue->start, st));
+        EventPair* ue = nullptr;
+        if (kev) {
+            if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
+            HIP_TRY(hipEventRecord(ue->start, st));
+        }
         HIP_TRY(launch_gicp_iter(a, w, g, npairs, it, st));
-        HIP_TRY(hipEventRecord(ue->stop, st));
+        if (kev) HIP_TRY(hipEventRecord(ue->stop, st));
         if ((it + 1) % kActiveCheck == 0 && it + 1 < gp.max_iterations) {
             int32_t h = 0;
             HIP_TRY(launch_gicp_active(w.state, npairs, active, st));

@@ -2769,17 +2769,29 @@ __device__ __forceinline__ void transform_pair(const WorkArgs& w, int p, int n, 
     float4* X = w.X + xs0;
     NNKey* key = w.nn_key + xs0;
     const float4* C = w.corr + xs0 * 2;
-    for (int i = threadIdx.x; i < n; i += WG) {
-        float4 s = X[i];
-        float4 t;
-        NNKey k0;
-        if (seed) {
-            t = C[2 * i + 1];
-            k0 = key[i];
+    // kPer points per thread with every load in flight before the first store (a load issued after a
+    // store waits behind it on vmcnt: one L2 round trip per point otherwise)
+    constexpr int kPer = 4;
+    for (int i0 = 0; i0 < n; i0 += WG * kPer) {
+        float4 s[kPer], t[kPer];
+        NNKey k0[kPer];
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const int i = min(i0 + e * WG + (int)threadIdx.x, n - 1);
+            s[e] = X[i];
+            if (seed) {
+                t[e] = C[2 * i + 1];
+                k0[e] = key[i];
+            }
         }
-        xform_pt(Tl, s.x, s.y, s.z, s.x, s.y, s.z);
-        X[i] = s;
-        if (seed) key[i] = make_key(l2_simple(s.x, s.y, s.z, t.x, t.y, t.z), (uint32_t)key_idx(k0));
+#pragma unroll
+        for (int e = 0; e < kPer; ++e) {
+            const int i = i0 + e * WG + (int)threadIdx.x;
+            if (i >= n) break;
+            xform_pt(Tl, s[e].x, s[e].y, s[e].z, s[e].x, s[e].y, s[e].z);
+            X[i] = s[e];
+            if (seed) key[i] = make_key(l2_simple(s[e].x, s[e].y, s[e].z, t[e].x, t[e].y, t[e].z), (uint32_t)key_idx(k0[e]));
+        }
     }
 }
 

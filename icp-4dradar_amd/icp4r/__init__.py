@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "icp4r_version", "icp4r_abi_version", "icp4r_last_error", "icp4r_params_default", "icp4r_device_count",
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
-    "icp4r_kernel_time_reset", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits", "icp4r_stage_time_ms",
+    "icp4r_kernel_time_reset", "icp4r_set_kernel_timing", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits", "icp4r_stage_time_ms",
     "icp4r_nn_stats",
 ]
 # include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
@@ -171,6 +171,7 @@ def load():
         "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "icp4r_nn_cache_hits": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "icp4r_stage_time_ms": (C.c_int, [vp, i32, C.POINTER(C.c_double), C.POINTER(i32)]),
+        "icp4r_set_kernel_timing": (C.c_int, [vp, i32]),
         "icp4r_nn_stats": (C.c_int, [vp, C.POINTER(C.c_uint64 * 8)]),
         # icp4r_map.h
         "icp4r_map_create": (C.c_int, [vp, C.POINTER(vp)]),
@@ -322,6 +323,11 @@ class Context:
         ms, k = C.c_double(), C.c_int32()
         _check(self._lib.icp4r_batch_time_ms(self._h, C.byref(ms), C.byref(k)), "icp4r_batch_time_ms")
         return ms.value, k.value
+
+    def set_kernel_timing(self, on: bool = True):
+        """Per-kernel events for kernel_time_ms / stage_time_ms (off by default: they cost device time
+        between kernels; batch_time_ms is always available)."""
+        _check(self._lib.icp4r_set_kernel_timing(self._h, 1 if on else 0), "icp4r_set_kernel_timing")
 
     def stage_time_ms(self, stage: int) -> tuple[float, int]:
         """(average ms, launches) of a stage (STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH)."""

@@ -167,6 +167,12 @@ int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream);
 int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
 int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);
 int icp4r_kernel_time_reset(icp4r_ctx* ctx);
+/* Per-kernel timing (the events behind icp4r_kernel_time_ms / icp4r_stage_time_ms for NN, NN_TEST and
+ * UPDATE): off by default — each event record between two kernels costs device time (an 8k pair's
+ * registration 1.89 ms without them, 2.19 ms with them; a 1024-pair batch 7.01 vs 7.31 ms).  The
+ * whole-call events (icp4r_batch_time_ms) are always recorded.  The environment variable
+ * ICP4R_KERNEL_EVENTS=1 turns it on for contexts created afterwards. */
+int icp4r_set_kernel_timing(icp4r_ctx* ctx, int32_t enable);
 
 /* Average device time of one stage of the registrations since the last reset (HIP events on the
  * launch stream), and how many launches it averages.  ICP4R_STAGE_NN is what icp4r_kernel_time_ms

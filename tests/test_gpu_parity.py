@@ -444,11 +444,19 @@ def test_kernel_timing_api(gpu_ctx, solo, monkeypatch):
     import icp4r
 
     monkeypatch.setenv("ICP4R_SOLO", solo)
-    gpu_ctx.reset_timers()
     s, t = _pair(700, 2048)
-    gpu_ctx.align(s, t, icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1))
-    ms, k = gpu_ctx.kernel_time_ms()
-    bms, bk = gpu_ctx.batch_time_ms()
+    p = icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1)
+    gpu_ctx.reset_timers()  # per-kernel timing off (the default): only the whole call is timed
+    gpu_ctx.align(s, t, p)
+    assert gpu_ctx.kernel_time_ms()[1] == 0 and gpu_ctx.batch_time_ms()[1] == 1
+    gpu_ctx.set_kernel_timing(True)
+    try:
+        gpu_ctx.reset_timers()
+        gpu_ctx.align(s, t, p)
+        ms, k = gpu_ctx.kernel_time_ms()
+        bms, bk = gpu_ctx.batch_time_ms()
+    finally:
+        gpu_ctx.set_kernel_timing(False)
     assert k == (1 if solo == "1" else 6) and ms > 0 and bk == 1 and bms >= ms
 
 

@@ -29,6 +29,7 @@ from icp4r import synth  # noqa: E402
 
 def run(name, src, tgt, params, oparams, reps=5):
     ctx = icp4r.Context(0)
+    ctx.set_kernel_timing(True)  # (this tool reports per-kernel times)
     r, _ = ctx.align(src, tgt, params)  # warm-up
     ctx.reset_timers()
     walls = []
