@@ -303,8 +303,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.qm = static_cast<uint2*>(ctx->qm.p);
             w.plist_n = static_cast<int32_t*>(ctx->plist_n.p);
             w.queue = w.plist_n + 1;
-            // (plist_n[3] of every group: the fused order's arrival counter, from zero per registration)
-            HIP_TRY(hipMemsetAsync(w.plist_n, 0, 4 * kMaxGroups * sizeof(int32_t), st));
+            // (plist_n[3] of every group: the fused order's arrival counter, zeroed per registration by
+            // init_kernel)
             HIP_TRY(ctx->owork.ensure((size_t)npairs * sizeof(int32_t)));
             w.owork = static_cast<int32_t*>(ctx->owork.p);
         }
@@ -327,9 +327,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
             w.part_size = env_int("ICP4R_PART", kDefaultPartSize);
             if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
-            // the search clears what it consumed; a fresh registration starts from zero anyway
-            HIP_TRY(hipMemsetAsync(w.need, 0, (size_t)npairs * w.need_stride * sizeof(uint32_t), st));
-            HIP_TRY(hipMemsetAsync(w.miss_cnt, 0, (size_t)npairs * sizeof(int32_t), st));
+            // (a fresh registration starts from zero: init_kernel clears the pair's bitmap and count —
+            // three memset launches per batch, and their boundaries, fewer)
         }
     }
     return ICP4R_OK;

@@ -226,6 +226,15 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
             if (i < nc) X[i] = o;
         }
     }
+    // the pass-scoped state this registration starts from: the pair's miss bitmap and count (cached-
+    // neighbour plans) and, by the group's first pair, its work-list counters (plist_n[0..3]: items,
+    // queue, part size, the fused order's arrival counter)
+    if (w.need) {
+        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+        for (int k = tid; k < w.need_stride; k += kInitWG) gneed[k] = 0u;
+    }
+    if (tid == 0 && w.miss_cnt) w.miss_cnt[p] = 0;
+    if (tid < 4 && p == 0 && w.plist_n) w.plist_n[tid] = 0;
     bad = __syncthreads_or(bad);
     if (tid == 0) {
         mat4_identity(st.T_inc);
@@ -332,10 +341,6 @@ typedef uint32_t kd_flag_t;
 #else
 typedef uint8_t kd_flag_t;
 #endif
-#ifndef ICP4R_IDX_TOUCH
-#define ICP4R_IDX_TOUCH 1  // index_kernel: the cloud's lines touched (coalesced) before the sorted gather
-#endif
-
 struct KdShared {
     uint16_t L[3][kKdMaxN];  // per axis: the point indices, sorted by that axis inside every segment
     union {
@@ -726,18 +731,6 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
             // a load-use loop had waited out one global round trip per position.  (t_stride is a
             // multiple of 64, so the position guard is wave-uniform: the shuffles below see every lane.)
             constexpr int kG = kKdPer / 2;  // two rounds of 8 (16 in flight spilled registers)
-#if ICP4R_IDX_TOUCH
-            // Every 128-B line of the cloud touched first (one dword each, coalesced): the gather below
-            // reads it in sorted order, 16 B per line visit, and the ~100 us of levels since the
-            // bounding-box read let the other builds on this XCD (two per CU, 8 MB of clouds against a
-            // 4-MB L2) evict it — each scattered 16-B load then refetched its whole line.
-            {
-                const uint32_t* pw = reinterpret_cast<const uint32_t*>(pts);
-                uint32_t acc = 0;
-                for (int l = tid; l < (n * 16 + 127) / 128; l += kIdxWG) acc ^= pw[l * 32];
-                asm volatile("" ::"v"(acc));
-            }
-#endif
 #pragma unroll
             for (int k0 = 0; k0 < kKdPer; k0 += kG) {
             float cx[kG], cy[kG], cz[kG];
@@ -1489,6 +1482,10 @@ __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float 
     return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
 }
 
+#ifndef ICP4R_PREFETCH_NEXT
+#define ICP4R_PREFETCH_NEXT 0  // nn_lds_kernel: claim the next item early and pull its targets into the L2
+#endif
+
 #ifndef ICP4R_SKIP_SEED
 #define ICP4R_SKIP_SEED 1  // the lane's seed block (evaluated whole up front) is never queued again
 #endif
@@ -1515,6 +1512,7 @@ struct LdsNN {
     uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query lane << 9) | block; + a spare slot per lane
     int32_t wsum[kLdsWaves];                           // staging: bitmap popcounts per wave
     int32_t cur;                                       // the pair this workgroup works on
+    int32_t nxt;                                       // ICP4R_PREFETCH_NEXT: the next item, claimed early
 };
 
 // LDS slot of sorted target position p: the slot inside its 16-target block XOR the block's low
@@ -2188,12 +2186,14 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     // keys: without the cached-neighbour state the next search's seed and the records read them
     const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
+    if (ICP4R_PREFETCH_NEXT && tid == 0) sh.nxt = -1;
     // work counters; debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1:
     // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
     // tools/nn_events.py): wave-uniform adds, stored once at the end
     RunStats rs;
     for (;;) {
-        if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
+        // (ICP4R_PREFETCH_NEXT: the item claimed during the previous one, if any)
+        if (tid == 0) sh.cur = (ICP4R_PREFETCH_NEXT && sh.nxt >= 0) ? sh.nxt : atomicAdd(w.queue, 1);
         __syncthreads();
         const int idx = sh.cur;
         if (idx >= npl) break;  // uniform: every wave read the same sh.cur
@@ -2332,9 +2332,23 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // (8 per thread, ~10-20 us per item under load).
         const LdsTile tv{sh.tl, sh.bx, sh.sbx};
         v4f isl, ish;
+        // ICP4R_PREFETCH_NEXT: while the queue is long (a full grid of items beyond this one), the next
+        // item is claimed now and its targets and boxes are pulled into the L2 (one dword per 128-B line)
+        // during this item's runs, so its staging reads the L2 instead of waiting on HBM behind the
+        // other group's update
+        if (ICP4R_PREFETCH_NEXT && tid == 0) sh.nxt = (idx + (int)gridDim.x < npl) ? atomicAdd(w.queue, 1) : -1;
         stage_tile<kLdsWG>(tv, w, p, nsb, isl, ish);
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
+        if (ICP4R_PREFETCH_NEXT && sh.nxt >= 0 && sh.nxt < npl) {
+            const int p2 = w.plist[sh.nxt] >> kPartBits;
+            const uint32_t* tw = reinterpret_cast<const uint32_t*>(w.tsort + (int64_t)p2 * w.t_stride);
+            const uint32_t* bw = reinterpret_cast<const uint32_t*>(w.tbox + (int64_t)p2 * 2 * w.b_stride);
+            const int tl = (int)(w.t_stride * 16 / 128), bl = (int)(w.b_stride * 32 / 128);
+            uint32_t acc = 0;
+            for (int l = tid; l < tl + bl; l += kLdsWG) acc ^= l < tl ? tw[l * 32] : bw[(l - tl) * 32];
+            asm volatile("" ::"v"(acc));
+        }
         unsigned long long* bestl = sh.r.best[wave];
         uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
