@@ -1482,10 +1482,6 @@ __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float 
     return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
 }
 
-#ifndef ICP4R_PREFETCH_NEXT
-#define ICP4R_PREFETCH_NEXT 0  // nn_lds_kernel: claim the next item early and pull its targets into the L2
-#endif
-
 #ifndef ICP4R_SKIP_SEED
 #define ICP4R_SKIP_SEED 1  // the lane's seed block (evaluated whole up front) is never queued again
 #endif
@@ -1512,7 +1508,6 @@ struct LdsNN {
     uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query lane << 9) | block; + a spare slot per lane
     int32_t wsum[kLdsWaves];                           // staging: bitmap popcounts per wave
     int32_t cur;                                       // the pair this workgroup works on
-    int32_t nxt;                                       // ICP4R_PREFETCH_NEXT: the next item, claimed early
 };
 
 // LDS slot of sorted target position p: the slot inside its 16-target block XOR the block's low
@@ -2186,14 +2181,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     // keys: without the cached-neighbour state the next search's seed and the records read them
     const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
-    if (ICP4R_PREFETCH_NEXT && tid == 0) sh.nxt = -1;
     // work counters; debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1:
     // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
     // tools/nn_events.py): wave-uniform adds, stored once at the end
     RunStats rs;
     for (;;) {
-        // (ICP4R_PREFETCH_NEXT: the item claimed during the previous one, if any)
-        if (tid == 0) sh.cur = (ICP4R_PREFETCH_NEXT && sh.nxt >= 0) ? sh.nxt : atomicAdd(w.queue, 1);
+        if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
         const int idx = sh.cur;
         if (idx >= npl) break;  // uniform: every wave read the same sh.cur
@@ -2332,23 +2325,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // (8 per thread, ~10-20 us per item under load).
         const LdsTile tv{sh.tl, sh.bx, sh.sbx};
         v4f isl, ish;
-        // ICP4R_PREFETCH_NEXT: while the queue is long (a full grid of items beyond this one), the next
-        // item is claimed now and its targets and boxes are pulled into the L2 (one dword per 128-B line)
-        // during this item's runs, so its staging reads the L2 instead of waiting on HBM behind the
-        // other group's update
-        if (ICP4R_PREFETCH_NEXT && tid == 0) sh.nxt = (idx + (int)gridDim.x < npl) ? atomicAdd(w.queue, 1) : -1;
         stage_tile<kLdsWG>(tv, w, p, nsb, isl, ish);
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
-        if (ICP4R_PREFETCH_NEXT && sh.nxt >= 0 && sh.nxt < npl) {
-            const int p2 = w.plist[sh.nxt] >> kPartBits;
-            const uint32_t* tw = reinterpret_cast<const uint32_t*>(w.tsort + (int64_t)p2 * w.t_stride);
-            const uint32_t* bw = reinterpret_cast<const uint32_t*>(w.tbox + (int64_t)p2 * 2 * w.b_stride);
-            const int tl = (int)(w.t_stride * 16 / 128), bl = (int)(w.b_stride * 32 / 128);
-            uint32_t acc = 0;
-            for (int l = tid; l < tl + bl; l += kLdsWG) acc ^= l < tl ? tw[l * 32] : bw[(l - tl) * 32];
-            asm volatile("" ::"v"(acc));
-        }
         unsigned long long* bestl = sh.r.best[wave];
         uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
