@@ -346,7 +346,7 @@ struct KdShared {
     union {
         uint32_t hist[3][kKdBins];  // the per-axis counting sorts
         struct {
-            kd_flag_t left[kKdMaxN];   // per point: left of its segment's split
+            kd_flag_t left[kKdMaxN + 4];  // per point: left of its segment's split (+ a junk slot)
             uint16_t tpre[3][kIdxWG];  // per list: exclusive prefix of "left" at each thread's first position
         } p;
         float4 bbox[2 * kKdMaxN / 16];  // index_kernel: block boxes (lo, hi) for the superblock boxes
@@ -526,6 +526,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             if (h) {
                 // the segment's extent per axis from the keys of its first and last point in that axis'
                 // list, re-quantised from the (cache-resident) cloud: no per-point key array in LDS
+                // (keeping the small clouds' bins in LDS instead was measured: no faster)
                 float ext[3];
                 float4 pf[3], pl[3];
 #pragma unroll
@@ -556,38 +557,64 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             mid = sh.seg_mid[s / kKdPer];
             ax = sh.seg_ax[s / kKdPer];
         }
-        // this thread's list entries (one 16-B LDS read per list; entries >= n are never used)
-        uint32_t v[3][kKdPer];  // (32-bit elements: a u16 array went to scratch)
+        // this thread's list entries (one 16-B LDS read per list; entries >= n are never used), two
+        // u16 entries per register as read (a u16 array went to scratch, 32-bit elements filled the
+        // register budget: a spill in every level)
+        uint32_t vp[3][kKdPer / 2];
         static_assert(kKdPer % 8 == 0, "whole 16-B reads of the lists");
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
             for (int q8 = 0; q8 < kKdPer / 8; ++q8) {
                 const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[a][p0 + 8 * q8]);
-                const uint32_t w4[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    v[a][8 * q8 + 2 * k] = w4[k] & 0xffffu;
-                    v[a][8 * q8 + 2 * k + 1] = w4[k] >> 16;
-                }
+                vp[a][4 * q8] = r.x;
+                vp[a][4 * q8 + 1] = r.y;
+                vp[a][4 * q8 + 2] = r.z;
+                vp[a][4 * q8 + 3] = r.w;
             }
+        auto ent = [&](int a, int k) -> uint32_t { return (vp[a][k >> 1] >> (16 * (k & 1))) & 0xffffu; };
         const int nv = min(kKdPer, n - p0);  // valid entries (<= 0: none)
-        if (ax < 3)  // "left" per point, from the split axis' list
+        const bool act = nv > 0 && ax < 3;    // this thread's segment splits
+        // Every LDS access of the level below is unconditional: a per-entry guard had put a branch and
+        // a wait around each (~6 us per level on a single 2k-point build).  Entries past nv (the thread
+        // holding position n - 1) may hold anything: their flag goes to the junk slot, their flag reads
+        // are masked into range and dropped, and their partition writes land in [n, p0 + kKdPer).
+        if (act) {  // "left" per point, from the split axis' list
+            uint32_t va[kKdPer / 2];  // the split axis' entries, re-read from LDS (a select among the
+                                      // registers became a dynamic index: a round trip through scratch)
 #pragma unroll
-            for (int k = 0; k < kKdPer; ++k)
-                if (k < nv) sh.u.p.left[ax == 0 ? v[0][k] : (ax == 1 ? v[1][k] : v[2][k])] = p0 + k < mid;  // (no dynamic register index: scratch)
+            for (int q8 = 0; q8 < kKdPer / 8; ++q8) {
+                const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[ax][p0 + 8 * q8]);
+                va[4 * q8] = r.x;
+                va[4 * q8 + 1] = r.y;
+                va[4 * q8 + 2] = r.z;
+                va[4 * q8 + 3] = r.w;
+            }
+            const uint32_t lf = p0 < mid ? 1u : 0u;  // (segment bounds and mid are multiples of kKdPer)
+#pragma unroll
+            for (int k = 0; k < kKdPer; ++k) {
+                const uint32_t i = (va[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                sh.u.p.left[k < nv ? i : kKdMaxN] = (kd_flag_t)lf;
+            }
+        }
         __syncthreads();
-        // stable partition of the three lists: exclusive prefix of "left" in list order; the flags
-        // of this thread's entries as bit masks (the split axis' own need no gather)
+        // stable partition of the three lists: exclusive prefix of "left" in list order; the flags of
+        // this thread's entries as bit masks (the split axis' own read back what this thread wrote)
         uint32_t fb[3] = {0u, 0u, 0u};
-        if (ax < 3)
+        if (act) {
+            uint32_t fl[3][kKdPer];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #pragma unroll
-                for (int k = 0; k < kKdPer; ++k) {
-                    const uint32_t f = k >= nv ? 0u : (a == ax ? (uint32_t)(p0 + k < mid) : (uint32_t)sh.u.p.left[v[a][k]]);
-                    fb[a] |= f << k;
-                }
+                for (int k = 0; k < kKdPer; ++k) fl[a][k] = sh.u.p.left[ent(a, k) & (kKdMaxN - 1)];
+            const uint32_t vm = nv >= 32 ? ~0u : (1u << nv) - 1u;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                for (int k = 0; k < kKdPer; ++k) fb[a] |= fl[a][k] << k;
+                fb[a] &= vm;
+            }
+        }
         const int cnt[3] = {__builtin_popcount(fb[0]), __builtin_popcount(fb[1]), __builtin_popcount(fb[2])};
         int incl[3] = {cnt[0], cnt[1], cnt[2]};
         for (int off = 1; off < 64; off <<= 1)
@@ -603,7 +630,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         for (int a = 0; a < 3; ++a) sh.u.p.tpre[a][tid] = (uint16_t)(incl[a] - cnt[a]);  // in-wave exclusive
         __syncthreads();  // wave totals and in-wave prefixes visible; every thread holds its entries in v
         const int sw = (s / kKdPer) >> 6;  // the wave owning the segment's first position
-        if (nv > 0 && ax < 3) {
+        if (act) {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
                 if (a == ax) continue;  // already partitioned: every entry stays where it is
@@ -629,7 +656,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
                     const int f = (fb[a] >> k) & 1;
                     const int np = f ? s + ones : mid + (p0 + k - s) - ones;
                     ones += f;
-                    if (k < nv) sh.L[a][np] = (uint16_t)v[a][k];
+                    sh.L[a][np] = (uint16_t)ent(a, k);
                 }
             }
             if (p0 < mid) {
