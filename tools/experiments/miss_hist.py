@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     os.environ["ICP4R_PHASE_TICKS"] = "1"
+    os.environ.setdefault("ICP4R_FUSE_ORDER", "0")  # (nn_order_kernel records the per-pair work)
     import icp4r
     from icp4r import synth
 
@@ -46,7 +47,9 @@ def main():
         s = np.sort(m)[::-1]
         print(json.dumps({"pass": k, "pairs": int((m > 0).sum()), "misses": int(m.sum()),
                           "top": s[:8].tolist(), "p50": int(np.median(m[m > 0])) if (m > 0).any() else 0,
-                          "over1024": int((m > 1024).sum()), "work_over1024": int(m[m > 1024].sum())}), flush=True)
+                          "over1024": int((m > 1024).sum()), "work_over1024": int(m[m > 1024].sum()),
+                          "le": {str(t): [int(((m > 0) & (m <= t)).sum()), int(m[(m > 0) & (m <= t)].sum())]
+                                 for t in (16, 64, 128, 256, 512)}}), flush=True)
 
 
 if __name__ == "__main__":
