@@ -23,6 +23,7 @@ struct Plan {
     int chunks;   // pruned (streamed): target chunks searched by separate waves (merged by atomicMin)
     bool tile;    // pruned, not batched: nn_tile_kernel (LDS target tiles x query parts; ICP4R_NN_TILE=0: the stream)
     int max_m;    // the plan's largest target (tile grid)
+    int tile_run; // tile: queries per wave run (64, 32, 16): 16 runs per workgroup
     bool solo;    // run_pairs: the whole registration of each pair in one workgroup (solo_kernel; PCL
                   // numerics, one target tile, sources <= kCacheMaxN; ICP4R_SOLO=0 disables)
     int64_t blocks;

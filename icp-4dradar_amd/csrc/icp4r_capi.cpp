@@ -108,6 +108,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
     pl.chunk_sb = 64;
     pl.chunks = 1;
     pl.tile = false;
+    pl.tile_run = 64;
     pl.solo = false;
     pl.max_m = max_m;
     const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
@@ -148,7 +149,17 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
             pl.tile = pl.leaf == 16 && max_m < (1 << 19) && env_int("ICP4R_NN_TILE", 1) != 0;
             if (pl.tile) {
                 pl.chunks = (max_m + 8191) / 8192;
-                pl.blocks = (int64_t)npairs * ((max_n + 1023) / 1024) * pl.chunks;
+                // queries per wave run: shorter runs (more workgroups, each staging its tile) until the
+                // grid covers the CUs — a single pair's search is latency-bound per run (C2 1.85 ->
+                // 1.75 ms, C5 2.35 -> 2.20 ms at 16; ICP4R_TILE_RUN=64 / 32 / 16 forces one)
+                const int tr = env_int("ICP4R_TILE_RUN", 0);
+                auto parts = [&](int run) { return (int64_t)npairs * ((max_n + 16 * run - 1) / (16 * run)) * pl.chunks; };
+                pl.tile_run = 64;
+                if (tr == 64 || tr == 32 || tr == 16)
+                    pl.tile_run = tr;
+                else
+                    while (pl.tile_run > 16 && parts(pl.tile_run) < 256) pl.tile_run /= 2;
+                pl.blocks = parts(pl.tile_run);
             }
             // a PCL-numerics registration whose targets fit one LDS tile: the whole registration of
             // each pair in one workgroup (solo_kernel; ICP4R_SOLO=0: the multi-launch plan)
@@ -369,7 +380,7 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
         return ICP4R_OK;
     }
     if (pl.tile) {  // the events bracket nn_tile_kernel itself (not its seed / record kernels)
-        HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, st, ne->start, ne->stop));
+        HIP_TRY(launch_nn_tile(a, w, npairs, max_n, pl.max_m, fitness_pass, first, pl.tile_run, st, ne->start, ne->stop));
         return ICP4R_OK;
     }
     if (kev) HIP_TRY(hipEventRecord(ne->start, st));

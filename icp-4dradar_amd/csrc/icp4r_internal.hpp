@@ -177,7 +177,7 @@ hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, 
 // the pruned plan's LDS-tiled search: nn_seed_kernel, nn_tile_kernel (target tiles x query parts),
 // corr_kernel (records, when the update reads them)
 hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
-                          int first, hipStream_t st, hipEvent_t tile_start = nullptr, hipEvent_t tile_stop = nullptr);
+                          int first, int qrun, hipStream_t st, hipEvent_t tile_start = nullptr, hipEvent_t tile_stop = nullptr);
 // events recorded around the batched NN's stages (any may be null)
 struct NNLdsEvents {
     hipEvent_t test_start = nullptr, test_stop = nullptr, search_start = nullptr, search_stop = nullptr;

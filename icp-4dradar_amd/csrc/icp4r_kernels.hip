@@ -2417,14 +2417,14 @@ constexpr int kTileMaxM = 1 << (32 - kLdsPosBits);  // target indices that fit t
 // relative sorted position — nn_seed_kernel's rule) is evaluated here, the key is stored, not merged,
 // and the correspondence record is written from the winner's LDS slot — one launch per NN pass
 // instead of three (seed, search, records), two kernel boundaries fewer per ICP iteration.
-__global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first) {
+__global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w, int fitness_pass, int first, int qrun) {
     __shared__ TileShared sh;
     const bool own = first >= 0;  // (single tile: launched with gridDim.x == 1)
     const int tile = blockIdx.x, part = blockIdx.y, p = blockIdx.z;
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
-    const int t0 = tile * kLdsTargets, q0 = part * kLdsWG;
+    const int t0 = tile * kLdsTargets, q0 = part * kLdsWaves * qrun;  // (qrun queries per wave: 64, 32, 16)
     if (t0 >= m || q0 >= n) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2467,12 +2467,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
         ish = sbg[2 * sbl + 1];
     }
     __syncthreads();
-    const int r0 = q0 + wave * 64;  // this wave's run: sorted sources [r0, r0 + 64)
-    if (r0 >= n) return;            // (no barrier follows)
+    const int r0 = q0 + wave * qrun;  // this wave's run: sorted sources [r0, r0 + qrun)
+    if (r0 >= n) return;              // (no barrier follows)
     unsigned long long* bestl = sh.best[wave];
     uint16_t* ring = sh.items[wave];
     NNKey* key = w.nn_key + xs0;
-    const bool live = r0 + lane < n;
+    const bool live = lane < qrun && r0 + lane < n;
     const int sq = live ? r0 + lane : r0;
     const int o = w.sperm[xs0 + sq];  // idle lanes shadow the run's first query
     const float4 v = w.X[xs0 + o];
@@ -4008,11 +4008,13 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
 }
 
 hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
-                          int first, hipStream_t st, hipEvent_t tile_start, hipEvent_t tile_stop) {
-    if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0)
+                          int first, int qrun, hipStream_t st, hipEvent_t tile_start, hipEvent_t tile_stop) {
+    if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0 ||
+        (qrun != 64 && qrun != 32 && qrun != 16))
         return hipErrorInvalidValue;
     hipError_t e;
-    const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + kLdsWG - 1) / kLdsWG, npairs);
+    const int qpart = kLdsWaves * qrun;  // queries per workgroup
+    const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + qpart - 1) / qpart, npairs);
     // one tile: the search kernel seeds, stores and writes the records itself (ICP4R_TILE_OWN=0: the
     // three-launch form, for A/B)
     static const int own_env = getenv("ICP4R_TILE_OWN") ? atoi(getenv("ICP4R_TILE_OWN")) : 1;
@@ -4022,7 +4024,7 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
         hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass,
                            first);
     if (tile_start && (e = hipEventRecord(tile_start, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass, own ? first : -1);
+    hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass, own ? first : -1, qrun);
     if (tile_stop && (e = hipEventRecord(tile_stop, st)) != hipSuccess) return e;
     if (!own && w.corr != nullptr && !fitness_pass)  // records from the merged keys
         hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);

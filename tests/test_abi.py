@@ -106,16 +106,20 @@ def test_plan_geometry(monkeypatch):
     assert c1["pruned"] and not c1["lds"] and c1["solo"] and c1["nn_blocks"] == 1
     assert icp4r.plan(200, 4096, 8192)["solo"] and not icp4r.plan(200, 4097, 8192)["solo"]
     assert not big["solo"] and not icp4r.plan(1, 2048, 8193)["solo"]
-    single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 8 query parts of 1024
-    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 8
+    single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 32 query parts of 256
+    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 32
+    monkeypatch.setenv("ICP4R_TILE_RUN", "64")  # runs of 64 queries: parts of 1024
+    assert icp4r.plan(1, 8192, 8192)["nn_blocks"] == 8 and icp4r.plan(1, 8192, 65540)["nn_blocks"] == 72
+    monkeypatch.delenv("ICP4R_TILE_RUN")
+    assert icp4r.plan(64, 8192, 8192)["nn_blocks"] == 64 * 8  # a small batch already covers the CUs
     monkeypatch.setenv("ICP4R_SOLO", "1")  # forced: up to the cached-neighbour test's 16384 sources
     assert icp4r.plan(1, 8192, 8192)["solo"] and icp4r.plan(200, 16384, 8192)["solo"]
     assert not icp4r.plan(200, 16385, 8192)["solo"]
     monkeypatch.setenv("ICP4R_SOLO", "0")
-    assert not icp4r.plan(1, 2048, 2048)["solo"] and icp4r.plan(1, 2048, 2048)["nn_blocks"] == 2
+    assert not icp4r.plan(1, 2048, 2048)["solo"] and icp4r.plan(1, 2048, 2048)["nn_blocks"] == 8
     monkeypatch.delenv("ICP4R_SOLO")
-    c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 8 query parts
-    assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 8 * 9
+    c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 32 query parts
+    assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 32 * 9
     monkeypatch.setenv("ICP4R_NN_TILE", "0")  # the streamed kernel instead
     single = icp4r.plan(1, 8192, 8192)  # one query per lane, the target in 4 chunks
     assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32 * 4

@@ -275,6 +275,26 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
             assert (cached[k]["T"].reshape(4, 4).T == o["T"]).all() and cached[k]["fitness"] == o["fitness"]
 
 
+def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
+    """nn_tile_kernel's queries per wave run (ICP4R_TILE_RUN 64 / 32 / 16: 1024 / 512 / 256 queries per
+    workgroup, the single-pair plans' default picks the length whose grid covers the CUs): bit-identical
+    registrations, one target tile (C2's shape) and several (a scan-to-map target), aligned clouds
+    included."""
+    import icp4r
+
+    cases = [_pair(41, 8192), _pair(42, 5000, 20000)]
+    p = icp4r.default_params(max_iterations=12, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    for s, t in cases:
+        out = {}
+        for run in ("64", "32", "16"):
+            monkeypatch.setenv("ICP4R_TILE_RUN", run)
+            pl = icp4r.plan(1, len(s), len(t))
+            assert pl["pruned"] and not pl["lds"] and not pl["solo"]
+            r, al = gpu_ctx.align(s, t, p, want_aligned=True)
+            out[run] = (bytes(r), al.tobytes())
+        assert out["64"] == out["32"] == out["16"]
+
+
 @pytest.mark.parametrize("early", [False, True])
 def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
     """The cached-neighbour test run in the tail of fold_update_kernel (default) instead of its own
