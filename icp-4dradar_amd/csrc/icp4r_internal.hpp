@@ -188,7 +188,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
 constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
-constexpr int kSoloMaxN = 4096;           // solo_kernel by default for single pairs of at most this many sources
+constexpr int kSoloMaxN = 1024;           // solo_kernel by default for single pairs of at most this many sources
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
                          hipStream_t st, int tail_test = 0,
                          int order_ncu = 0);  // > 0: the launch also builds the next pass's work list

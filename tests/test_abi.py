@@ -102,9 +102,11 @@ def test_plan_geometry(monkeypatch):
     monkeypatch.delenv("ICP4R_NN_LDS")
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
-    c1 = icp4r.plan(1, 2048, 2048)  # C1: the whole registration in one workgroup (solo_kernel)
-    assert c1["pruned"] and not c1["lds"] and c1["solo"] and c1["nn_blocks"] == 1
-    assert icp4r.plan(200, 4096, 8192)["solo"] and not icp4r.plan(200, 4097, 8192)["solo"]
+    c1 = icp4r.plan(1, 2048, 2048)  # C1: the multi-launch plan, one tile x 8 query parts of 256
+    assert c1["pruned"] and not c1["lds"] and not c1["solo"] and c1["nn_blocks"] == 8
+    small = icp4r.plan(1, 1024, 2048)  # up to 1024 sources: the whole registration in one workgroup
+    assert small["pruned"] and not small["lds"] and small["solo"] and small["nn_blocks"] == 1
+    assert icp4r.plan(200, 1024, 8192)["solo"] and not icp4r.plan(200, 1025, 8192)["solo"]
     assert not big["solo"] and not icp4r.plan(1, 2048, 8193)["solo"]
     single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 32 query parts of 256
     assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 32
