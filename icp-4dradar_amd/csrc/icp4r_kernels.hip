@@ -176,7 +176,9 @@ __device__ __forceinline__ void write_corr(const WorkArgs& w, const PairArgs& a,
 
 // ---------------------------------------------------------------------------------------------
 // init_kernel: one workgroup per pair.
-constexpr int kInitWG = 256;
+// WG threads per pair: 256 for batches (HBM-bound there), 1024 for a few pairs, whose validation
+// passes are latency-bound rounds of loads (C5's 65k-point map: 16 rounds of 256 x 16 -> 4)
+template <int kInitWG>
 __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     __shared__ float Tg[16];
     __shared__ int ident;
@@ -683,14 +685,27 @@ __device__ void index_boxes(const WorkArgs& w, int p, int n) {
     const int B = w.leaf;
     const int nb = (n + B - 1) / B;
     float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+    // (each block's points, and each superblock's block boxes, loaded all at once: a load-use loop
+    // had waited out one round trip per point — 8 blocks x 16 points per thread for a 65k-point map)
+    constexpr int kHalf = 16;  // w.leaf: 16 or 32 points, 16 at a time
     for (int b = tid; b < w.b_stride; b += kIdxWG) {
         float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
         if (b < nb) {
-            const int e = min(n, (b + 1) * B);
-            for (int k = b * B; k < e; ++k) {
-                const float4 v = ts[k];
-                l.x = fminf(l.x, v.x); l.y = fminf(l.y, v.y); l.z = fminf(l.z, v.z);
-                h.x = fmaxf(h.x, v.x); h.y = fmaxf(h.y, v.y); h.z = fmaxf(h.z, v.z);
+            const int e = min(n, (b + 1) * B) - 1;  // the block's last real point
+            for (int h0 = 0; h0 < B; h0 += kHalf) {
+                float vx[kHalf], vy[kHalf], vz[kHalf];
+#pragma unroll
+                for (int k = 0; k < kHalf; ++k) {  // (repeats of the last point: no change)
+                    const float4 v = ts[min(b * B + h0 + k, e)];
+                    vx[k] = v.x;
+                    vy[k] = v.y;
+                    vz[k] = v.z;
+                }
+#pragma unroll
+                for (int k = 0; k < kHalf; ++k) {
+                    l.x = fminf(l.x, vx[k]); l.y = fminf(l.y, vy[k]); l.z = fminf(l.z, vz[k]);
+                    h.x = fmaxf(h.x, vx[k]); h.y = fmaxf(h.y, vy[k]); h.z = fmaxf(h.z, vz[k]);
+                }
             }
         }
         tb[2 * b] = l;
@@ -700,8 +715,12 @@ __device__ void index_boxes(const WorkArgs& w, int p, int n) {
     float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
     for (int s = tid; s < w.sb_stride; s += kIdxWG) {
         float4 l = make_float4(INFINITY, INFINITY, INFINITY, 0.f), h = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-        for (int b = s * kSuper; b < (s + 1) * kSuper; ++b) {
-            const float4 bl = tb[2 * b], bh = tb[2 * b + 1];
+        float4 bb[2 * kSuper];
+#pragma unroll
+        for (int k = 0; k < 2 * kSuper; ++k) bb[k] = tb[2 * s * kSuper + k];
+#pragma unroll
+        for (int k = 0; k < kSuper; ++k) {
+            const float4 bl = bb[2 * k], bh = bb[2 * k + 1];
             l.x = fminf(l.x, bl.x); l.y = fminf(l.y, bl.y); l.z = fminf(l.z, bl.z);
             h.x = fmaxf(h.x, bh.x); h.y = fmaxf(h.y, bh.y); h.z = fmaxf(h.z, bh.z);
         }
@@ -830,7 +849,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     // Large clouds (the scan-to-map target): every pass over the cloud keeps kMoPer points per thread
     // in flight (a load-use loop had waited out one round trip per 512 points: 3 x 128 of them for a
     // 65k-point map, ~140 us of a single registration)
-    constexpr int kMoPer = 8;
+    constexpr int kMoPer = 16;
     auto sweep = [&](auto&& f) {
         for (int i0 = 0; i0 < n; i0 += kIdxWG * kMoPer) {
             float4 v[kMoPer];
@@ -3932,7 +3951,10 @@ hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st) {
 
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
-    hipLaunchKernelGGL(init_kernel, dim3(npairs), dim3(kInitWG), 0, st, a, w);
+    if (npairs < 64)
+        hipLaunchKernelGGL(init_kernel<1024>, dim3(npairs), dim3(1024), 0, st, a, w);
+    else
+        hipLaunchKernelGGL(init_kernel<256>, dim3(npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();
 }
 
