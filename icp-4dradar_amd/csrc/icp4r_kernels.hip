@@ -2686,6 +2686,54 @@ __device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
     return acc;
 }
 
+// The double chains (PCL's MSE sum and getFitnessScore) over values the fillers stored as doubles:
+// the widening (exact) is done by the filler waves, so the fold lane only adds — a v_cvt_f64_f32 in
+// front of every dependent v_add_f64 had put the chain at ~13.5 cycles per element.  Groups of 16
+// doubles (8 x b128), three in rotation as in fold_seq.
+__device__ __forceinline__ void load_group_d(double2 (&g)[8], const double* f) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) g[u] = *reinterpret_cast<const double2*>(f + 2 * u);
+}
+__device__ __forceinline__ void add_group_d(double& acc, const double2 (&g)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        acc = acc + g[u].x;
+        acc = acc + g[u].y;
+    }
+}
+__device__ __forceinline__ double fold_seq_d(const double* f, int len, double acc) {
+    int k = 0;
+    if (len >= 48) {
+        double2 a[8], b[8], c[8];
+        load_group_d(a, f);
+        load_group_d(b, f + 16);
+        for (; k + 48 <= len; k += 48) {
+            // the loads past this round re-read group 0 harmlessly when nothing follows
+            const int n1 = (k + 64 <= len) ? k + 48 : 0, n2 = (k + 80 <= len) ? k + 64 : 0;
+            load_group_d(c, f + k + 32);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group_d(acc, a);
+            load_group_d(a, f + n1);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group_d(acc, b);
+            load_group_d(b, f + n2);
+            __builtin_amdgcn_sched_barrier(0);
+            add_group_d(acc, c);
+        }
+        // a, b hold [k, k + 16) and [k + 16, k + 32) when they exist
+        if (k + 16 <= len) {
+            add_group_d(acc, a);
+            k += 16;
+            if (k + 16 <= len) {
+                add_group_d(acc, b);
+                k += 16;
+            }
+        }
+    }
+    for (; k < len; ++k) acc = acc + f[k];
+    return acc;
+}
+
 // Brute-force path: the correspondence arrays from the merged NN keys (the pruned kernel writes
 // them itself).
 __global__ __launch_bounds__(256) void corr_kernel(PairArgs a, WorkArgs w) {
@@ -3185,7 +3233,7 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
 #pragma unroll
             for (int k = 0; k < 6; ++k) b[k][o] = v[k];
             b[6][o] = wt;
-            b[7][o] = dd;
+            reinterpret_cast<double*>(b[7])[o] = (double)dd;  // (rows 7-8: the MSE chain's doubles)
         }
     };
     float acc = (lane < 6) ? ident : 0.0f;
@@ -3201,7 +3249,7 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     } else if (wv * 64 < fill0) {  // the MSE chain
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane == 0) dacc = fold_seq<double>(buf[c & 1][7], min(CH, n - c * CH), dacc);
+            if (lane == 0) dacc = fold_seq_d(reinterpret_cast<const double*>(buf[c & 1][7]), min(CH, n - c * CH), dacc);
         }
     } else {
         if (nch > 0) {
@@ -3546,7 +3594,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     // index order, by wave 0 lane 0 over LDS chunks that waves 1..3 stage (double buffer); points
     // beyond max_range contribute +0 (a no-op on the non-negative running sum); the count is an
     // exact integer reduction.  Bit-identical to the reference loop.
-    __shared__ float chunk[2][kFoldChunkP];
+    __shared__ double chunk[2][kFoldChunkP];  // (doubles: the fold lane only adds, fold_seq_d)
     __shared__ int32_t fcnt_w[kFinWG / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double fsum = 0.0;
@@ -3558,7 +3606,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
             for (int o = threadIdx.x - 64; o < len; o += kFinWG - 64) {
                 const float d2 = key_d2(w.nn_key[slot0 + base + o]);  // (d² only: see WorkArgs::nn_key)
                 const bool in = (double)d2 <= a.kp.fit_max_range;
-                chunk[c & 1][o] = in ? d2 : 0.0f;
+                chunk[c & 1][o] = in ? (double)d2 : 0.0;
                 fcnt += in ? 1 : 0;
             }
         };
@@ -3566,7 +3614,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
             if (wave == 0) {
-                if (lane == 0) fsum = fold_seq<double>(chunk[c & 1], min(kFoldChunkP, n - c * kFoldChunkP), fsum);
+                if (lane == 0) fsum = fold_seq_d(chunk[c & 1], min(kFoldChunkP, n - c * kFoldChunkP), fsum);
             } else if (c + 1 < nch) {
                 fill(c + 1);
             }
@@ -3662,7 +3710,7 @@ struct SoloShared {
         SoloSearch s;
         SoloFold f;
         SoloTest c;
-        alignas(16) float fit[2][kSoloFitChunk];  // the fitness sum's chunks
+        alignas(16) double fit[2][kSoloFitChunk];  // the fitness sum's chunks (doubles: fold_seq_d)
     } u;
     int32_t wtot[kLdsWaves];  // per-wave counts (the test's misses, the fitness count)
     int32_t mcount;           // the test's LDS record count
@@ -3675,7 +3723,7 @@ struct SoloShared {
         SoloTile t;
         SoloFold f;
         SoloTest c;
-        alignas(16) float fit[2][kSoloFitChunk];
+        alignas(16) double fit[2][kSoloFitChunk];
     } u;
     SoloSearch s;
     int32_t wtot[kLdsWaves];
@@ -3896,7 +3944,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
             for (int o = tid - 64; o < len; o += kSoloWG - 64) {
                 const float d2 = key_d2(key[base + o]);
                 const bool in = (double)d2 <= kp.fit_max_range;
-                SOLO_FIT(sh)[c & 1][o] = in ? d2 : 0.0f;
+                SOLO_FIT(sh)[c & 1][o] = in ? (double)d2 : 0.0;
                 fcnt += in ? 1 : 0;
             }
         };
@@ -3904,7 +3952,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
             if (wave == 0) {
-                if (lane == 0) fsum = fold_seq<double>(SOLO_FIT(sh)[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
+                if (lane == 0) fsum = fold_seq_d(SOLO_FIT(sh)[c & 1], min(kSoloFitChunk, n - c * kSoloFitChunk), fsum);
             } else if (c + 1 < nch) {
                 fill(c + 1);
             }
