@@ -463,6 +463,11 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     w.stage_first = (w.src_by_tgt && (pl.lds || pl.solo) && w.qv && w.qm) ? 1 : 0;
     // multi-tile plan (the scan-to-map target), PCL numerics: seeds written by the update's transform
     w.seed_next = (pl.tile && pl.chunks > 1 && pcl && w.corr && env_int("ICP4R_FUSE_SEED", 1) != 0) ? 1 : 0;
+    // one-tile plan (C1, C2), PCL numerics: the update's transformCloud(T_inc) deferred into the next
+    // search, which reads every query anyway (nn_tile_kernel; ICP4R_TILE_DEFER=0: the update does it)
+    if (pl.tile && pl.chunks == 1 && !pl.solo && pcl && w.corr && env_int("ICP4R_TILE_OWN", 1) != 0 &&
+        env_int("ICP4R_TILE_DEFER", 1) != 0)
+        w.defer_xform = 1;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));

@@ -2494,7 +2494,17 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     const bool live = lane < qrun && r0 + lane < n;
     const int sq = live ? r0 + lane : r0;
     const int o = w.sperm[xs0 + sq];  // idle lanes shadow the run's first query
-    const float4 v = w.X[xs0 + o];
+    float4 v = w.X[xs0 + o];
+    if (own && first == 0 && !fitness_pass && w.defer_xform) {
+        // the previous update's transformCloud(T_inc), deferred to here (one read and write of X
+        // per pass instead of a pass over the cloud by the update's one workgroup); every query
+        // belongs to one lane of one workgroup of the single tile, which writes it back
+        float T[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].T_inc[q]);
+        xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
+        if (live) w.X[xs0 + o] = v;
+    }
     NNKey k0 = key[o];
     const float x = v.x, y = v.y, z = v.z;
     if (own) {  // the seed (nn_seed_kernel's rule), evaluated at the query's current position

@@ -277,22 +277,26 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
 
 def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
     """nn_tile_kernel's queries per wave run (ICP4R_TILE_RUN 64 / 32 / 16: 1024 / 512 / 256 queries per
-    workgroup, the single-pair plans' default picks the length whose grid covers the CUs): bit-identical
-    registrations, one target tile (C2's shape) and several (a scan-to-map target), aligned clouds
-    included."""
+    workgroup, the single-pair plans' default picks the length whose grid covers the CUs), and the
+    update's transform deferred into the one-tile search or not (ICP4R_TILE_DEFER): bit-identical
+    registrations, one target tile (C2's and C1's shapes) and several (a scan-to-map target), fixed
+    iterations and PCL's defaults, aligned clouds included."""
     import icp4r
 
-    cases = [_pair(41, 8192), _pair(42, 5000, 20000)]
-    p = icp4r.default_params(max_iterations=12, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-    for s, t in cases:
-        out = {}
-        for run in ("64", "32", "16"):
-            monkeypatch.setenv("ICP4R_TILE_RUN", run)
-            pl = icp4r.plan(1, len(s), len(t))
-            assert pl["pruned"] and not pl["lds"] and not pl["solo"]
-            r, al = gpu_ctx.align(s, t, p, want_aligned=True)
-            out[run] = (bytes(r), al.tobytes())
-        assert out["64"] == out["32"] == out["16"]
+    cases = [_pair(41, 8192), _pair(42, 5000, 20000), _pair(43, 2048)]
+    for params in (icp4r.default_params(max_iterations=12, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0),
+                   icp4r.default_params()):
+        for s, t in cases:
+            out = {}
+            # (ICP4R_TILE_DEFER=0: the update transforms the cloud itself instead of the next search)
+            for run, defer in (("64", "1"), ("32", "1"), ("16", "1"), ("16", "0")):
+                monkeypatch.setenv("ICP4R_TILE_RUN", run)
+                monkeypatch.setenv("ICP4R_TILE_DEFER", defer)
+                pl = icp4r.plan(1, len(s), len(t))
+                assert pl["pruned"] and not pl["lds"] and not pl["solo"]
+                r, al = gpu_ctx.align(s, t, params, want_aligned=True)
+                out[run + defer] = (bytes(r), al.tobytes())
+            assert out["641"] == out["321"] == out["161"] == out["160"]
 
 
 @pytest.mark.parametrize("early", [False, True])
