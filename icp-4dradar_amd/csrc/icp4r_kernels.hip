@@ -411,8 +411,11 @@ __device__ __forceinline__ int kd_split(int S, int leaf) {
 // bits at [0, 6)) and every internal node at [8 + heap id] (root 1, children 2i / 2i + 1) as
 // 1 << 31 | mid << 13 | axis << 11 | key of the first point right of the split (on its axis); the
 // caller zeroes the node slots (0: leaf).
-template <typename Get>  // Get: int -> float4, point i of the cloud
+// KPER: list positions per thread in the levels (16 covers kKdMaxN; 8 for clouds of at most
+// kKdMaxN / 2 points, so that a level's per-thread LDS work halves).
+template <int KPER, typename Get>  // Get: int -> float4, point i of the cloud
 __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, uint32_t* kdn = nullptr) {
+    static_assert(KPER % 8 == 0 && KPER <= 16 && KPER * kIdxWG >= kKdMaxN / 2, "list positions per thread");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
     // 1. bounding box -> quantisation.  The thread's points (i = tid + k * kIdxWG) are loaded once,
@@ -516,9 +519,9 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
     __syncthreads();
     if (tk) tk[1] = __builtin_amdgcn_s_memrealtime();
     // 3. levels: split every non-leaf segment at the median of its widest axis.  Segment bounds are
-    // multiples of 16 >= kKdPer, so a thread's positions [p0, p0 + kKdPer) share one segment [s, e),
+    // multiples of 16 >= KPER, so a thread's positions [p0, p0 + KPER) share one segment [s, e),
     // tracked per thread; the thread owning a segment's first position decides its split.
-    const int p0 = tid * kKdPer;
+    const int p0 = tid * KPER;
     int s = 0, e = n, node = 1;  // this thread's segment and its heap id
     for (;;) {
         bool any = false;
@@ -556,18 +559,18 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         }
         int mid = 0, ax = 3;
         if (p0 < n) {
-            mid = sh.seg_mid[s / kKdPer];
-            ax = sh.seg_ax[s / kKdPer];
+            mid = sh.seg_mid[s / KPER];
+            ax = sh.seg_ax[s / KPER];
         }
         // this thread's list entries (one 16-B LDS read per list; entries >= n are never used), two
         // u16 entries per register as read (a u16 array went to scratch, 32-bit elements filled the
         // register budget: a spill in every level)
-        uint32_t vp[3][kKdPer / 2];
-        static_assert(kKdPer % 8 == 0, "whole 16-B reads of the lists");
+        uint32_t vp[3][KPER / 2];
+        static_assert(KPER % 8 == 0, "whole 16-B reads of the lists");
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int q8 = 0; q8 < kKdPer / 8; ++q8) {
+            for (int q8 = 0; q8 < KPER / 8; ++q8) {
                 const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[a][p0 + 8 * q8]);
                 vp[a][4 * q8] = r.x;
                 vp[a][4 * q8 + 1] = r.y;
@@ -575,26 +578,26 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
                 vp[a][4 * q8 + 3] = r.w;
             }
         auto ent = [&](int a, int k) -> uint32_t { return (vp[a][k >> 1] >> (16 * (k & 1))) & 0xffffu; };
-        const int nv = min(kKdPer, n - p0);  // valid entries (<= 0: none)
+        const int nv = min(KPER, n - p0);  // valid entries (<= 0: none)
         const bool act = nv > 0 && ax < 3;    // this thread's segment splits
         // Every LDS access of the level below is unconditional: a per-entry guard had put a branch and
         // a wait around each (~6 us per level on a single 2k-point build).  Entries past nv (the thread
         // holding position n - 1) may hold anything: their flag goes to the junk slot, their flag reads
-        // are masked into range and dropped, and their partition writes land in [n, p0 + kKdPer).
+        // are masked into range and dropped, and their partition writes land in [n, p0 + KPER).
         if (act) {  // "left" per point, from the split axis' list
-            uint32_t va[kKdPer / 2];  // the split axis' entries, re-read from LDS (a select among the
+            uint32_t va[KPER / 2];  // the split axis' entries, re-read from LDS (a select among the
                                       // registers became a dynamic index: a round trip through scratch)
 #pragma unroll
-            for (int q8 = 0; q8 < kKdPer / 8; ++q8) {
+            for (int q8 = 0; q8 < KPER / 8; ++q8) {
                 const uint4 r = *reinterpret_cast<const uint4*>(&sh.L[ax][p0 + 8 * q8]);
                 va[4 * q8] = r.x;
                 va[4 * q8 + 1] = r.y;
                 va[4 * q8 + 2] = r.z;
                 va[4 * q8 + 3] = r.w;
             }
-            const uint32_t lf = p0 < mid ? 1u : 0u;  // (segment bounds and mid are multiples of kKdPer)
+            const uint32_t lf = p0 < mid ? 1u : 0u;  // (segment bounds and mid are multiples of KPER)
 #pragma unroll
-            for (int k = 0; k < kKdPer; ++k) {
+            for (int k = 0; k < KPER; ++k) {
                 const uint32_t i = (va[k >> 1] >> (16 * (k & 1))) & 0xffffu;
                 sh.u.p.left[k < nv ? i : kKdMaxN] = (kd_flag_t)lf;
             }
@@ -604,16 +607,16 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         // this thread's entries as bit masks (the split axis' own read back what this thread wrote)
         uint32_t fb[3] = {0u, 0u, 0u};
         if (act) {
-            uint32_t fl[3][kKdPer];
+            uint32_t fl[3][KPER];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #pragma unroll
-                for (int k = 0; k < kKdPer; ++k) fl[a][k] = sh.u.p.left[ent(a, k) & (kKdMaxN - 1)];
+                for (int k = 0; k < KPER; ++k) fl[a][k] = sh.u.p.left[ent(a, k) & (kKdMaxN - 1)];
             const uint32_t vm = nv >= 32 ? ~0u : (1u << nv) - 1u;
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
 #pragma unroll
-                for (int k = 0; k < kKdPer; ++k) fb[a] |= fl[a][k] << k;
+                for (int k = 0; k < KPER; ++k) fb[a] |= fl[a][k] << k;
                 fb[a] &= vm;
             }
         }
@@ -631,7 +634,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
 #pragma unroll
         for (int a = 0; a < 3; ++a) sh.u.p.tpre[a][tid] = (uint16_t)(incl[a] - cnt[a]);  // in-wave exclusive
         __syncthreads();  // wave totals and in-wave prefixes visible; every thread holds its entries in v
-        const int sw = (s / kKdPer) >> 6;  // the wave owning the segment's first position
+        const int sw = (s / KPER) >> 6;  // the wave owning the segment's first position
         if (act) {
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -652,9 +655,9 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
                     bs += k < sw ? c : 0;
                 }
                 // "left" points before p0 inside the segment
-                int ones = (bw + incl[a] - cnt[a]) - (bs + (int)sh.u.p.tpre[a][s / kKdPer]);
+                int ones = (bw + incl[a] - cnt[a]) - (bs + (int)sh.u.p.tpre[a][s / KPER]);
 #pragma unroll
-                for (int k = 0; k < kKdPer; ++k) {
+                for (int k = 0; k < KPER; ++k) {
                     const int f = (fb[a] >> k) & 1;
                     const int np = f ? s + ones : mid + (p0 + k - s) - ones;
                     ones += f;
@@ -763,7 +766,10 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
         uint32_t* kdn = (is_tgt && w.kdn && w.src_by_tgt) ? w.kdn + (int64_t)p * kKdnStride : nullptr;
         if (kdn)
             for (int k = tid; k < kKdnStride; k += kIdxWG) kdn[k] = 0u;  // (kd_order syncs before writing)
-        kd_order(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
+        if (n <= kKdMaxN / 2)
+            kd_order<8>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
+        else
+            kd_order<16>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
         const uint16_t* ord = shu.kd.L[0];
         if (is_tgt) {
             // sorted targets, padding (+inf coordinates, .w = the last target's index: never a match,
@@ -1139,7 +1145,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_refine_kernel(PairArgs a, Wor
     const int len = min(kKdMaxN, m - c0);
     const int tid = threadIdx.x, lane = tid & 63;
     float4* ts = w.tsort + (int64_t)p * w.t_stride + c0;
-    kd_order(shu.kd, [&](int i) { return ts[i]; }, len, w.leaf, nullptr);
+    kd_order<16>(shu.kd, [&](int i) { return ts[i]; }, len, w.leaf, nullptr);
     const uint16_t* ord = shu.kd.L[0];
     float4 v[kKdPer];  // the chunk in its new order (read before anything is overwritten)
 #pragma unroll
