@@ -151,14 +151,15 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
                 pl.chunks = (max_m + 8191) / 8192;
                 // queries per wave run: shorter runs (more workgroups, each staging its tile) until the
                 // grid covers the CUs — a single pair's search is latency-bound per run (C2 1.85 ->
-                // 1.75 ms, C5 2.35 -> 2.20 ms at 16; ICP4R_TILE_RUN=64 / 32 / 16 forces one)
+                // 1.75 ms, C5 2.35 -> 2.20 ms at 16; C1 0.457 -> 0.449 ms at 8; ICP4R_TILE_RUN=64 / 32 /
+                // 16 / 8 forces one)
                 const int tr = env_int("ICP4R_TILE_RUN", 0);
                 auto parts = [&](int run) { return (int64_t)npairs * ((max_n + 16 * run - 1) / (16 * run)) * pl.chunks; };
                 pl.tile_run = 64;
-                if (tr == 64 || tr == 32 || tr == 16)
+                if (tr == 64 || tr == 32 || tr == 16 || tr == 8)
                     pl.tile_run = tr;
                 else
-                    while (pl.tile_run > 16 && parts(pl.tile_run) < 256) pl.tile_run /= 2;
+                    while (pl.tile_run > 8 && parts(pl.tile_run) < 256) pl.tile_run /= 2;
                 pl.blocks = parts(pl.tile_run);
             }
             // a PCL-numerics registration whose targets fit one LDS tile: the whole registration of

@@ -2449,7 +2449,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
-    const int t0 = tile * kLdsTargets, q0 = part * kLdsWaves * qrun;  // (qrun queries per wave: 64, 32, 16)
+    const int t0 = tile * kLdsTargets, q0 = part * kLdsWaves * qrun;  // (qrun queries per wave: 64, 32, 16, 8)
     if (t0 >= m || q0 >= n) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -4096,7 +4096,7 @@ hipError_t launch_nn_lds(const PairArgs& a, const WorkArgs& w, int npairs, int m
 hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int max_m, int fitness_pass,
                           int first, int qrun, hipStream_t st, hipEvent_t tile_start, hipEvent_t tile_stop) {
     if (w.leaf != kLdsLeaf || !w.tsort || !w.sperm || max_m >= kTileMaxM || npairs <= 0 || max_n <= 0 ||
-        (qrun != 64 && qrun != 32 && qrun != 16))
+        (qrun != 64 && qrun != 32 && qrun != 16 && qrun != 8))
         return hipErrorInvalidValue;
     hipError_t e;
     const int qpart = kLdsWaves * qrun;  // queries per workgroup

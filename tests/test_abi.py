@@ -102,14 +102,14 @@ def test_plan_geometry(monkeypatch):
     monkeypatch.delenv("ICP4R_NN_LDS")
     assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
     assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
-    c1 = icp4r.plan(1, 2048, 2048)  # C1: the multi-launch plan, one tile x 8 query parts of 256
-    assert c1["pruned"] and not c1["lds"] and not c1["solo"] and c1["nn_blocks"] == 8
+    c1 = icp4r.plan(1, 2048, 2048)  # C1: the multi-launch plan, one tile x 16 query parts of 128
+    assert c1["pruned"] and not c1["lds"] and not c1["solo"] and c1["nn_blocks"] == 16
     small = icp4r.plan(1, 1024, 2048)  # up to 1024 sources: the whole registration in one workgroup
     assert small["pruned"] and not small["lds"] and small["solo"] and small["nn_blocks"] == 1
     assert icp4r.plan(200, 1024, 8192)["solo"] and not icp4r.plan(200, 1025, 8192)["solo"]
     assert not big["solo"] and not icp4r.plan(1, 2048, 8193)["solo"]
-    single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 32 query parts of 256
-    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 32
+    single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 64 query parts of 128
+    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 64
     monkeypatch.setenv("ICP4R_TILE_RUN", "64")  # runs of 64 queries: parts of 1024
     assert icp4r.plan(1, 8192, 8192)["nn_blocks"] == 8 and icp4r.plan(1, 8192, 65540)["nn_blocks"] == 72
     monkeypatch.delenv("ICP4R_TILE_RUN")
@@ -118,7 +118,7 @@ def test_plan_geometry(monkeypatch):
     assert icp4r.plan(1, 8192, 8192)["solo"] and icp4r.plan(200, 16384, 8192)["solo"]
     assert not icp4r.plan(200, 16385, 8192)["solo"]
     monkeypatch.setenv("ICP4R_SOLO", "0")
-    assert not icp4r.plan(1, 2048, 2048)["solo"] and icp4r.plan(1, 2048, 2048)["nn_blocks"] == 8
+    assert not icp4r.plan(1, 2048, 2048)["solo"] and icp4r.plan(1, 2048, 2048)["nn_blocks"] == 16
     monkeypatch.delenv("ICP4R_SOLO")
     c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 32 query parts
     assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 32 * 9

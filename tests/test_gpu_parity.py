@@ -276,7 +276,7 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
 
 
 def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
-    """nn_tile_kernel's queries per wave run (ICP4R_TILE_RUN 64 / 32 / 16: 1024 / 512 / 256 queries per
+    """nn_tile_kernel's queries per wave run (ICP4R_TILE_RUN 64 / 32 / 16 / 8: 1024 / 512 / 256 / 128 queries per
     workgroup, the single-pair plans' default picks the length whose grid covers the CUs), and the
     update's transform deferred into the one-tile search or not (ICP4R_TILE_DEFER): bit-identical
     registrations, one target tile (C2's and C1's shapes) and several (a scan-to-map target), fixed
@@ -289,14 +289,14 @@ def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
         for s, t in cases:
             out = {}
             # (ICP4R_TILE_DEFER=0: the update transforms the cloud itself instead of the next search)
-            for run, defer in (("64", "1"), ("32", "1"), ("16", "1"), ("16", "0")):
+            for run, defer in (("64", "1"), ("32", "1"), ("16", "1"), ("8", "1"), ("16", "0")):
                 monkeypatch.setenv("ICP4R_TILE_RUN", run)
                 monkeypatch.setenv("ICP4R_TILE_DEFER", defer)
                 pl = icp4r.plan(1, len(s), len(t))
                 assert pl["pruned"] and not pl["lds"] and not pl["solo"]
                 r, al = gpu_ctx.align(s, t, params, want_aligned=True)
                 out[run + defer] = (bytes(r), al.tobytes())
-            assert out["641"] == out["321"] == out["161"] == out["160"]
+            assert out["641"] == out["321"] == out["161"] == out["81"] == out["160"]
 
 
 @pytest.mark.parametrize("early", [False, True])
