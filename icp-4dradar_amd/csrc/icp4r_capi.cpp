@@ -285,8 +285,9 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.tbox = static_cast<float4*>(ctx->tbox.p);
         w.sbox = static_cast<float4*>(ctx->sbox.p);
         w.sperm = static_cast<int32_t*>(ctx->sperm.p);
-        HIP_TRY(ctx->kdn.ensure((size_t)npairs * kKdnStride * sizeof(uint32_t)));
+        HIP_TRY(ctx->kdn.ensure((size_t)npairs * (kKdnStride + 8) * sizeof(uint32_t)));
         w.kdn = static_cast<uint32_t*>(ctx->kdn.p);
+        w.tbb = reinterpret_cast<float*>(w.kdn + (size_t)npairs * kKdnStride);
         if (pl.solo) {  // the query list and the cached-neighbour state (solo_kernel)
             HIP_TRY(ctx->qv.ensure((size_t)slots * sizeof(float4)));
             HIP_TRY(ctx->qm.ensure((size_t)slots * sizeof(uint2)));
@@ -423,6 +424,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.sbox += (int64_t)p0 * 2 * w.sb_stride;
         wg.sperm += xs;
         if (wg.kdn) wg.kdn += (int64_t)p0 * kKdnStride;
+        if (wg.tbb) wg.tbb += (int64_t)p0 * 8;
     }
     if (wg.nn_u) {
         wg.nn_u += xs;

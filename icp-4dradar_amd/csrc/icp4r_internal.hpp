@@ -119,6 +119,8 @@ struct WorkArgs {
                           // write the next NN pass's seed keys (the previous NN at the moved point) from the
                           // correspondence records, so no nn_seed_kernel launch
                           // (qv / qm, sorted order) itself; 0: the first pass' nn_key seeds
+    float* tbb;         // [npairs * 8] the target's bounding box (lo xyz, hi xyz), from init_kernel's
+                        // validation pass (the Morton index skips its own pass over the cloud); or nullptr
     uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,
                         // [8 + node] internal node (heap order) = 1 << 31 | mid << 13 | axis << 11 | key
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):

@@ -207,13 +207,40 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     int bad = 0;
     // (the target is only validated: 16 points per thread in flight — a scan-to-map target of 65k
     // points had taken 64 dependent rounds of 1024, ~65 us of a single registration)
+    // (and its bounding box, for the Morton index of a large target: w.tbb)
     constexpr int kTgtPer = 16;
+    float bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i0 = 0; i0 < m; i0 += kInitWG * kTgtPer) {
         float4 t[kTgtPer];
 #pragma unroll
         for (int e = 0; e < kTgtPer; ++e) t[e] = tgt[min(i0 + e * kInitWG + tid, m - 1)];
 #pragma unroll
-        for (int e = 0; e < kTgtPer; ++e) bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
+        for (int e = 0; e < kTgtPer; ++e) {  // (a clamped duplicate of point m - 1 changes no extent)
+            bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
+            bl[0] = fminf(bl[0], t[e].x); bl[1] = fminf(bl[1], t[e].y); bl[2] = fminf(bl[2], t[e].z);
+            bh[0] = fmaxf(bh[0], t[e].x); bh[1] = fmaxf(bh[1], t[e].y); bh[2] = fmaxf(bh[2], t[e].z);
+        }
+    }
+    if (w.tbb) {
+        __shared__ float bred[kInitWG / 64][6];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                bl[k] = fminf(bl[k], __shfl_xor(bl[k], off, 64));
+                bh[k] = fmaxf(bh[k], __shfl_xor(bh[k], off, 64));
+            }
+        if ((tid & 63) == 0)
+            for (int k = 0; k < 3; ++k) {
+                bred[tid >> 6][k] = bl[k];
+                bred[tid >> 6][3 + k] = bh[k];
+            }
+        __syncthreads();
+        if (tid < 6) {
+            float v = bred[0][tid];
+            for (int q = 1; q < kInitWG / 64; ++q) v = tid < 3 ? fminf(v, bred[q][tid]) : fmaxf(v, bred[q][tid]);
+            w.tbb[(int64_t)p * 8 + tid] = v;
+        }
     }
     for (int i0 = 0; i0 < n; i0 += kInitWG * kInitPer) {
         float4 v[kInitPer];
@@ -866,12 +893,19 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
                 if (i0 + e * kIdxWG + tid < n) f(i0 + e * kIdxWG + tid, v[e]);
         }
     };
-    // 1. bounding box
+    // 1. bounding box (a target's from init_kernel's validation pass: one pass over the cloud fewer)
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    sweep([&](int, const float4& v) {
-        mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
-        mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
-    });
+    if (is_tgt && w.tbb) {
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = w.tbb[(int64_t)p * 8 + k];
+            mx[k] = w.tbb[(int64_t)p * 8 + 3 + k];
+        }
+    } else {
+        sweep([&](int, const float4& v) {
+            mn[0] = fminf(mn[0], v.x); mn[1] = fminf(mn[1], v.y); mn[2] = fminf(mn[2], v.z);
+            mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
+        });
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
