@@ -288,6 +288,17 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         HIP_TRY(ctx->kdn.ensure((size_t)npairs * (kKdnStride + 8) * sizeof(uint32_t)));
         w.kdn = static_cast<uint32_t*>(ctx->kdn.p);
         w.tbb = reinterpret_cast<float*>(w.kdn + (size_t)npairs * kKdnStride);
+        // a target too large for the in-LDS kd build, for few pairs: its Morton sort on several
+        // workgroups (one 8192-point chunk each) before index_refine_kernel re-orders every chunk
+        // (ICP4R_MORTON_MWG=0: one workgroup per target, as for the batches)
+        constexpr int kChunk = 8192;
+        const int64_t mog = (w.t_stride + kChunk - 1) / kChunk;
+        if ((w.kd_index & 1) && w.t_stride > kChunk && (pl.leaf == 16 || pl.leaf == 32) &&
+            npairs * mog <= 2048 && env_int("ICP4R_MORTON_MWG", 1)) {
+            HIP_TRY(ctx->mo_hist.ensure((size_t)npairs * mog * (1u << 14) * sizeof(uint32_t)));
+            w.mo_hist = static_cast<uint32_t*>(ctx->mo_hist.p);
+            w.mo_groups = (int32_t)mog;
+        }
         if (pl.solo) {  // the query list and the cached-neighbour state (solo_kernel)
             HIP_TRY(ctx->qv.ensure((size_t)slots * sizeof(float4)));
             HIP_TRY(ctx->qm.ensure((size_t)slots * sizeof(uint2)));
@@ -425,6 +436,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         wg.sperm += xs;
         if (wg.kdn) wg.kdn += (int64_t)p0 * kKdnStride;
         if (wg.tbb) wg.tbb += (int64_t)p0 * 8;
+        if (wg.mo_hist) wg.mo_hist += (int64_t)p0 * w.mo_groups * (1 << 14);
     }
     if (wg.nn_u) {
         wg.nn_u += xs;

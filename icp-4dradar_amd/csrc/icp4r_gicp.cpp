@@ -57,7 +57,11 @@ int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, c
         ai.tgt = cloud;
         ai.tgt_off = off;
         ai.tgt_n = cnt;
-        HIP_TRY(launch_index(ai, w, npairs, st));
+        // (w.tbb holds init_kernel's target boxes, not this cloud's: the index finds its own)
+        WorkArgs wi = w;
+        wi.tbb = nullptr;
+        wi.mo_hist = nullptr;
+        HIP_TRY(launch_index(ai, wi, npairs, st));
         HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, w, npairs, max_n, stride, k, reg, out, st));
     } else {
         HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, st));

@@ -767,13 +767,9 @@ __device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArg
            a.src_n[p] <= kKdMaxN;
 }
 
-__global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
-    __shared__ IndexShared shu;
-    // grid (pairs, 2): target and source of every pair; (pairs, 1): targets only (every source is
-    // ordered by src_order_kernel — launched alone, the targets spread over every CU)
-    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-    const int p = gridDim.y == 2 ? g >> 1 : g;
-    const bool is_tgt = gridDim.y == 2 ? (g & 1) == 0 : true;
+// One cloud's index (the target or the source of pair p) by one workgroup: index_kernel, and the
+// source column of index_refine_kernel when the target's Morton sort is multi-workgroup (w.mo_hist).
+__device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a, const WorkArgs& w, int p, bool is_tgt) {
     if (w.state[p].phase == kPhaseInvalid) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = is_tgt ? a.tgt_n[p] : a.src_n[p];
@@ -874,6 +870,7 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
 #endif
         return;
     }
+    if (is_tgt && w.mo_hist) return;  // index_mo_hist_kernel / index_mo_scatter_kernel sort it
     uint32_t* bins = shu.mo.bins;
     float(*red)[6] = shu.mo.red;
     uint32_t* wsum = shu.mo.wsum;
@@ -973,6 +970,140 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
             const uint32_t pos = atomicAdd(&bins[cell_code(v.x, v.y, v.z, lo, sc)], 1u);
             sp[pos] = i;
         });
+    }
+}
+
+__global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
+    __shared__ IndexShared shu;
+    // grid (pairs, 2): target and source of every pair; (pairs, 1): targets only (every source is
+    // ordered by src_order_kernel — launched alone, the targets spread over every CU)
+    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int p = gridDim.y == 2 ? g >> 1 : g;
+    const bool is_tgt = gridDim.y == 2 ? (g & 1) == 0 : true;
+    index_cloud(shu, a, w, p, is_tgt);
+}
+
+// Multi-workgroup Morton sort of a large target (the C5 submap: 65k points), for few pairs: the
+// one-workgroup sort above spends ~125 us of a single registration in its three sweeps over the
+// cloud.  Workgroup g of pair p owns points [g * kMoChunk, (g + 1) * kMoChunk): one sweep, 16 points
+// per thread in flight.  index_mo_hist_kernel writes each workgroup's cell histogram (row p * G + g
+// of w.mo_hist); index_mo_scatter_kernel gives every workgroup the exclusive prefix over (cell,
+// workgroup) — the cells of all rows before its cell, plus its cell in the rows before its own —
+// and scatters its points there.  The quantisation (w.tbb, from init_kernel) is the one-workgroup
+// sort's.  Only for plans whose index_refine_kernel re-orders every chunk afterwards (it writes tinv
+// and the boxes of every real block); the scatter writes the padding and the empty tail's boxes.
+constexpr int kMoChunk = kIdxWG * 16;
+
+__device__ __forceinline__ void mo_quant(const WorkArgs& w, int p, float* lo, float* sc) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float l = w.tbb[(int64_t)p * 8 + k], h = w.tbb[(int64_t)p * 8 + 3 + k];
+        lo[k] = l;
+        sc[k] = h > l ? (k == 2 ? 16.0f : 32.0f) / (h - l) : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(kIdxWG) void index_mo_hist_kernel(PairArgs a, WorkArgs w) {
+    __shared__ uint32_t bins[kCellBins];
+    const int g = blockIdx.x, p = blockIdx.y, tid = threadIdx.x;
+    const int m = a.tgt_n[p];
+    if (w.state[p].phase == kPhaseInvalid || m <= 0 || g * kMoChunk >= m) return;
+    const float4* pts = a.tgt + a.tgt_off[p];
+    float lo[3], sc[3];
+    mo_quant(w, p, lo, sc);
+    for (int b = tid; b < kCellBins; b += kIdxWG) bins[b] = 0;
+    const int i0 = g * kMoChunk;
+    float4 v[kMoChunk / kIdxWG];
+#pragma unroll
+    for (int e = 0; e < kMoChunk / kIdxWG; ++e) v[e] = pts[min(i0 + e * kIdxWG + tid, m - 1)];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kMoChunk / kIdxWG; ++e)
+        if (i0 + e * kIdxWG + tid < m) atomicAdd(&bins[cell_code(v[e].x, v[e].y, v[e].z, lo, sc)], 1u);
+    __syncthreads();
+    uint4* row = reinterpret_cast<uint4*>(w.mo_hist + ((int64_t)p * w.mo_groups + g) * kCellBins);
+    const uint4* b4 = reinterpret_cast<const uint4*>(bins);
+    for (int k = tid; k < kCellBins / 4; k += kIdxWG) row[k] = b4[k];
+}
+
+__global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, WorkArgs w) {
+    __shared__ uint32_t bins[kCellBins];
+    __shared__ uint32_t wsum[kIdxWaves];
+    const int g = blockIdx.x, p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = a.tgt_n[p];
+    if (w.state[p].phase == kPhaseInvalid || m <= 0 || g * kMoChunk >= m) return;
+    const int ng = (m + kMoChunk - 1) / kMoChunk;  // rows of this pair
+    const float4* pts = a.tgt + a.tgt_off[p];
+    const int i0 = g * kMoChunk;
+    float4 v[kMoChunk / kIdxWG];  // this workgroup's points, in flight while the prefix is formed
+#pragma unroll
+    for (int e = 0; e < kMoChunk / kIdxWG; ++e) v[e] = pts[min(i0 + e * kIdxWG + tid, m - 1)];
+    // thread t owns cells [per * t, per * (t + 1)): per cell its count over every row (tot) and over the
+    // rows before g (bef), four cells per 16-B read
+    constexpr int per = kCellBins / kIdxWG;
+    static_assert(per % 4 == 0, "whole 16-B reads of the rows");
+    uint32_t tot[per], bef[per];
+#pragma unroll
+    for (int k = 0; k < per; ++k) tot[k] = bef[k] = 0u;
+    const uint32_t* rows = w.mo_hist + (int64_t)p * w.mo_groups * kCellBins + tid * per;
+    for (int r = 0; r < ng; ++r) {
+        const uint4* rr = reinterpret_cast<const uint4*>(rows + (int64_t)r * kCellBins);
+        const uint32_t into_bef = r < g ? 1u : 0u;
+#pragma unroll
+        for (int q = 0; q < per / 4; ++q) {
+            const uint4 c = rr[q];
+            tot[4 * q] += c.x; tot[4 * q + 1] += c.y; tot[4 * q + 2] += c.z; tot[4 * q + 3] += c.w;
+            bef[4 * q] += into_bef * c.x; bef[4 * q + 1] += into_bef * c.y;
+            bef[4 * q + 2] += into_bef * c.z; bef[4 * q + 3] += into_bef * c.w;
+        }
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) {  // bef[k] := exclusive prefix of cell k inside the thread + its rows before g
+        const uint32_t t = tot[k];
+        bef[k] += run;
+        run += t;
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t tbase = incl - run;
+    for (int q = 0; q < wave; ++q) tbase += wsum[q];
+#pragma unroll
+    for (int k = 0; k < per; ++k) bins[tid * per + k] = tbase + bef[k];
+    __syncthreads();
+    float lo[3], sc[3];
+    mo_quant(w, p, lo, sc);
+    float4* ts = w.tsort + (int64_t)p * w.t_stride;
+#pragma unroll
+    for (int e = 0; e < kMoChunk / kIdxWG; ++e) {
+        const int i = i0 + e * kIdxWG + tid;
+        if (i < m) {
+            const uint32_t pos = atomicAdd(&bins[cell_code(v[e].x, v[e].y, v[e].z, lo, sc)], 1u);
+            ts[pos] = make_float4(v[e].x, v[e].y, v[e].z, __uint_as_float((uint32_t)i));
+        }
+    }
+    if (g != ng - 1) return;
+    // the tail: padding (+inf coordinates, .w = a real index: never a match) and the boxes of the
+    // blocks and superblocks past the last real block (index_refine_kernel writes the real ones)
+    for (int64_t pos = m + tid; pos < w.t_stride; pos += kIdxWG)
+        ts[pos] = make_float4(INFINITY, INFINITY, INFINITY, __uint_as_float((uint32_t)(m - 1)));
+    const int nb = (m + w.leaf - 1) / w.leaf, nsb = (nb + kSuper - 1) / kSuper;
+    const float4 el = make_float4(INFINITY, INFINITY, INFINITY, 0.f), eh = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    float4* tb = w.tbox + (int64_t)p * 2 * w.b_stride;
+    for (int64_t b = nb + tid; b < w.b_stride; b += kIdxWG) {
+        tb[2 * b] = el;
+        tb[2 * b + 1] = eh;
+    }
+    float4* sbx = w.sbox + (int64_t)p * 2 * w.sb_stride;
+    for (int64_t s = nsb + tid; s < w.sb_stride; s += kIdxWG) {
+        sbx[2 * s] = el;
+        sbx[2 * s + 1] = eh;
     }
 }
 
@@ -1171,6 +1302,10 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
 __global__ __launch_bounds__(kIdxWG, 4) void index_refine_kernel(PairArgs a, WorkArgs w) {
     __shared__ IndexShared shu;
     const int c = blockIdx.x, p = blockIdx.y;
+    if (w.mo_hist && c == (int)gridDim.x - 1) {  // (multi-workgroup Morton sort: no index_kernel launch)
+        index_cloud(shu, a, w, p, false);         // the last column builds the pair's source index
+        return;
+    }
     if (w.state[p].phase == kPhaseInvalid) return;
     const int m = a.tgt_n[p];
     if (m <= 0 || (m <= kKdMaxN && w.t_stride <= kKdMaxN)) return;  // index_kernel's kd path did it
@@ -4087,12 +4222,22 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
     // every source by the target's tree: launch the target builds alone (a grid with idle source
     // workgroups left half the CUs without a build)
     const bool tgt_only = w.src_by_tgt && w.kdn && (w.kd_index & 1) && w.t_stride <= kKdMaxN && w.x_stride <= kKdMaxN;
+    const unsigned nch = (unsigned)((w.t_stride + kKdMaxN - 1) / kKdMaxN);
+    if (w.mo_hist) {  // (setup_work sets it only for plans that refine: see index_mo_hist_kernel)
+        if (!(w.tbb && (w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32) &&
+              (int64_t)w.mo_groups * kMoChunk >= w.t_stride))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(index_mo_hist_kernel, dim3(w.mo_groups, npairs), dim3(kIdxWG), 0, st, a, w);
+        hipLaunchKernelGGL(index_mo_scatter_kernel, dim3(w.mo_groups, npairs), dim3(kIdxWG), 0, st, a, w);
+        // (no src_order_kernel: a target past kKdMaxN has no kd tree for its source to descend)
+        hipLaunchKernelGGL(index_refine_kernel, dim3(nch + 1, npairs), dim3(kIdxWG), 0, st, a, w);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(index_kernel, dim3(npairs, tgt_only ? 1 : 2), dim3(kIdxWG), 0, st, a, w);
     if (w.src_by_tgt && w.kdn)
         hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);
     if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))
-        hipLaunchKernelGGL(index_refine_kernel, dim3((unsigned)((w.t_stride + kKdMaxN - 1) / kKdMaxN), npairs),
-                           dim3(kIdxWG), 0, st, a, w);
+        hipLaunchKernelGGL(index_refine_kernel, dim3(nch, npairs), dim3(kIdxWG), 0, st, a, w);
     return hipGetLastError();
 }
 

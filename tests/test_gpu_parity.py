@@ -608,3 +608,37 @@ def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
     assert r.fitness == o["fitness"]
     assert r.n_correspondences == o["n_correspondences"]
     assert (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("npairs", [1, 5])
+def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypatch):
+    """Targets too large for the in-LDS kd build (the C5 submap class): their Morton sort on one
+    workgroup per 8192-point chunk (index_mo_hist_kernel / index_mo_scatter_kernel, the default for
+    few pairs) or on one workgroup per target (ICP4R_MORTON_MWG=0) — the order changes, the
+    registrations do not: bit-identical, ragged targets (8193 .. 40000 points, a partial last chunk,
+    a lattice with ties, a small target in the same batch), and bit-equal to the oracle."""
+    import icp4r
+
+    rng = np.random.default_rng(11)
+    if npairs == 1:
+        pairs = [_pair(2100, 4096, 30001)]
+    else:
+        lat = _lattice(rng, 22)  # 22^3 = 10648 points: ties everywhere
+        ls = lat[rng.permutation(len(lat))[:3000]].copy()
+        ls[:, :3] += np.float32(0.25)
+        pairs = [_pair(2100 + k, n, m) for k, (n, m) in enumerate([(4096, 8193), (1000, 40000), (2048, 600),
+                                                                     (8192, 16384)])] + [(ls, lat)]
+    args = _batch(pairs)
+    p = icp4r.default_params(max_iterations=12)
+    out = {}
+    for mwg in ("0", "1"):
+        monkeypatch.setenv("ICP4R_MORTON_MWG", mwg)
+        out[mwg] = gpu_ctx.align_batch_host(*args, params=p)
+    assert out["0"].tobytes() == out["1"].tobytes()
+    assert (out["1"]["status"] == 0).all()
+    for k in (0, len(pairs) - 1):
+        s, t = pairs[k]
+        o = oracle_mod.align(s, t, numerics=oracle_mod.NUM_F32, max_iterations=12)
+        T = out["1"]["T"][k].reshape(4, 4).T
+        assert (T == o["T"]).all()
+        assert out["1"]["iterations"][k] == o["iterations"]
