@@ -295,8 +295,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         const int64_t mog = (w.t_stride + kChunk - 1) / kChunk;
         if ((w.kd_index & 1) && w.t_stride > kChunk && (pl.leaf == 16 || pl.leaf == 32) &&
             npairs * mog <= 2048 && env_int("ICP4R_MORTON_MWG", 1)) {
-            HIP_TRY(ctx->mo_hist.ensure((size_t)npairs * mog * (1u << 14) * sizeof(uint32_t)));
-            w.mo_hist = static_cast<uint32_t*>(ctx->mo_hist.p);
+            HIP_TRY(ctx->mo_hist.ensure((size_t)npairs * mog * (1u << 14) * sizeof(uint16_t)));
+            w.mo_hist = static_cast<uint16_t*>(ctx->mo_hist.p);
             w.mo_groups = (int32_t)mog;
         }
         if (pl.solo) {  // the query list and the cached-neighbour state (solo_kernel)

@@ -121,7 +121,7 @@ struct WorkArgs {
                           // (qv / qm, sorted order) itself; 0: the first pass' nn_key seeds
     float* tbb;         // [npairs * 8] the target's bounding box (lo xyz, hi xyz), from init_kernel's
                         // validation pass (the Morton index skips its own pass over the cloud); or nullptr
-    uint32_t* mo_hist;  // [npairs * mo_groups * 2^14] per-workgroup Morton cell counts of a large target
+    uint16_t* mo_hist;  // [npairs * mo_groups * 2^14] per-workgroup Morton cell counts (u16) of a large target
                         // (multi-workgroup sort, index_mo_hist_kernel); nullptr: one workgroup per target
     int32_t mo_groups;  // workgroups per target of that sort (>= t_stride / 8192)
     uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,

@@ -1021,9 +1021,14 @@ __global__ __launch_bounds__(kIdxWG) void index_mo_hist_kernel(PairArgs a, WorkA
     for (int e = 0; e < kMoChunk / kIdxWG; ++e)
         if (i0 + e * kIdxWG + tid < m) atomicAdd(&bins[cell_code(v[e].x, v[e].y, v[e].z, lo, sc)], 1u);
     __syncthreads();
+    // the row as u16 counts (a workgroup's cell holds at most kMoChunk points), 8 cells per 16-B store
+    static_assert(kMoChunk < 65536, "u16 cell counts");
     uint4* row = reinterpret_cast<uint4*>(w.mo_hist + ((int64_t)p * w.mo_groups + g) * kCellBins);
     const uint4* b4 = reinterpret_cast<const uint4*>(bins);
-    for (int k = tid; k < kCellBins / 4; k += kIdxWG) row[k] = b4[k];
+    for (int k = tid; k < kCellBins / 8; k += kIdxWG) {
+        const uint4 lo4 = b4[2 * k], hi4 = b4[2 * k + 1];
+        row[k] = make_uint4(lo4.x | lo4.y << 16, lo4.z | lo4.w << 16, hi4.x | hi4.y << 16, hi4.z | hi4.w << 16);
+    }
 }
 
 __global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, WorkArgs w) {
@@ -1039,22 +1044,36 @@ __global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, Wo
 #pragma unroll
     for (int e = 0; e < kMoChunk / kIdxWG; ++e) v[e] = pts[min(i0 + e * kIdxWG + tid, m - 1)];
     // thread t owns cells [per * t, per * (t + 1)): per cell its count over every row (tot) and over the
-    // rows before g (bef), four cells per 16-B read
+    // rows before g (bef); u16 counts, eight cells per 16-B read, kMoRows rows' reads in flight at once
+    // (a row at a time had waited out one L2 round trip per row: ~15 us of a 65k-point sort)
     constexpr int per = kCellBins / kIdxWG;
-    static_assert(per % 4 == 0, "whole 16-B reads of the rows");
+    constexpr int kMoRows = 3;
+    static_assert(per % 8 == 0, "whole 16-B reads of the rows");
     uint32_t tot[per], bef[per];
 #pragma unroll
     for (int k = 0; k < per; ++k) tot[k] = bef[k] = 0u;
-    const uint32_t* rows = w.mo_hist + (int64_t)p * w.mo_groups * kCellBins + tid * per;
-    for (int r = 0; r < ng; ++r) {
-        const uint4* rr = reinterpret_cast<const uint4*>(rows + (int64_t)r * kCellBins);
-        const uint32_t into_bef = r < g ? 1u : 0u;
+    const uint16_t* rows = w.mo_hist + (int64_t)p * w.mo_groups * kCellBins + tid * per;
+    for (int r0 = 0; r0 < ng; r0 += kMoRows) {
+        uint4 c[kMoRows][per / 8];
 #pragma unroll
-        for (int q = 0; q < per / 4; ++q) {
-            const uint4 c = rr[q];
-            tot[4 * q] += c.x; tot[4 * q + 1] += c.y; tot[4 * q + 2] += c.z; tot[4 * q + 3] += c.w;
-            bef[4 * q] += into_bef * c.x; bef[4 * q + 1] += into_bef * c.y;
-            bef[4 * q + 2] += into_bef * c.z; bef[4 * q + 3] += into_bef * c.w;
+        for (int j = 0; j < kMoRows; ++j) {
+            const uint4* rr = reinterpret_cast<const uint4*>(rows + (int64_t)min(r0 + j, ng - 1) * kCellBins);
+#pragma unroll
+            for (int q = 0; q < per / 8; ++q) c[j][q] = rr[q];
+        }
+#pragma unroll
+        for (int j = 0; j < kMoRows; ++j) {
+            const uint32_t use = r0 + j < ng ? 0xffffffffu : 0u, into_bef = r0 + j < g ? 0xffffffffu : 0u;
+#pragma unroll
+            for (int q = 0; q < per / 8; ++q) {
+                const uint32_t u[4] = {c[j][q].x & use, c[j][q].y & use, c[j][q].z & use, c[j][q].w & use};
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    const uint32_t cnt = (u[h >> 1] >> (16 * (h & 1))) & 0xffffu;
+                    tot[8 * q + h] += cnt;
+                    bef[8 * q + h] += cnt & into_bef;
+                }
+            }
         }
     }
     uint32_t run = 0;
@@ -3781,10 +3800,102 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
     // exact integer reduction.  Bit-identical to the reference loop.
     __shared__ double chunk[2][kFoldChunkP];  // (doubles: the fold lane only adds, fold_seq_d)
     __shared__ int32_t fcnt_w[kFinWG / 64];
+    __shared__ uint64_t fsum_w[kFinWG / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     double fsum = 0.0;
     int fcnt = 0;
-    if (have) {
+    // Exact parallel form of the same sum.  Every term is a float widened to double, so every term is
+    // an integer multiple of 2^e, e = the lowest set bit's exponent over the nonzero terms.  When the
+    // exact total S is below 2^(e + 53), every partial sum of the non-negative terms is a multiple of
+    // 2^e below 2^(e + 53), i.e. a double: the sequential loop never rounds and returns S itself.  S is
+    // then an integer sum in units of 2^e (associative), saturated at 2^53; otherwise (a span of more
+    // than 53 bits between the smallest term's last bit and the total) the sequential fold below runs.
+    // Batches of at least kFinExactMaxPairs pairs keep the sequential fold only: their chains overlap
+    // across the pairs, and the exact attempt measured slower there (C3: 43 -> 63 us per batch; a
+    // pair whose span test fails pays both forms).
+    constexpr int kFinExactMaxPairs = 256;
+    bool exact = false;
+    if (have && (int)gridDim.x < kFinExactMaxPairs) {
+        constexpr uint64_t kSat = 1ull << 53;
+        // the values: in registers for clouds of at most kFinWG * kFinPer points (every load in flight
+        // at once, one read of the keys), else re-read per pass; NaN = no point (never in range)
+        constexpr int kFinPer = 32;
+        const bool reg = n <= kFinWG * kFinPer;
+        float v[kFinPer];
+        if (reg) {
+#pragma unroll
+            for (int k = 0; k < kFinPer; ++k) {
+                const int i = threadIdx.x + k * kFinWG;
+                v[k] = i < n ? key_d2(w.nn_key[slot0 + i]) : __int_as_float(0x7fc00000);
+            }
+        }
+        auto each = [&](auto&& f) {
+            if (reg) {
+#pragma unroll
+                for (int k = 0; k < kFinPer; ++k) f(v[k]);
+            } else {
+                for (int i = threadIdx.x; i < n; i += kFinWG) f(key_d2(w.nn_key[slot0 + i]));
+            }
+        };
+        int emin = INT_MAX;
+        each([&](float d2) {
+            const double x = (double)d2;
+            if (x <= a.kp.fit_max_range) {
+                ++fcnt;
+                if (x > 0.0) {
+                    const uint64_t b = (uint64_t)__double_as_longlong(x);
+                    const int ex = (int)((b >> 52) & 0x7ff);
+                    const uint64_t mant = (b & ((1ull << 52) - 1)) | (1ull << 52);
+                    emin = min(emin, ex - 1075 + (int)__builtin_ctzll(mant));
+                }
+            }
+        });
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            emin = min(emin, __shfl_xor(emin, off, 64));
+            fcnt += __shfl_xor(fcnt, off, 64);
+        }
+        if (lane == 0) {
+            fcnt_w[wave] = fcnt;
+            fsum_w[wave] = (uint64_t)(uint32_t)emin;
+        }
+        __syncthreads();
+        fcnt = 0;
+        emin = INT_MAX;
+        for (int k = 0; k < kFinWG / 64; ++k) {
+            fcnt += fcnt_w[k];
+            emin = min(emin, (int)(uint32_t)fsum_w[k]);
+        }
+        __syncthreads();  // (fsum_w reused below)
+        uint64_t S = 0;
+        if (emin != INT_MAX) {
+            each([&](float d2) {
+                const double x = (double)d2;
+                if (x <= a.kp.fit_max_range && x > 0.0) {
+                    const uint64_t b = (uint64_t)__double_as_longlong(x);
+                    const int ex = (int)((b >> 52) & 0x7ff);
+                    const uint64_t mant = (b & ((1ull << 52) - 1)) | (1ull << 52);
+                    // x = mant * 2^(ex - 1075); below 2^(emin + 53) iff ex - 1023 - emin <= 52, and then
+                    // x / 2^emin = mant >> (emin + 1075 - ex), a shift by at most ctz(mant): exact
+                    const uint64_t t = (ex - 1023 - emin <= 52) ? (mant >> (emin + 1075 - ex)) : kSat;
+                    S = min(S + t, kSat);
+                }
+            });
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) S = min(S + __shfl_xor(S, off, 64), kSat);
+            if (lane == 0) fsum_w[wave] = S;
+            __syncthreads();
+            S = 0;
+            for (int k = 0; k < kFinWG / 64; ++k) S = min(S + fsum_w[k], kSat);
+        }
+        if (S < kSat) {
+            exact = true;
+            fsum = emin == INT_MAX ? 0.0 : ldexp((double)S, emin);
+        }
+    }
+    if (have && !exact) {
+        fcnt = 0;
+        __syncthreads();  // (fcnt_w reused)
         const int nch = (n + kFoldChunkP - 1) / kFoldChunkP;
         auto fill = [&](int c) {
             const int base = c * kFoldChunkP, len = min(kFoldChunkP, n - base);

@@ -642,3 +642,27 @@ def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypat
         T = out["1"]["T"][k].reshape(4, 4).T
         assert (T == o["T"]).all()
         assert out["1"]["iterations"][k] == o["iterations"]
+
+
+def test_fitness_exact_and_sequential_forms(gpu_ctx, oracle_mod):
+    """finish_kernel's fitness sum: the exact integer form (terms within 53 bits of the total) and the
+    sequential fold it falls back to (a term whose last bit lies more than 53 bits below the total: a
+    point 1e-15 off its target, d² = 1e-30), an all-zero sum (the source on the target), a single
+    point, far points beyond max_range, and a source over 8192 points (keys re-read, not in registers) — every case bit-equal to the oracle's sequential loop."""
+    s, t = _pair(601, 4096)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [0.05, -0.02, 0.01]
+    tiny_t = t.copy()
+    tiny_t[7, :3] = [1e-15, 0.0, 0.0]
+    tiny_s = s.copy()
+    tiny_s[3, :3] = [0.0, 0.0, 0.0]
+    wide = s.copy()
+    wide[::97, :3] *= np.float32(1000.0)  # a few distant points: large terms beside the small ones
+    bs, bt = _pair(602, 9000, 3000)  # over 8192 sources: the keys re-read per pass, not held in registers
+    cases = [(s, t, T), (tiny_s, tiny_t, np.eye(4, dtype=np.float32)), (t.copy(), t, np.eye(4, dtype=np.float32)),
+             (s[:1].copy(), t, T), (wide, t, T), (bs, bt, T)]
+    for k, (cs, ct, cT) in enumerate(cases):
+        for mr in (np.finfo(np.float64).max, 0.5, 1e-3):
+            g = gpu_ctx.fitness(cs, ct, cT, mr)
+            o = oracle_mod.fitness(cs, ct, cT, mr)
+            assert g == o, (k, mr, g, o)
