@@ -3368,6 +3368,40 @@ struct FoldIn {
     int n;
 };
 
+// A running exact sum of non-negative doubles that are widened floats: S in units of 2^E (E = the
+// lowest set bit's exponent over the nonzero terms so far), saturated at 2^53 — the argument of
+// finish_kernel: while S < 2^53 the sequential double loop over the same terms never rounds, so its
+// result is S * 2^E.  Each lane keeps its own (S, E) over the terms it is handed (no cross-lane step
+// per chunk: the per-chunk wave reductions had cost as much as the float chains beside them);
+// wave_exact_total combines the lanes (a lane's saturation means the whole total reaches 2^53).
+constexpr uint64_t kExactSat = 1ull << 53;
+__device__ __forceinline__ uint64_t exact_rescale(uint64_t S, int sh) {  // S * 2^sh, saturated (sh >= 0)
+    return S == 0 ? 0 : ((sh >= 53 || (S >> (53 - sh)) != 0) ? kExactSat : (S << sh));
+}
+__device__ __forceinline__ void lane_exact_add(double x, uint64_t& S, int& E) {
+    if (!(x > 0.0)) return;
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int ex = (int)((b >> 52) & 0x7ff);
+    const uint64_t mant = (b & ((1ull << 52) - 1)) | (1ull << 52);
+    const int lo = ex - 1075 + (int)__builtin_ctzll(mant);
+    if (lo < E) {  // re-express S in the finer unit (exact while it stays below 2^53)
+        S = E == INT_MAX ? 0 : exact_rescale(S, E - lo);
+        E = lo;
+    }
+    // x / 2^E = mant >> (E + 1075 - ex), a shift by at most ctz(mant): exact; below 2^53 iff ex - 1023 - E <= 52
+    S = min(S + ((ex - 1023 - E <= 52) ? (mant >> (E + 1075 - ex)) : kExactSat), kExactSat);
+}
+__device__ __forceinline__ void wave_exact_total(uint64_t& S, int& E) {  // every lane ends with the wave's
+    int e = E;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) e = min(e, __shfl_xor(e, off, 64));
+    uint64_t t = E == INT_MAX ? 0 : exact_rescale(S, E - e);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t = min(t + __shfl_xor(t, off, 64), kExactSat);
+    S = t;
+    E = e;
+}
+
 // Pass A of the PCL-numerics update by a workgroup of WG threads over LDS chunks of CH points
 // (buf: two chunks of 9 rows of ROW floats): wave 0 lanes 0..6 fold Σs, Σd (Eigen 3.3
 // rowwise().sum(): from the first element == from -0.0f; Huber: w·x from +0) and Σw; wave 1 lane 0
@@ -3450,11 +3484,18 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
             __syncthreads();
             if (lane < 7) acc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), acc);
         }
-    } else if (wv * 64 < fill0) {  // the MSE chain
+    } else if (wv * 64 < fill0) {  // the MSE sum: its exact form, the whole wave per chunk
+        uint64_t xs = 0;
+        int xe = INT_MAX;
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane == 0) dacc = fold_seq_d(reinterpret_cast<const double*>(buf[c & 1][7]), min(CH, n - c * CH), dacc);
+            const double* dv = reinterpret_cast<const double*>(buf[c & 1][7]);
+            const int len = min(CH, n - c * CH);
+            for (int o = lane; o < len; o += 64) lane_exact_add(dv[o], xs, xe);
         }
+        wave_exact_total(xs, xe);
+        // -1: the span test failed (the sequential chain runs below)
+        dacc = xs >= kExactSat ? -1.0 : (xe == INT_MAX ? 0.0 : ldexp((double)xs, xe));
     } else {
         if (nch > 0) {
             float4 r[kPerA][2];
@@ -3487,6 +3528,34 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
         for (int k = 0; k < 6; ++k) s.mean[k] = res[k] * one_over_n;
     }
     __syncthreads();
+    if (mse && s.mse_sum < 0.0) {  // (uniform) the MSE terms span more than 53 bits: PCL's sequential
+        dacc = 0.0;                 // double chain, over the chunks staged again (wave 0 idles)
+        if (wv == 0) {
+            for (int c = 0; c < nch; ++c) __syncthreads();
+        } else if (wv * 64 < fill0) {
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (lane == 0) dacc = fold_seq_d(reinterpret_cast<const double*>(buf[c & 1][7]), min(CH, n - c * CH), dacc);
+            }
+        } else {
+            if (nch > 0) {
+                float4 r[kPerA][2];
+                load_a(0, r);
+                store_a(0, r);
+            }
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (c + 1 < nch) {
+                    float4 r[kPerA][2];
+                    load_a(c + 1, r);
+                    store_a(c + 1, r);
+                }
+            }
+        }
+        __syncthreads();  // (the last chunk folded before s.mse_sum is rewritten)
+        if (wave == 1 && lane == 0) s.mse_sum = dacc;
+        __syncthreads();
+    }
 }
 
 // Pass B: the fillers form the 9 products d'_a·s'_b (Huber: (w·d'_a)·s'_b) over the float-demeaned

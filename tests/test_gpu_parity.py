@@ -666,3 +666,30 @@ def test_fitness_exact_and_sequential_forms(gpu_ctx, oracle_mod):
             g = gpu_ctx.fitness(cs, ct, cT, mr)
             o = oracle_mod.fitness(cs, ct, cT, mr)
             assert g == o, (k, mr, g, o)
+
+
+@pytest.mark.parametrize("n", [700, 2048, 8192])
+@pytest.mark.parametrize("tiny", [False, True])
+def test_mse_exact_and_sequential_forms(gpu_ctx, oracle_mod, n, tiny):
+    """Pass A's MSE sum under PCL's default criteria (live): its exact parallel form, and the sequential
+    chain it falls back to when the terms span more than 53 bits (tiny: a source point 1e-15 off a
+    target, d² = 1e-30 in the first iteration) — single pairs (solo_kernel at 700 sources, the
+    multi-launch update above) and a batch; T, iterations, convergence state and fitness bit-equal
+    to the oracle."""
+    import icp4r
+
+    s, t = _pair(610 + n, n)
+    if tiny:
+        t = t.copy()
+        s = s.copy()
+        t[5, :3] = [1e-15, 0.0, 0.0]
+        s[9, :3] = [0.0, 0.0, 0.0]
+    p = icp4r.default_params()
+    o = oracle_mod.align(s, t, numerics=oracle_mod.NUM_F32)
+    r, _ = gpu_ctx.align(s, t, p)
+    assert r.status == 0 and r.iterations == o["iterations"]
+    assert r.convergence_state == o["convergence_state"]
+    assert (r.matrix() == o["T"]).all()
+    assert r.fitness == o["fitness"]
+    res = gpu_ctx.align_batch_host(*_batch([(s, t), _pair(620, 3000)]), params=p)
+    assert (res[0]["T"] == np.array(r.T, np.float32)).all() and res[0]["iterations"] == r.iterations
