@@ -298,6 +298,8 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             HIP_TRY(ctx->mo_hist.ensure((size_t)npairs * mog * (1u << 14) * sizeof(uint16_t)));
             w.mo_hist = static_cast<uint16_t*>(ctx->mo_hist.p);
             w.mo_groups = (int32_t)mog;
+            HIP_TRY(ctx->mo_rep.ensure((size_t)npairs * (1u << 14) * sizeof(int32_t)));
+            w.mo_rep = static_cast<int32_t*>(ctx->mo_rep.p);
         }
         if (pl.solo) {  // the query list and the cached-neighbour state (solo_kernel)
             HIP_TRY(ctx->qv.ensure((size_t)slots * sizeof(float4)));
@@ -437,6 +439,7 @@ void group_view(const PairArgs& a, const WorkArgs& w, int p0, int g, PairArgs& a
         if (wg.kdn) wg.kdn += (int64_t)p0 * kKdnStride;
         if (wg.tbb) wg.tbb += (int64_t)p0 * 8;
         if (wg.mo_hist) wg.mo_hist += (int64_t)p0 * w.mo_groups * (1 << 14);
+        if (wg.mo_rep) wg.mo_rep += (int64_t)p0 * (1 << 14);
     }
     if (wg.nn_u) {
         wg.nn_u += xs;

@@ -61,6 +61,7 @@ int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, c
         WorkArgs wi = w;
         wi.tbb = nullptr;
         wi.mo_hist = nullptr;
+        wi.mo_rep = nullptr;
         HIP_TRY(launch_index(ai, wi, npairs, st));
         HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, w, npairs, max_n, stride, k, reg, out, st));
     } else {

@@ -68,7 +68,7 @@ struct icp4r_ctx {
     icp4r_host::DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace
     icp4r_host::DevBuf X, nn_key, state, tsort, tinv, tbox, sbox, sperm, corr, ticks, nn_lu, nn_t, kdn, sq, sm, qv, qm, need,
-        miss_cnt, plist, plist_n, owork, mo_hist;  // nn_lu holds U (float) per source point
+        miss_cnt, plist, plist_n, owork, mo_hist, mo_rep;  // nn_lu holds U (float) per source point
     int ncu = 256;  // compute units of the device (persistent launches)
     bool kernel_timing = false;  // per-kernel events (icp4r_set_kernel_timing)
     // HIP events on the launch stream: the dominant NN kernel (the batched search, or the whole NN

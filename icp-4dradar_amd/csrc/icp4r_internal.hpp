@@ -124,6 +124,8 @@ struct WorkArgs {
     uint16_t* mo_hist;  // [npairs * mo_groups * 2^14] per-workgroup Morton cell counts (u16) of a large target
                         // (multi-workgroup sort, index_mo_hist_kernel); nullptr: one workgroup per target
     int32_t mo_groups;  // workgroups per target of that sort (>= t_stride / 8192)
+    int32_t* mo_rep;    // [npairs * 2^14] per Morton cell: the original index of one of its targets, -1: empty
+                        // (written by that sort; nn_seed_kernel's first-pass seed: a target in the query's cell)
     uint32_t* kdn;      // [npairs * kKdnStride] the target kd tree: [0, 6) quantisation lo / scale bits,
                         // [8 + node] internal node (heap order) = 1 << 31 | mid << 13 | axis << 11 | key
     // Pruned-search index, built once per registration by index_kernel (SURVEY.md §8f "sorted map"):

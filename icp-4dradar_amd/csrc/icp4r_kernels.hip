@@ -1093,8 +1093,12 @@ __global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, Wo
     __syncthreads();
     uint32_t tbase = incl - run;
     for (int q = 0; q < wave; ++q) tbase += wsum[q];
+    int32_t* rep = w.mo_rep ? w.mo_rep + (int64_t)p * kCellBins : nullptr;
 #pragma unroll
-    for (int k = 0; k < per; ++k) bins[tid * per + k] = tbase + bef[k];
+    for (int k = 0; k < per; ++k) {
+        bins[tid * per + k] = tbase + bef[k];
+        if (rep && g == 0 && tot[k] == 0) rep[tid * per + k] = -1;  // (the others: a point's index, below)
+    }
     __syncthreads();
     float lo[3], sc[3];
     mo_quant(w, p, lo, sc);
@@ -1103,8 +1107,10 @@ __global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, Wo
     for (int e = 0; e < kMoChunk / kIdxWG; ++e) {
         const int i = i0 + e * kIdxWG + tid;
         if (i < m) {
-            const uint32_t pos = atomicAdd(&bins[cell_code(v[e].x, v[e].y, v[e].z, lo, sc)], 1u);
+            const uint32_t cell = cell_code(v[e].x, v[e].y, v[e].z, lo, sc);
+            const uint32_t pos = atomicAdd(&bins[cell], 1u);
             ts[pos] = make_float4(v[e].x, v[e].y, v[e].z, __uint_as_float((uint32_t)i));
+            if (rep) rep[cell] = i;  // (any of the cell's points: the last store wins)
         }
     }
     if (g != ng - 1) return;
@@ -1467,8 +1473,18 @@ __global__ __launch_bounds__(256) void nn_seed_kernel(PairArgs a, WorkArgs w, in
     NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
     const NNKey k0 = key[o];
     const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
-    const uint32_t j = (first && !seed_key(k0, m)) ? __float_as_uint(tsg[((int64_t)s * m) / n].w)
-                                                   : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+    uint32_t j;
+    if (first && !seed_key(k0, m)) {
+        j = __float_as_uint(tsg[((int64_t)s * m) / n].w);
+        if (w.mo_rep) {  // a multi-workgroup Morton target: a target in the query's own cell, if any
+            float lo[3], sc[3];
+            mo_quant(w, p, lo, sc);
+            const int32_t r = w.mo_rep[(int64_t)p * kCellBins + cell_code(v.x, v.y, v.z, lo, sc)];
+            if (r >= 0 && r < m) j = (uint32_t)r;
+        }
+    } else {
+        j = min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+    }
     const float4 t = a.tgt[uload(a.tgt_off + p) + j];
     key[o] = make_key(l2_simple(v.x, v.y, v.z, t.x, t.y, t.z), j);
 }
