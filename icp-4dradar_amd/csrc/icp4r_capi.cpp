@@ -168,7 +168,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
             // misses costs more than the multi-launch plan's boundaries since its search spreads over
             // the CUs in runs of 16 — C1's 2k pair 0.55 ms solo vs 0.50 multi at PCL's 10 iterations;
             // solo stays ahead on long fixed runs up to 3k sources, 0.78 vs 0.81 ms at 20 — see
-            // tools/solo_sweep.py, profiles/round3/s4/solo_sweep_r16.jsonl; ICP4R_SOLO=1 forces it up to
+            // tools/experiments/solo_sweep.py, profiles/round3/s4/solo_sweep_r16.jsonl; ICP4R_SOLO=1 forces it up to
             // kCacheMaxN, 0 disables it)
             const int solo_env = env_int("ICP4R_SOLO", -1);
             pl.solo = registration && pl.tile && pl.chunks == 1 && solo_env != 0 &&

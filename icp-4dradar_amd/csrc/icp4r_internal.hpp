@@ -167,7 +167,7 @@ struct WorkArgs {
     uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
                         // boundaries of pair 0 — start, pass A, pass B, solve, transform
     uint64_t* pass_ticks;  // debug (ICP4R_PHASE_TICKS=1): this NN pass' own slots [kPassTickSlots] of the
-                           // batched search's event counts / clocks (tools/nn_events.py), or nullptr
+                           // batched search's event counts / clocks (tools/experiments/nn_events.py), or nullptr
 };
 constexpr int kPassTickSlots = 16;  // per NN pass: 11 event counters / clocks + 4 per-item walls
 constexpr int kMaxTickPasses = 64;  // passes with their own slots (later passes: none)

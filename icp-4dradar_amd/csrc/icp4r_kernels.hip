@@ -2056,7 +2056,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
 }
 
 // Counters of the LDS search runs (device work counts; per-wave events and clocks for
-// ICP4R_PHASE_TICKS=1 — tools/nn_events.py)
+// ICP4R_PHASE_TICKS=1 — tools/experiments/nn_events.py)
 struct RunStats {
     unsigned long long evals = 0, tests = 0;
     uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
@@ -2439,7 +2439,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     const int npl = uload(w.plist_n);
     // work counters; debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1:
     // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
-    // tools/nn_events.py): wave-uniform adds, stored once at the end
+    // tools/experiments/nn_events.py): wave-uniform adds, stored once at the end
     RunStats rs;
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
@@ -4239,7 +4239,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
     };
     // debug (ICP4R_PHASE_TICKS=1): pair 0's phase walls summed over the registration (s_memrealtime,
     // 100 MHz) into ticks[0..9]: staging, test, search, pass A, pass B, solve, fitness test, fitness
-    // search, fitness sum, iterations (tools/solo_phases.py)
+    // search, fitness sum, iterations (tools/experiments/solo_phases.py)
     unsigned long long* tk = (w.ticks && p == 0 && tid == 0) ? reinterpret_cast<unsigned long long*>(w.ticks) : nullptr;
     uint64_t tk_last = tk ? __builtin_amdgcn_s_memrealtime() : 0;
     auto tick = [&](int slot) {

@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
 # A/B of library builds on one box (boxes differ by up to ~6 %, so only same-session pairs compare).
-#   tools/ab.sh <rounds> <lib_a.so> <lib_b.so> [more libs...]
+#   tools/experiments/ab.sh <rounds> <lib_a.so> <lib_b.so> [more libs...]
 # Alternates `bench.py` (C3, no CPU baseline / upload / C5 legs) over the libraries, `rounds` times,
 # and prints per library: value, search / update launch averages (ICP4R_LIBRARY selects the build).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$1; shift
 mkdir -p gpurun_out
 for r in $(seq 1 "$R"); do

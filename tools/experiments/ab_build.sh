@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
-# Build a variant of the library for same-box A/B runs (tools/ab.sh): objects and .so under
+# Build a variant of the library for same-box A/B runs (tools/experiments/ab.sh): objects and .so under
 # _var/ab/<name>/ (git-ignored, but it travels to the GPU box).
-#   tools/ab_build.sh <name> "<-DFLAG=value ...>"
+#   tools/experiments/ab_build.sh <name> "<-DFLAG=value ...>"
 set -eu
-cd "$(dirname "$0")/../icp-4dradar_amd"
+cd "$(dirname "$0")/../../icp-4dradar_amd"
 NAME=$1; FLAGS=${2:-}
 OUT=../_var/ab/$NAME
 mkdir -p "$OUT"

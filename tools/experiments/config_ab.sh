@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
-# A/B of runtime switches on the single-pair configs (same box): tools/config_ab.sh <rounds> <configs> "<ENV=V ...>" ...
-#   e.g. tools/config_ab.sh 2 C5 - ICP4R_FUSE_SEED=0      ("-" = defaults)
+# A/B of runtime switches on the single-pair configs (same box): tools/experiments/config_ab.sh <rounds> <configs> "<ENV=V ...>" ...
+#   e.g. tools/experiments/config_ab.sh 2 C5 - ICP4R_FUSE_SEED=0      ("-" = defaults)
 # Prints per setting and config: registration device time, wall time, bit-exactness vs the oracle.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 R=$1; CFG=$2; shift 2
 for r in $(seq 1 "$R"); do

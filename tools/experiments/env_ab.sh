@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
-# A/B of runtime switches on one box: tools/env_ab.sh <rounds> "<ENV=V ...>" "<ENV=V ...>" ...
+# A/B of runtime switches on one box: tools/experiments/env_ab.sh <rounds> "<ENV=V ...>" "<ENV=V ...>" ...
 # Alternates bench.py (C3, no CPU / upload / C5 legs) over the settings and prints value, search /
 # update launch averages and batch time per setting ("-" = defaults).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$1; shift
 mkdir -p gpurun_out
 for r in $(seq 1 "$R"); do

@@ -1,6 +1,6 @@
 """Per-cloud timeline of index_kernel in the C3 batch (diagnostic build).
 
-    tools/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
+    tools/experiments/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
     ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/experiments/idx_ticks.py [--pairs 1024]
 
 Every cloud's kd build stamps s_memrealtime (100 MHz) at its start and end, with the CU it ran on.

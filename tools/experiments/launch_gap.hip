@@ -1,5 +1,5 @@
 // Microbenchmark: the gap between dependent kernels on one stream, plain launches vs a hipGraph.
-//   hipcc -O3 --offload-arch=gfx950 -o _var/launch_gap tools/launch_gap.hip
+//   hipcc -O3 --offload-arch=gfx950 -o _var/launch_gap tools/experiments/launch_gap.hip
 // K kernels in a chain (each reads the previous one's value): tiny (1 workgroup) and "dirty" (each
 // also streams 32 MB of stores, so the L2 holds dirty lines at every kernel boundary).  Prints the
 // time per kernel for plain stream launches and for the same chain captured once and replayed.

@@ -1,7 +1,7 @@
 """Per-pass event counts and per-run clocks of the persistent batched search (diagnostic;
 ICP4R_PHASE_TICKS=1, ICP4R_GROUPS=1).
 
-    python tools/nn_events.py [--pairs 1024] [--iters 20]
+    python tools/experiments/nn_events.py [--pairs 1024] [--iters 20]
 
 For every NN pass of one registration (each pass adds into its own tick slots), summed over every
 wave of nn_lds_kernel:
@@ -20,7 +20,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 NAMES = ["runs", "queries", "sb_visits", "sb_passed", "blk_cands", "pushes", "drains", "items",

@@ -1,7 +1,7 @@
 """Per-dispatch durations of one benchmark batch, grouped by ICP pass (diagnostic).
 
     rocprofv3 --kernel-trace -d gpurun_out/trace -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --check 0
-    python tools/pass_trace.py gpurun_out/trace
+    python tools/experiments/pass_trace.py gpurun_out/trace
 
 Prints, for the last batch in the trace, every icp4r kernel dispatch in order with its duration (us),
 so the cost of each NN pass (test / order / search) and update is visible per iteration.

@@ -4,7 +4,7 @@ C2, summed per phase by its thread 0 (s_memrealtime, 100 MHz), printed in us —
 iteration.  Slots (icp4r_kernels.hip, solo_kernel): staging, test, search, pass A, pass B, solve,
 fitness test, fitness search, fitness sum, iterations.
 
-    python tools/solo_phases.py
+    python tools/experiments/solo_phases.py
 """
 import ctypes as C
 import json
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 NAMES = ["stage", "test", "search", "pass_a", "pass_b", "solve", "fit_test", "fit_search", "fit_sum"]
 

@@ -4,14 +4,14 @@ the solo plan (solo_kernel, ICP4R_SOLO=1), the multi-launch plan (ICP4R_SOLO=0) 
 LDS plan forced on one pair (ICP4R_NN_LDS=1).  Every mode's result is checked bit-identical to the
 multi-launch plan's.  Prints one JSON line per (size, iteration setting).
 
-    python tools/solo_sweep.py [--sizes 1024,2048,4096,6144,8192] [--reps 20]
+    python tools/experiments/solo_sweep.py [--sizes 1024,2048,4096,6144,8192] [--reps 20]
 """
 import argparse
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 
 MODES = {"solo": {"ICP4R_SOLO": "1"}, "multi": {"ICP4R_SOLO": "0"}, "lds1": {"ICP4R_SOLO": "0", "ICP4R_NN_LDS": "1"}}

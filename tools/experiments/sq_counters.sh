@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
 # SQ instruction / wait counters of the benchmark's kernels (separate --pmc passes, kernel trace only).
-#   tools/sq_counters.sh <outdir>
+#   tools/experiments/sq_counters.sh <outdir>
 set -eu
 OUT=${1:-gpurun_out/sq}
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 # kernel-level profiles of the single-stream configuration (bench.py prices its kernels on the same)
 export ICP4R_GROUPS=1

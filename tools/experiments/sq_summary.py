@@ -1,6 +1,6 @@
-"""Summarise tools/sq_counters.sh output per kernel (sum over the kernel's dispatches).
+"""Summarise tools/experiments/sq_counters.sh output per kernel (sum over the kernel's dispatches).
 
-    python tools/sq_summary.py gpurun_out/sq [--kernel nn_lds_kernel] [--json out.json]
+    python tools/experiments/sq_summary.py gpurun_out/sq [--kernel nn_lds_kernel] [--json out.json]
 """
 from __future__ import annotations
 

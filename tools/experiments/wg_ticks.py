@@ -1,6 +1,6 @@
 """Per-workgroup phase timeline of fold_update_kernel in the C3 batch (diagnostic build).
 
-    tools/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
+    tools/experiments/ab_build.sh wgticks "-DICP4R_WG_TICKS=1"
     ICP4R_LIBRARY=_var/ab/wgticks/libicp4r.so python tools/experiments/wg_ticks.py [--pairs 1024]
 
 Every pair's workgroup stamps s_memrealtime (100 MHz) at its start, after pass A, pass B, the solve
