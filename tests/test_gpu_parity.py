@@ -610,7 +610,7 @@ def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
     assert (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all()
 
 
-@pytest.mark.parametrize("npairs", [1, 5])
+@pytest.mark.parametrize("npairs", [1, 5, 40])
 def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypatch):
     """Targets too large for the in-LDS kd build (the C5 submap class): their Morton sort on one
     workgroup per 8192-point chunk (index_mo_hist_kernel / index_mo_scatter_kernel, the default for
@@ -622,6 +622,8 @@ def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypat
     rng = np.random.default_rng(11)
     if npairs == 1:
         pairs = [_pair(2100, 4096, 30001)]
+    elif npairs == 40:  # a larger batch: 40 pairs x 3 chunk rows of histograms and 40 cell tables
+        pairs = [_pair(2200 + k, 1024 + 97 * k, 8193 + 311 * k) for k in range(npairs)]
     else:
         lat = _lattice(rng, 22)  # 22^3 = 10648 points: ties everywhere
         ls = lat[rng.permutation(len(lat))[:3000]].copy()
