@@ -490,6 +490,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
     if (pl.solo) {  // init, the two kd builds, then every iteration and the fitness pass in one launch
+        icp4r_host::Range solo_range("icp4r solo registration");
         HIP_TRY(launch_init(a, w, npairs, st));
         HIP_TRY(launch_index(a, w, npairs, st));
         const bool kev = ctx->kernel_timing;
@@ -541,7 +542,10 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // nn_order_kernel)
     const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
     const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
+    char pass_name[48];
     for (int it = 0; it < iters; ++it) {
+        snprintf(pass_name, sizeof(pass_name), "icp4r ICP pass %d", it + 1);
+        icp4r_host::Range pass_range(pass_name);
         for (int g = 0; g < groups; ++g) {
             const int ncu_g = search_cu > 0 ? search_cu : ctx->ncu;
             if ((rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 0, it == 0, gs[g], search_cu, fuse && it > 0, it,
@@ -557,6 +561,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
             if (kev) HIP_TRY(hipEventRecord(ue->stop, gs[g]));
         }
     }
+    icp4r_host::Range fit_range("icp4r fitness pass");
     for (int g = 0; g < groups; ++g) {
         // the fitness pass' cached-neighbour test runs inside fitness_prep_kernel when fused
         const int ftest = fuse && a.kp.compute_fitness ? 1 : 0;
@@ -721,6 +726,7 @@ int icp4r_align(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_
                 int32_t tgt_stride_bytes, const float* guess, const icp4r_params* params, icp4r_result* out,
                 float* aligned_out, int32_t out_stride_bytes) {
     if (!ctx || !out) return fail(ICP4R_E_INVALID, "ctx/out is NULL");
+    icp4r_host::Range range("icp4r_align");
     int rc;
     if ((rc = check_cloud(src, n, src_stride_bytes, "source"))) return rc;
     if ((rc = check_cloud(tgt, m, tgt_stride_bytes, "target"))) return rc;
@@ -793,6 +799,7 @@ int icp4r_align(icp4r_ctx* ctx, const float* src, int32_t n, int32_t src_stride_
 int icp4r_align_batch_device(icp4r_ctx* ctx, const icp4r_batch* b, const icp4r_params* params, icp4r_result* results,
                              void* hip_stream) {
     if (!ctx || !b || !results) return fail(ICP4R_E_INVALID, "ctx/batch/results is NULL");
+    icp4r_host::Range range("icp4r_align_batch_device");
     if (b->npairs < 0) return fail(ICP4R_E_INVALID, "npairs < 0");
     if (b->npairs == 0) return ICP4R_OK;
     if (!b->src || !b->tgt || !b->src_off || !b->src_n || !b->tgt_off || !b->tgt_n)
@@ -822,6 +829,7 @@ int icp4r_align_batch_host(icp4r_ctx* ctx, const float* src, const int64_t* src_
                            const float* tgt, const int64_t* tgt_off, const int32_t* tgt_n, int32_t npairs,
                            const float* guess, const icp4r_params* params, icp4r_result* results) {
     if (!ctx || !results || npairs < 0) return fail(ICP4R_E_INVALID, "bad arguments");
+    icp4r_host::Range range("icp4r_align_batch_host");
     if (npairs == 0) return ICP4R_OK;
     if (!src_off || !src_n || !tgt_off || !tgt_n) return fail(ICP4R_E_INVALID, "NULL offset/count array");
     // only the point ranges the pairs cover are uploaded, offsets rebased to them (a shard of a larger

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdint.h>
 
 #include <vector>
@@ -44,6 +45,16 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+};
+
+// A roctx range over a host scope (SURVEY.md §5 "Tracing"): the entry points and every ICP pass show
+// up as named ranges in `rocprofv3 --marker-trace` beside the kernels they launched.  Without a
+// profiler attached a push / pop is a few tens of ns.
+struct Range {
+    explicit Range(const char* name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range&) = delete;
+    Range& operator=(const Range&) = delete;
 };
 
 struct EventPair {

@@ -3747,6 +3747,14 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
 // the launch's count reads the words back with agent-scope (L1-bypassing) loads.  The counter only
 // grows (plist_n[3], zeroed per registration): a launch's last add is the one that makes it a
 // multiple of the grid size.
+// Ordering: this is the measured-valid hand-off of MI355X_MICROARCH.md §Workgroup dispatch (the
+// first row of its sc1 table): ONE lane per workgroup, its payload (owork[p]) stored sc1
+// (write-through) and drained with s_waitcnt vmcnt(0) before the agent-scope add; the consumer is the
+// workgroup whose add came last, told by the add's return value, and every load of the payload is an
+// sc1 load issued after that add returned (the other waves: after the barrier below).  The asm
+// statement's "memory" clobber keeps the compiler from moving the store past the add.  An acq_rel add
+// would instead put an L2 write-back (buffer_wbl2) in every workgroup — 1.7-6.5 us each by the same
+// section's price list — for an ordering the sc1 accesses already give.
 __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test, int order_ncu) {
     __shared__ FoldShared sh;
     __shared__ OrderShared osh;
@@ -3963,7 +3971,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
                     // x = mant * 2^(ex - 1075); below 2^(emin + 53) iff ex - 1023 - emin <= 52, and then
                     // x / 2^emin = mant >> (emin + 1075 - ex), a shift by at most ctz(mant): exact
                     const uint64_t t = (ex - 1023 - emin <= 52) ? (mant >> (emin + 1075 - ex)) : kSat;
-                    S = min(S + t, kSat);
+                    S = (S + t < kSat) ? S + t : kSat;
                 }
             });
 #pragma unroll

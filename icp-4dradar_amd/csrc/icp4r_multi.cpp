@@ -5,6 +5,7 @@
 // when one process drives every device, an RCCL all-gather (xGMI) when each GPU has its own process.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -19,10 +20,19 @@ using icp4r_host::DevBuf;
 using icp4r_host::fail;
 
 struct icp4r_comm {
-    icp4r_ctx* ctx = nullptr;
+    icp4r_ctx* ctx = nullptr;  // (not touched by icp4r_comm_destroy: the context may be gone by then)
+    int device = 0;
     ncclComm_t nccl = nullptr;
     int32_t rank = 0, nranks = 1;
     DevBuf send, recv;  // padded staging for unequal shards
+    // The last gather's completion on the stream it ran on: a gather on another stream waits for it
+    // before it reuses the staging buffers, and icp4r_comm_destroy waits for it before freeing them.
+    hipEvent_t done = nullptr;
+    bool done_recorded = false;
+    hipStream_t last = nullptr;
+    // Test switch (ICP4R_GATHER_PADDED=1 at creation): every gather takes the padded branch, so a
+    // one-rank communicator exercises the staging path that only unequal multi-rank shards reach.
+    bool force_padded = false;
 };
 
 #define RCCL_TRY(expr)                                                                                     \
@@ -55,10 +65,16 @@ int icp4r_align_batch_multi(icp4r_ctx* const* ctxs, int32_t nctx, const float* s
                             const int32_t* src_n, const float* tgt, const int64_t* tgt_off, const int32_t* tgt_n,
                             int32_t npairs, const float* guess, const icp4r_params* params, icp4r_result* results) {
     if (!ctxs || nctx <= 0 || npairs < 0 || !results) return fail(ICP4R_E_INVALID, "icp4r_align_batch_multi: bad arguments");
-    for (int32_t k = 0; k < nctx; ++k)
+    for (int32_t k = 0; k < nctx; ++k) {
         if (!ctxs[k]) return fail(ICP4R_E_INVALID, "icp4r_align_batch_multi: context %d is NULL", k);
+        // one host thread per context: a context listed twice would share its workspace and stream
+        for (int32_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k])
+                return fail(ICP4R_E_INVALID, "icp4r_align_batch_multi: contexts %d and %d are the same context", j, k);
+    }
     if (npairs == 0) return ICP4R_OK;
     if (!src_off || !src_n || !tgt_off || !tgt_n) return fail(ICP4R_E_INVALID, "NULL offset/count array");
+    icp4r_host::Range range("icp4r_align_batch_multi");
     // one host thread per context: each sets its device and runs its shard on its own stream
     std::vector<int> rc((size_t)nctx, ICP4R_OK);
     std::vector<std::string> msg((size_t)nctx);
@@ -99,10 +115,18 @@ int icp4r_comm_create(icp4r_comm** out, icp4r_ctx* ctx, int32_t nranks, int32_t 
     memcpy(&u, id, sizeof(u));
     icp4r_comm* c = new icp4r_comm();
     c->ctx = ctx;
+    c->device = ctx->device;
     c->rank = rank;
     c->nranks = nranks;
+    const char* fp = getenv("ICP4R_GATHER_PADDED");
+    c->force_padded = fp && atoi(fp) != 0;
+    if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return fail(ICP4R_E_HIP, "icp4r_comm_create: hipEventCreate failed");
+    }
     const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
     if (r != ncclSuccess) {
+        (void)hipEventDestroy(c->done);
         delete c;
         return fail(ICP4R_E_RCCL, "ncclCommInitRank (rank %d of %d, device %d): %s", rank, nranks, ctx->device,
                     ncclGetErrorString(r));
@@ -113,11 +137,13 @@ int icp4r_comm_create(icp4r_comm** out, icp4r_ctx* ctx, int32_t nranks, int32_t 
 
 int icp4r_comm_destroy(icp4r_comm* comm) {
     if (!comm) return ICP4R_OK;
-    (void)hipSetDevice(comm->ctx->device);
-    (void)hipStreamSynchronize(comm->ctx->stream);
+    (void)hipSetDevice(comm->device);
+    // the last gather (and with it every earlier one on its stream) done before the staging is freed
+    if (comm->done_recorded) (void)hipEventSynchronize(comm->done);
     const ncclResult_t r = comm->nccl ? ncclCommDestroy(comm->nccl) : ncclSuccess;
     comm->send.release();
     comm->recv.release();
+    if (comm->done) (void)hipEventDestroy(comm->done);
     delete comm;
     if (r != ncclSuccess) return fail(ICP4R_E_RCCL, "ncclCommDestroy: %s", ncclGetErrorString(r));
     return ICP4R_OK;
@@ -146,11 +172,14 @@ int icp4r_gather_results(icp4r_comm* comm, const icp4r_result* shard_rows, int32
     shard_of(npairs, comm->nranks, comm->rank, &first, &count);
     if (count > 0 && !shard_rows) return fail(ICP4R_E_INVALID, "icp4r_gather_results: shard_rows is NULL");
     if (npairs == 0) return ICP4R_OK;
-    HIP_TRY(hipSetDevice(comm->ctx->device));
+    icp4r_host::Range range("icp4r_gather_results");
+    HIP_TRY(hipSetDevice(comm->device));
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : comm->ctx->stream;
     constexpr size_t R = sizeof(icp4r_result);
     const int32_t maxc = (npairs + comm->nranks - 1) / comm->nranks;
-    if (npairs % comm->nranks == 0) {
+    // a gather on another stream than the previous one must not overwrite staging that is still read
+    if (comm->done_recorded && st != comm->last) HIP_TRY(hipStreamWaitEvent(st, comm->done, 0));
+    if (npairs % comm->nranks == 0 && !comm->force_padded) {
         // equal shards: rank r's rows are exactly gathered[r * count, ...) — in place
         RCCL_TRY(ncclAllGather(shard_rows, gathered, (size_t)count * R, ncclUint8, comm->nccl, st));
     } else {
@@ -166,6 +195,9 @@ int icp4r_gather_results(icp4r_comm* comm, const icp4r_result* shard_rows, int32
                                        (size_t)c * R, hipMemcpyDeviceToDevice, st));
         }
     }
+    HIP_TRY(hipEventRecord(comm->done, st));
+    comm->done_recorded = true;
+    comm->last = st;
     return icp4r_comm_check(comm);
 }
 

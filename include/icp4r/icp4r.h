@@ -39,7 +39,8 @@ typedef enum icp4r_status {
     ICP4R_E_TOO_FEW_CORR = -3, /* |C| < min_correspondences: PCL_ERROR, converged = false       */
     ICP4R_E_NONFINITE = -4,    /* NaN/Inf coordinate in an input cloud (rejected up front)      */
     ICP4R_E_HIP = -5,          /* HIP runtime failure (message has the HIP error string)        */
-    ICP4R_E_RCCL = -6,         /* reserved for the multi-GPU driver                              */
+    ICP4R_E_RCCL = -6,         /* RCCL failure in the multi-GPU entries (icp4r_multi.h), incl.
+                                  asynchronous errors reported by ncclCommGetAsyncError        */
     ICP4R_E_NOMEM = -7,        /* device or host allocation failed                               */
     ICP4R_E_TOO_LARGE = -8     /* a size exceeds what the selected kernel supports               */
 } icp4r_status;
@@ -227,8 +228,10 @@ typedef struct icp4r_plan_info {
                            exact); off with ICP4R_NN_CACHE=0                          */
     int64_t nn_blocks;  /* workgroups of one NN launch                               */
     int32_t solo;       /* 1: a PCL-numerics registration of this shape runs whole in one
-                           workgroup per pair (solo_kernel: targets <= 8192, sources <=
-                           16384, fewer than 256 pairs); off with ICP4R_SOLO=0        */
+                           workgroup per pair (solo_kernel): targets <= 8192, sources <=
+                           1024 by default (ICP4R_SOLO=1: up to 16384), and a plan that
+                           does not take the batched LDS search (fewer than 256 pairs,
+                           or ICP4R_NN_LDS=0); ICP4R_SOLO=0: never                    */
     int32_t reserved;
 } icp4r_plan_info;
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);

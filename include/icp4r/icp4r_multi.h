@@ -35,7 +35,9 @@ typedef struct icp4r_comm icp4r_comm;
  * min(rank, npairs % nranks), count = npairs / nranks + (rank < npairs % nranks). */
 int icp4r_shard(int32_t npairs, int32_t nranks, int32_t rank, int32_t* first, int32_t* count);
 
-/* One process, `nctx` contexts (normally one per device; a device may appear twice): context k
+/* One process, `nctx` distinct contexts (normally one per device; two contexts may share a device,
+ * but one context listed twice is ICP4R_E_INVALID: each context's workspace and stream serve one
+ * host thread at a time): context k
  * registers shard k of the batch (icp4r_align_batch_host's arguments, float4 points) on its own
  * device and stream, all shards concurrently (one host thread each); results[npairs] on the host in
  * global pair order, bit-identical to one icp4r_align_batch_host call over the whole batch.
@@ -52,6 +54,8 @@ int icp4r_comm_unique_id(unsigned char id[ICP4R_COMM_ID_BYTES]);
  * unless a call passes another. */
 int icp4r_comm_create(icp4r_comm** out, icp4r_ctx* ctx, int32_t nranks, int32_t rank,
                       const unsigned char id[ICP4R_COMM_ID_BYTES]);
+/* Waits for the communicator's last gather, then frees it.  It does not touch the context it was
+ * created on, so it may run before or after icp4r_destroy of that context. */
 int icp4r_comm_destroy(icp4r_comm* comm);
 int icp4r_comm_rank(const icp4r_comm* comm, int32_t* rank, int32_t* nranks);
 
@@ -62,7 +66,10 @@ int icp4r_comm_check(icp4r_comm* comm);
 /* All-gather of result rows: this rank's icp4r_shard(npairs, nranks, rank) rows, `shard_rows`
  * (device), land at gathered[first, first + count) on every rank (`gathered`: device, npairs rows).
  * Asynchronous on hip_stream (NULL: the context's stream); equal shards gather in place, unequal
- * ones through a padded staging buffer and one copy per rank. */
+ * ones through a padded staging buffer and one copy per rank.  Gathers of one communicator may run
+ * on different streams: a gather waits for the previous one (an event on its stream) before it
+ * reuses the staging buffers.  ICP4R_GATHER_PADDED=1 at icp4r_comm_create (a test switch) sends
+ * every gather through the padded branch. */
 int icp4r_gather_results(icp4r_comm* comm, const icp4r_result* shard_rows, int32_t npairs, icp4r_result* gathered,
                          void* hip_stream);
 

@@ -105,6 +105,59 @@ def test_rccl_single_rank_sharded_batch(gpu_ctx):
         comm.close()
 
 
+def test_rccl_gather_padded_branch(gpu_ctx, monkeypatch):
+    """icp4r_gather_results' unequal-shard branch (padded send / recv staging, one copy per rank),
+    forced on a one-rank communicator by the ICP4R_GATHER_PADDED test switch: the rows of a batch
+    whose size no rank count divides evenly (7 pairs) land byte for byte in global order, also when
+    consecutive gathers run on different streams (the staging is reused behind an event)."""
+    import torch
+
+    import icp4r
+
+    pairs = _pairs(2300, [(2048, 2048), (1500, 1800), (2048, 700), (900, 2048), (37, 500), (2000, 1990),
+                          (1024, 1024)])
+    P = len(pairs)
+    args = _batch(pairs)
+    params = icp4r.default_params(max_iterations=8)
+    ref_h = gpu_ctx.align_batch_host(*args, params=params)
+    dev = torch.device("cuda", 0)
+    rows = torch.from_numpy(np.frombuffer(ref_h.tobytes(), dtype=np.uint8).reshape(P, 96).copy()).to(dev)
+    monkeypatch.setenv("ICP4R_GATHER_PADDED", "1")
+    comm = icp4r.Comm(gpu_ctx, 1, 0, icp4r.Comm.unique_id())
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    try:
+        outs = []
+        for k, s in enumerate([s1, s2, s1, None]):
+            g = torch.full((P, 96), 255, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize(dev)
+            comm.gather(rows.data_ptr(), P, g.data_ptr(), s.cuda_stream if s is not None else None)
+            outs.append(g)
+        torch.cuda.synchronize(dev)
+        comm.check()
+        for g in outs:
+            assert g.cpu().numpy().tobytes() == ref_h.tobytes()
+    finally:
+        comm.close()
+
+
+def test_align_batch_multi_rejects_duplicate_context(gpu_ctx):
+    import icp4r
+
+    args = _batch(_pairs(2400, [(1024, 1024)] * 3))
+    with pytest.raises(icp4r.ICP4RError):
+        icp4r.align_batch_multi([gpu_ctx, gpu_ctx], *args)
+
+
+def test_comm_destroy_after_context(gpu_ctx):
+    """A communicator may outlive its context: icp4r_comm_destroy does not touch the context."""
+    import icp4r
+
+    ctx = icp4r.Context(0)
+    comm = icp4r.Comm(ctx, 1, 0, icp4r.Comm.unique_id())
+    ctx.close()
+    comm.close()
+
+
 def _rank_worker(rank, world, port, P, n, q):
     """One rank on cuda:0: its shard of the pairs through the library (device tensors), the device rows
     gathered over gloo."""
