@@ -222,6 +222,9 @@ int make_kparams(const icp4r_params* p, KParams* kp) {
     kp->huber_delta = p->huber_delta;
     kp->fit_max_range = p->fitness_max_range;
     kp->need_mse = (p->mse_threshold_absolute > 0 || p->euclidean_fitness_epsilon > 0) ? 1 : 0;
+    if (p->eigen_gebp_mr < 0 || p->eigen_gebp_mr > 64)
+        return fail(ICP4R_E_INVALID, "eigen_gebp_mr %d out of range (0: the default 8)", p->eigen_gebp_mr);
+    kp->sigma_max_kc = sigma_max_kc(p->eigen_l1_bytes, p->eigen_gebp_mr);
     return ICP4R_OK;
 }
 

@@ -55,6 +55,8 @@ struct KParams {
     double fit_max_range;  // getFitnessScore(max_range): keep d2 <= max_range
     int32_t need_mse;      // 0 when no MSE criterion can fire (both thresholds <= 0): the MSE only
                            // feeds those two '<' tests, so its sequential sum is skipped
+    int32_t sigma_max_kc;  // Eigen's largest GEMM panel depth for sigma (sigma_max_kc(); INT32_MAX:
+                           // no panels) — the panel depth of |C| correspondences is sigma_kc()
 };
 
 struct PairArgs {

@@ -2973,9 +2973,10 @@ struct SolveShared {
     double sigma[9], ms[3], md[3];
     SvdWork svd;
     SvdWorkF svdf;
-    float sigmaf[9];
+    float sigmaf[9];  // PCL numerics: sigma as Eigen's GEMM leaves it (one_over_n applied per panel)
     float mean[6];
     float one_over_n;
+    int32_t bnd[16];  // pass B with rejected correspondences: the group's panel starts (point index)
     double mse_sum;
     float T_inc[16];
     int32_t flag;  // 0 continue, 1 error (no transform), 2 converged after this transform
@@ -3016,12 +3017,12 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
     mat4_identity(Tinc);
     double mse;
     if constexpr (NUM == kNumericsPCL) {
-        // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (the fold), float SVD,
-        // R as Matrix4f, Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean.
+        // Eigen umeyama, Scalar = float: sigma = one_over_n * Σ d' s'ᵀ (fold_pass_b: Eigen's blocked
+        // GEMM, already scaled), float SVD, R as Matrix4f, Rt.col(3) = dst_mean; Rt.col(3) -= R * src_mean.
         // (in registers: umeyama_rotation_f32_reg is umeyama_rotation_f32 with static indices)
         float sg[9], R[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) sg[k] = sh.one_over_n * sh.sigmaf[k];
+        for (int k = 0; k < 9; ++k) sg[k] = sh.sigmaf[k];
         umeyama_rotation_f32_reg(sg, R);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -3574,9 +3575,94 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     }
 }
 
-// Pass B: the fillers form the 9 products d'_a·s'_b (Huber: (w·d'_a)·s'_b) over the float-demeaned
-// points and wave 0 lanes 0..8 fold them (IEEE addition commutes: p + acc == a·b + acc bit for bit).
-// Leaves sigma (unscaled) in s.sigmaf.
+// Pass B: sigma = one_over_n * Σ d'_a·s'_b over the float-demeaned correspondences, in Eigen 3.3's
+// GEMM order (icp4r_math.hpp sigma_kc; oracle/icp_oracle.c umeyama_f32): the |C| correspondences are
+// cut into S panels of kc, each panel's 9 coefficients are sequential float chains from +0, and the
+// panels are added into sigma (from +0) as one_over_n * chain, in panel order.  The fillers form the
+// products (Huber: (w·d'_a)·s'_b) and the fold lanes sum them (IEEE addition is commutative:
+// p + acc == a·b + acc bit for bit).  Rejected correspondences (d² > max_d2) are not in PCL's list:
+// they add the chain's identity (+0) where they fall, and panel boundaries are counted in accepted
+// correspondences only (fold_bounds).
+//  * one panel (|C| <= 680 at the default host facts): wave 0 lanes 0..8 fold the 9 chains over
+//    chunks of CH points, as before;
+//  * S panels: up to kSliceGroup panels at once — 9·G chains, one fold lane each (waves 0..1), over
+//    LDS chunks that hold T steps of every panel of the group (row (panel, ab) of T floats, rows
+//    strided ≡ 4 mod 8 floats so the fold lanes' ds_read_b128 hit distinct banks): the chain per
+//    panel is kc long instead of |C|.
+// Leaves the finished sigma in s.sigmaf.
+constexpr int kSliceGroup = 14;  // panels folded together (9 x 14 = 126 chains: two fold waves)
+#ifndef ICP4R_FILL_BATCH
+#define ICP4R_FILL_BATCH 2
+#endif
+constexpr int kFillBatch = ICP4R_FILL_BATCH;  // a filler's correspondences in flight per round
+
+// Panel starts of panels [s0, s0 + G] (point indices) when some correspondences are rejected: the
+// panel of rank r starts at the point holding the (s·kc)-th accepted correspondence.  A scan over
+// the points from the group's first start, WG at a time (ranks by ballot + wave prefix), until the
+// group's last boundary is found.  bnd[0] must hold the group's first start; bnd[G] = n when s0 + G
+// reaches S.
+template <int WG, typename Acc>
+__device__ __forceinline__ void fold_bounds(int n, int kc, int S, int s0, int G, Acc accepted, int32_t* bnd,
+                                            int32_t* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NW = WG / 64;
+    const int last = min(s0 + G, S);  // boundaries s0 + 1 .. last
+    if (tid == 0 && last == S) bnd[last - s0] = n;
+    int base = bnd[0];
+    int running = s0 * kc;  // the rank of the first accepted correspondence at or after bnd[0]
+    const int stop_rank = (last == S) ? INT_MAX : last * kc;
+    while (base < n && running <= stop_rank) {
+        const int i = base + tid;
+        const bool acc = i < n && accepted(i);
+        const uint64_t bal = __ballot(acc);
+        const int pre = __builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = __builtin_popcountll(bal);
+        __syncthreads();
+        int off = running, tot = running;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+            off += v < wave ? wsum[v] : 0;
+            tot += wsum[v];
+        }
+        const int r = off + pre;
+        if (acc && r > s0 * kc && r % kc == 0) {
+            const int sl = r / kc;
+            if (sl <= last && sl < S) bnd[sl - s0] = i;
+        }
+        running = tot;
+        base += WG;
+        __syncthreads();  // (wsum reused)
+    }
+    __syncthreads();
+}
+
+// A panel chain's step over one chunk row (len <= T floats, 16-B aligned): groups of 8 floats, the
+// next group's two ds_read_b128 issued before this group's adds (few registers: the fold lanes of the
+// panel groups share their waves' allocation with the fillers).
+__device__ __forceinline__ float fold_row(const float* f, int len, float acc) {
+    int k = 0;
+    if (len >= 8) {
+        float4 a0 = *reinterpret_cast<const float4*>(f), a1 = *reinterpret_cast<const float4*>(f + 4);
+        for (; k + 8 <= len; k += 8) {
+            const int nx = (k + 16 <= len) ? k + 8 : k;  // the next group, or a harmless re-read
+            const float4 b0 = *reinterpret_cast<const float4*>(f + nx), b1 = *reinterpret_cast<const float4*>(f + nx + 4);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = acc + a0.x;
+            acc = acc + a0.y;
+            acc = acc + a0.z;
+            acc = acc + a0.w;
+            acc = acc + a1.x;
+            acc = acc + a1.y;
+            acc = acc + a1.z;
+            acc = acc + a1.w;
+            a0 = b0;
+            a1 = b1;
+        }
+    }
+    for (; k < len; ++k) acc = acc + f[k];
+    return acc;
+}
+
 template <int WG, int CH, int ROW>
 __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], SolveShared& s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3598,65 +3684,165 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
         }
     };
     const int n = f.n;
-    const int nch = (n + CH - 1) / CH;
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const float ms[3] = {s.mean[0], s.mean[1], s.mean[2]};
     const float md[3] = {s.mean[3], s.mean[4], s.mean[5]};
-    constexpr int kFillB = WG - 64, kPerB = (CH + kFillB - 1) / kFillB;
-    auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
-        const int base = c * CH, len = min(CH, n - base);
-#pragma unroll
-        for (int e = 0; e < kPerB; ++e) {
-            const int i = base + min(tid - 64 + e * kFillB, len - 1);
-            rec(i, r[e][0], r[e][1]);
+    const float oon = s.one_over_n;
+    const int cnt = (int)s.mom[0];
+    const int kc = sigma_kc(cnt, kp.sigma_max_kc);
+    const int S = (cnt > 0 && kc > 0) ? (cnt + kc - 1) / kc : 1;
+    // the 9 products of one correspondence (0 when it is rejected)
+    auto products = [&](float4 r0, float4 r1, float (&pr)[9]) __attribute__((always_inline)) {
+        rec_fix(r0, r1);
+        float sv[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f}, wt = 0.f;
+        if (!(r1.w > kp.max_d2)) {
+            sv[0] = r0.x - ms[0];
+            sv[1] = r0.y - ms[1];
+            sv[2] = r0.z - ms[2];
+            dv[0] = r1.x - md[0];
+            dv[1] = r1.y - md[1];
+            dv[2] = r1.z - md[2];
+            wt = r0.w;
         }
-    };
-    auto store_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {  // waves 1..3
-        float(*b)[ROW] = buf[c & 1];
-        const int base = c * CH, len = min(CH, n - base);
 #pragma unroll
-        for (int e = 0; e < kPerB; ++e) {
-            const int o = tid - 64 + e * kFillB;
-            if (o >= len) break;
-            rec_fix(r[e][0], r[e][1]);
-            float sv[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f}, wt = 0.f;
-            if (!(r[e][1].w > kp.max_d2)) {
-                sv[0] = r[e][0].x - ms[0];
-                sv[1] = r[e][0].y - ms[1];
-                sv[2] = r[e][0].z - ms[2];
-                dv[0] = r[e][1].x - md[0];
-                dv[1] = r[e][1].y - md[1];
-                dv[2] = r[e][1].z - md[2];
-                wt = r[e][0].w;
+        for (int ra = 0; ra < 3; ++ra)
+#pragma unroll
+            for (int rb = 0; rb < 3; ++rb) pr[ra * 3 + rb] = weighted ? (wt * dv[ra]) * sv[rb] : dv[ra] * sv[rb];
+    };
+    if (S <= 1) {
+        // one panel: the 9 chains over every point, wave 0 lanes 0..8
+        const int nch = (n + CH - 1) / CH;
+        constexpr int kFillB = WG - 64, kPerB = (CH + kFillB - 1) / kFillB;
+        auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
+            const int base = c * CH, len = min(CH, n - base);
+#pragma unroll
+            for (int e = 0; e < kPerB; ++e) {
+                const int i = base + min(tid - 64 + e * kFillB, len - 1);
+                rec(i, r[e][0], r[e][1]);
             }
+        };
+        auto store_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {  // waves 1..
+            float(*b)[ROW] = buf[c & 1];
+            const int base = c * CH, len = min(CH, n - base);
 #pragma unroll
-            for (int ra = 0; ra < 3; ++ra)
+            for (int e = 0; e < kPerB; ++e) {
+                const int o = tid - 64 + e * kFillB;
+                if (o >= len) break;
+                float pr[9];
+                products(r[e][0], r[e][1], pr);
 #pragma unroll
-                for (int rb = 0; rb < 3; ++rb) b[ra * 3 + rb][o] = weighted ? (wt * dv[ra]) * sv[rb] : dv[ra] * sv[rb];
-        }
-    };
-    float sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b)
-    if (wv == 0) {
-        for (int c = 0; c < nch; ++c) {
-            __syncthreads();
-            if (lane < 9) sacc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), sacc);
-        }
-    } else {
-        if (nch > 0) {
-            float4 r[kPerB][2];
-            load_b(0, r);
-            store_b(0, r);
-        }
-        for (int c = 0; c < nch; ++c) {
-            __syncthreads();
-            if (c + 1 < nch) {
+                for (int k = 0; k < 9; ++k) b[k][o] = pr[k];
+            }
+        };
+        float sacc = 0.0f;  // lane a*3+b of wave 0: the chain of sigma(a, b)
+        if (wv == 0) {
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (lane < 9) sacc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), sacc);
+            }
+        } else {
+            if (nch > 0) {
                 float4 r[kPerB][2];
-                load_b(c + 1, r);
-                store_b(c + 1, r);
+                load_b(0, r);
+                store_b(0, r);
+            }
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (c + 1 < nch) {
+                    float4 r[kPerB][2];
+                    load_b(c + 1, r);
+                    store_b(c + 1, r);
+                }
             }
         }
+        // res(i, j) += alpha * C0 into the zeroed sigma
+        if (wave == 0 && lane < 9) s.sigmaf[lane] = 0.0f + oon * sacc;
+        __syncthreads();
+        return;
     }
-    if (wave == 0 && lane < 9) s.sigmaf[lane] = sacc;
+
+    // S panels, in groups of up to kSliceGroup
+    constexpr int CAP = 9 * ROW;  // floats per chunk buffer
+    auto bufs = [&](int k) -> float* { return &buf[k & 1][0][0]; };  // (no local array: it went to scratch)
+    const bool rejected = cnt < n;  // some correspondence left PCL's list: panel starts by rank
+    float sig = 0.0f;               // wave 0 lanes 0..8: sigma(a, b), the panels added in order
+    if (tid == 0) s.bnd[0] = 0;
+    __syncthreads();
+    for (int s0 = 0; s0 < S; s0 += kSliceGroup) {
+        const int G = min(kSliceGroup, S - s0);
+        const int R = 9 * G;                                      // fold chains of the group
+        const int stride = (((CAP / R) - 4) & ~7) + 4;            // row stride, ≡ 4 mod 8 floats
+        const int T = stride - 4;                                 // steps per chunk (a multiple of 8)
+        const int FW = (R + 63) / 64;                             // fold waves (1 or 2)
+        const int nF = WG - 64 * FW;                              // fillers
+        if (rejected) {
+            auto accepted = [&](int i) {
+                float4 r0, r1;
+                rec(i, r0, r1);
+                rec_fix(r0, r1);
+                return !(r1.w > kp.max_d2);
+            };
+            fold_bounds<WG>(n, kc, S, s0, G, accepted, s.bnd, reinterpret_cast<int32_t*>(bufs(0)));
+        }
+        // panel sl of the group covers points [start(sl), start(sl + 1))
+        auto start = [&](int sl) -> int {
+            return rejected ? s.bnd[sl] : min((s0 + sl) * kc, n);
+        };
+        int maxlen = 0;
+        for (int sl = 0; sl < G; ++sl) maxlen = max(maxlen, (s0 + sl + 1 >= S ? n : start(sl + 1)) - start(sl));
+        const int nch = (maxlen + T - 1) / T;
+        // the fillers' slots of chunk c: slot q = (panel sl, step t), q = sl * T + t
+        const int per = (G * T + nF - 1) / nF;
+        auto fill = [&](int c) __attribute__((always_inline)) {
+            float* b = bufs(c);
+            const int me = tid - 64 * FW;
+            for (int e0 = 0; e0 < per; e0 += kFillBatch) {
+                float4 r[kFillBatch][2];
+                int at[kFillBatch];
+#pragma unroll
+                for (int e = 0; e < kFillBatch; ++e) {
+                    const int q = me + (e0 + e) * nF;
+                    const int sl = q / T, t = q - sl * T;
+                    const int i0 = sl < G ? start(sl) : n;
+                    const int i1 = sl < G ? (s0 + sl + 1 >= S ? n : start(sl + 1)) : n;
+                    const int i = i0 + c * T + t;
+                    at[e] = (e0 + e < per && sl < G && i < i1) ? sl * 9 * stride + t : -1;
+                    rec(at[e] >= 0 ? i : 0, r[e][0], r[e][1]);
+                }
+#pragma unroll
+                for (int e = 0; e < kFillBatch; ++e) {
+                    if (at[e] < 0) continue;
+                    float pr[9];
+                    products(r[e][0], r[e][1], pr);
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) b[at[e] + k * stride] = pr[k];
+                }
+            }
+        };
+        float acc = 0.0f;  // fold lane L = sl * 9 + ab: the chain of panel s0 + sl, coefficient ab
+        const int L = tid;
+        const int my_sl = L / 9;
+        const int my_len = (wv < FW && L < R) ? ((s0 + my_sl + 1 >= S ? n : start(my_sl + 1)) - start(my_sl)) : 0;
+        if (wv >= FW && nch > 0) fill(0);
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (wv < FW) {
+                const int len = min(T, my_len - c * T);
+                if (L < R && len > 0) acc = fold_row(bufs(c) + L * stride, len, acc);
+            } else if (c + 1 < nch) {
+                fill(c + 1);
+            }
+        }
+        __syncthreads();  // every chunk folded: the buffer of chunk nch (unused) takes the chains
+        float* cs = bufs(nch);
+        if (wv < FW && L < R) cs[L] = acc;
+        __syncthreads();
+        if (wave == 0 && lane < 9)
+            for (int sl = 0; sl < G; ++sl) sig = sig + oon * cs[sl * 9 + lane];  // res += alpha * C0
+        if (rejected && tid == 0) s.bnd[0] = s.bnd[G];  // the next group's first start
+        __syncthreads();
+    }
+    if (wave == 0 && lane < 9) s.sigmaf[lane] = sig;
     __syncthreads();
 }
 

@@ -25,6 +25,29 @@ __device__ __forceinline__ float l2_simple(float qx, float qy, float qz, float t
     return r;
 }
 
+// ---- the depth blocking of umeyama's sigma GEMM (Eigen 3.3; oracle/icp_oracle.c umeyama_f32) ----
+// pcl::umeyama's sigma = one_over_n * dst_demean * src_demean^T is an Eigen GEMM of depth |C|: the
+// depth is cut into panels of kc (evaluateProductBlockingSizesHeuristic), and gebp's scalar tail path
+// (3 rows < LhsProgress, 3 columns < nr) forms each coefficient of a panel as a sequential chain
+// C0 = a*b + C0 from 0, then res += alpha * C0 panel by panel (DESIGN.md §2 has the derivation).
+// sigma_max_kc: the largest panel depth for the reference host's L1d size and gebp mr (KcFactor 1,
+// nr 4, float, k_peeling 8); l1 < 0: no blocking.
+__host__ __device__ inline int32_t sigma_max_kc(int32_t l1, int32_t mr) {
+    if (l1 < 0) return INT32_MAX;
+    if (l1 == 0) l1 = 32768;
+    if (mr <= 0) mr = 8;
+    const int32_t k_div = mr * 4 + 4 * 4, k_sub = mr * 4 * 4;
+    const int32_t mkc = ((l1 - k_sub) / k_div) & ~7;
+    return mkc < 1 ? 1 : mkc;
+}
+// the panel depth Eigen picks for a depth of k: the same number of panels as max_kc would give, the
+// last one as large as possible (k <= max_kc, or k < 48: one panel)
+__host__ __device__ inline int32_t sigma_kc(int32_t k, int32_t max_kc) {
+    if (max_kc <= 0 || k < 48 || k <= max_kc) return k;
+    const int32_t r = k % max_kc;
+    return r == 0 ? max_kc : max_kc - 8 * ((max_kc - 1 - r) / (8 * (k / max_kc + 1)));
+}
+
 // T: column-major 4x4 float (12 used entries: T[c*4 + r])
 __device__ __forceinline__ void xform_pt(const float* T, float x, float y, float z, float& ox, float& oy,
                                          float& oz) {

@@ -95,7 +95,9 @@ class Params(C.Structure):
         ("compute_fitness", C.c_int32),
         ("huber_delta", C.c_double),
         ("fitness_max_range", C.c_double),
-        ("reserved", C.c_int32 * 8),
+        ("eigen_l1_bytes", C.c_int32),
+        ("eigen_gebp_mr", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ICP4R_ABI_VERSION 3
+#define ICP4R_ABI_VERSION 4
 
 typedef enum icp4r_status {
     ICP4R_OK = 0,
@@ -56,8 +56,9 @@ typedef enum icp4r_convergence_state {
 } icp4r_convergence_state;
 
 /* Umeyama arithmetic.
- * PCL: PCL's Scalar = float Umeyama restated operation by operation: centroids and the 3x3
- *      cross-covariance as the sequential float folds Eigen 3.3 performs, float one-sided Jacobi
+ * PCL: PCL's Scalar = float Umeyama restated operation by operation: centroids as the sequential
+ *      float folds Eigen 3.3 performs, the 3x3 cross-covariance as its depth-blocked GEMM (one
+ *      sequential chain per panel of kc correspondences, panels added in order), float one-sided Jacobi
  *      SVD, R and t as Matrix4f, MSE and fitness as sequential double sums.  Bit-identical to the
  *      float restatement in oracle/ (tests assert equal bits); the default.
  * F64: every moment summed in double (more accurate than PCL; differs from it by PCL's own
@@ -87,7 +88,12 @@ typedef struct icp4r_params {
     int32_t compute_fitness;                   /* 1: getFitnessScore(fitness_max_range) computed once   */
     double huber_delta;                        /* build extension (no PCL counterpart); +inf == PCL     */
     double fitness_max_range;                  /* getFitnessScore(max_range);     DBL_MAX               */
-    int32_t reserved[8];
+    /* PCL numerics: Eigen 3.3 evaluates umeyama's sigma = one_over_n * dst_demean * src_demean^T as a
+     * GEMM whose depth (the correspondences) is cut into panels of kc, each a sequential float chain
+     * added into sigma in order.  kc follows from two facts of the reference's host:   */
+    int32_t eigen_l1_bytes;                    /* L1d size Eigen queried: 0 = 32768; < 0 = no panels    */
+    int32_t eigen_gebp_mr;                     /* gebp_traits<float>::mr: 0 = 8 (SSE, no FMA)           */
+    int32_t reserved[6];
 } icp4r_params;
 
 typedef struct icp4r_result {

@@ -478,14 +478,56 @@ static inline double huber_w(double d2, double delta) {
     return r <= delta ? 1.0 : delta / r;
 }
 
+/* The depth blocking of the sigma product (Eigen 3.3, single thread).
+ *
+ * pcl::umeyama (PCL 1.8.1 common/impl/eigen.hpp) forms
+ *     sigma = one_over_n * dst_demean * src_demean.transpose()
+ * with dst_demean a 3 x n row-major float matrix.  Eigen 3.3 evaluates a product with two small
+ * fixed dimensions and a dynamic depth as a GEMM (product_type_selector<Small,Small,Large>) once
+ * depth + 3 + 3 >= 20 (generic_product_impl<...,GemmProduct>::evalTo; below that a coefficient-based
+ * product, whose vectorised redux order depends on the operands' alignment — not replicated here,
+ * those n < 14 registrations use the GEMM form too).  The scalar factor is popped off the lhs
+ * (blas_traits of scalar * matrix), so alpha = one_over_n, and sigma is zeroed before the GEMM adds
+ * into it.  general_matrix_matrix_product::run walks the depth in panels of kc
+ * (computeProductBlockingSizes -> evaluateProductBlockingSizesHeuristic) and calls gebp once per
+ * panel; with 3 rows (< LhsProgress = 4) and 3 columns (< nr = 4) gebp takes its scalar tail path
+ * ("remaining columns", one coefficient at a time):
+ *     C0 = 0; for k in panel: C0 = pmadd(A0, B0, C0) = A0*B0 + C0;   res(i, j) += alpha * C0;
+ * so every coefficient is a sequential float chain per panel, the panels added into sigma in order.
+ * kc: max_kc = ((l1 - mr*nr*4) / (mr*4 + nr*4)) & ~7 (KcFactor 1, k_peeling 8), then for depth
+ * k > max_kc, kc = max_kc when max_kc divides k, else max_kc - 8 * ((max_kc - 1 - k % max_kc) /
+ * (8 * (k / max_kc + 1))) — the last panel as large as possible for the same number of panels.
+ * Assumptions (the reference's build is not in this image): float, SSE without FMA (packet of 4,
+ * gebp_traits<float>::mr = default_mr = 8, nr = 4), L1 data cache 32 KiB as queried by CPUID on
+ * the node's x86-64 host: max_kc = 680, and n = 8192 runs 13 panels of kc = 632; n = 2048, 4 of
+ * 520; n <= 680 one panel (the plain sequential chain).  eigen_l1_bytes / eigen_gebp_mr override
+ * the two host facts; eigen_l1_bytes < 0 turns the blocking off (one panel of depth n). */
+int32_t oracle_sigma_max_kc(int32_t l1, int32_t mr) {
+    if (l1 < 0) return INT32_MAX;
+    if (l1 == 0) l1 = 32768;
+    if (mr <= 0) mr = 8;
+    const int32_t nr = 4, k_peeling = 8;
+    const int32_t k_div = mr * 4 + nr * 4, k_sub = mr * nr * 4;
+    int32_t max_kc = ((l1 - k_sub) / k_div) & ~(k_peeling - 1);
+    return max_kc < 1 ? 1 : max_kc;
+}
+
+int32_t oracle_sigma_kc(int32_t k, int32_t max_kc) {
+    if (max_kc <= 0 || k < 48 || k <= max_kc) return k;  /* early return for max(k, 3, 3) < 48; no depth blocking */
+    const int32_t r = k % max_kc;
+    return r == 0 ? max_kc : max_kc - 8 * ((max_kc - 1 - r) / (8 * (k / max_kc + 1)));
+}
+
 /* Umeyama, Scalar = float (Eigen 3.3 Geometry/Umeyama.h as called by
  * TransformationEstimationSVD::estimateRigidTransformation with use_umeyama_).
  * rowwise().sum() on a 3xN column-major matrix has a strided inner access and is a sequential
- * float fold in Eigen 3.3; the sigma GEMM is restated as a sequential float accumulation
- * scaled once by one_over_n (Eigen's blocked GEMM order is not replicated — see DESIGN.md). */
+ * float fold in Eigen 3.3; sigma is the blocked GEMM above: per panel of kc correspondences a
+ * sequential float chain of d'_a * s'_b products from +0, added as one_over_n * chain into sigma
+ * (from +0) in panel order.  Huber (build-only, no PCL counterpart): the same panels over the
+ * products (w * d'_a) * s'_b, one_over_n = 1 / Σw. */
 static void umeyama_f32(const float* X, const float* tgt, int32_t tgt_stride, const int32_t* cq,
-                        const int32_t* cm, const float* cd2, int32_t n, double huber, float T[16],
-                        oracle_trace* tr, int it) {
+                        const int32_t* cm, const float* cd2, int32_t n, double huber, int32_t max_kc,
+                        float T[16], oracle_trace* tr, int it) {
     float one_over_n;
     float ms[3] = {0, 0, 0}, md[3] = {0, 0, 0};
     float sigma[9] = {0};
@@ -501,16 +543,6 @@ static void umeyama_f32(const float* X, const float* tgt, int32_t tgt_stride, co
             ms[k] = a * one_over_n;
             md[k] = b * one_over_n;
         }
-        for (int32_t i = 0; i < n; ++i) {
-            float s[3], d[3];
-            for (int k = 0; k < 3; ++k) {
-                s[k] = X[(size_t)cq[i] * 3 + k] - ms[k];
-                d[k] = tgt[(size_t)cm[i] * tgt_stride + k] - md[k];
-            }
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) sigma[a * 3 + b] = d[a] * s[b] + sigma[a * 3 + b];
-        }
-        for (int k = 0; k < 9; ++k) sigma[k] = one_over_n * sigma[k];
     } else {
         float sw = 0;
         for (int32_t i = 0; i < n; ++i) {
@@ -523,17 +555,27 @@ static void umeyama_f32(const float* X, const float* tgt, int32_t tgt_stride, co
         }
         one_over_n = 1.0f / sw;
         for (int k = 0; k < 3; ++k) { ms[k] *= one_over_n; md[k] *= one_over_n; }
-        for (int32_t i = 0; i < n; ++i) {
-            float w = (float)huber_w(cd2[i], huber);
+    }
+    const int32_t kc = oracle_sigma_kc(n, max_kc);
+    for (int32_t k0 = 0; k0 < n; k0 += kc) {
+        const int32_t k1 = n - k0 < kc ? n : k0 + kc;
+        float c[9] = {0};
+        for (int32_t i = k0; i < k1; ++i) {
             float s[3], d[3];
             for (int k = 0; k < 3; ++k) {
                 s[k] = X[(size_t)cq[i] * 3 + k] - ms[k];
                 d[k] = tgt[(size_t)cm[i] * tgt_stride + k] - md[k];
             }
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) sigma[a * 3 + b] += w * d[a] * s[b];
+            if (weighted) {
+                const float w = (float)huber_w(cd2[i], huber);
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) c[a * 3 + b] = (w * d[a]) * s[b] + c[a * 3 + b];
+            } else {
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) c[a * 3 + b] = d[a] * s[b] + c[a * 3 + b];
+            }
         }
-        for (int k = 0; k < 9; ++k) sigma[k] = one_over_n * sigma[k];
+        for (int k = 0; k < 9; ++k) sigma[k] = sigma[k] + one_over_n * c[k];
     }
     float R[9];
     rot_f32(sigma, R);
@@ -792,7 +834,8 @@ int oracle_align(const float* src, int32_t n, int32_t src_stride, const float* t
         if (p.numerics == ORACLE_NUM_F64)
             umeyama_f64(X, tgt, tgt_stride, cq, cm, cd, cnt, p.huber_delta, Tinc, tr, nr_iterations);
         else
-            umeyama_f32(X, tgt, tgt_stride, cq, cm, cd, cnt, p.huber_delta, Tinc, tr, nr_iterations);
+            umeyama_f32(X, tgt, tgt_stride, cq, cm, cd, cnt, p.huber_delta,
+                        oracle_sigma_max_kc(p.eigen_l1_bytes, p.eigen_gebp_mr), Tinc, tr, nr_iterations);
         /* transformCloud(*input_transformed, *input_transformed, transformation_) */
         for (int32_t i = 0; i < n; ++i) {
             float o[3];

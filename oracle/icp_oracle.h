@@ -45,7 +45,18 @@ typedef struct oracle_params {
     int32_t compute_fitness;                /* 1: run getFitnessScore(fitness_max_range) once */
     double  huber_delta;                    /* build-only extension; +inf == PCL                 */
     double  fitness_max_range;              /* getFitnessScore(max_range) default DBL_MAX         */
+    /* The sigma GEMM's depth blocking (Eigen 3.3 evaluateProductBlockingSizesHeuristic, see
+     * umeyama_f32): the L1 data cache size Eigen queried on the reference host (0: 32768, the x86
+     * L1d of the ROS-melodic era; < 0: no blocking, one sequential chain) and gebp_traits<float>::mr
+     * of its SIMD build (0: 8 = SSE without FMA). */
+    int32_t eigen_l1_bytes;
+    int32_t eigen_gebp_mr;
 } oracle_params;
+
+/* The sigma GEMM's depth blocking (umeyama_f32): Eigen's largest panel depth for these host
+ * facts, and the panel depth kc it picks for a depth of k correspondences. */
+int32_t oracle_sigma_max_kc(int32_t l1_bytes, int32_t gebp_mr);
+int32_t oracle_sigma_kc(int32_t k, int32_t max_kc);
 
 typedef struct oracle_result {
     float   T[16];              /* final_transformation_, column-major (Eigen storage order) */

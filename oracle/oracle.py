@@ -35,6 +35,8 @@ class OracleParams(C.Structure):
         ("compute_fitness", C.c_int32),
         ("huber_delta", C.c_double),
         ("fitness_max_range", C.c_double),
+        ("eigen_l1_bytes", C.c_int32),
+        ("eigen_gebp_mr", C.c_int32),
     ]
 
 

@@ -73,6 +73,48 @@ def umeyama_f64(s: np.ndarray, d: np.ndarray) -> np.ndarray:
     return T.astype(F32), sigma, ms, md
 
 
+def eigen_gemm_kc(depth: int, l1: int = 32 * 1024, mr: int = 8, nr: int = 4) -> int:
+    """Panel depth of Eigen 3.3's blocked GEMM for sigma = one_over_n * dst_demean * src_demean^T
+    (evaluateProductBlockingSizesHeuristic, float, one thread, KcFactor 1): the lhs micro-panel
+    (mr x kc) plus the rhs micro-panel (kc x nr) plus the mr x nr result block fit in L1, kc a
+    multiple of the peeling factor 8; a longer depth is cut into equal-count panels, the last one as
+    large as possible."""
+    if depth < 48:
+        return depth
+    max_kc = max(((l1 - mr * nr * 4) // (mr * 4 + nr * 4)) & ~7, 1)
+    if depth <= max_kc:
+        return depth
+    rem = depth % max_kc
+    if rem == 0:
+        return max_kc
+    return max_kc - 8 * ((max_kc - 1 - rem) // (8 * (depth // max_kc + 1)))
+
+
+def umeyama_sigma_f32(s: np.ndarray, d: np.ndarray, kc: int | None = None):
+    """PCL's float Umeyama moments (Scalar = float): the centroids as Eigen's sequential
+    rowwise().sum() times one_over_n, and sigma as Eigen's blocked GEMM — per panel of kc
+    correspondences a sequential chain of fl(d'_a * s'_b) from +0, each panel added into sigma (from
+    +0) scaled by one_over_n.  Sequential float sums via np.cumsum (numpy's add.reduce is pairwise)."""
+    s = np.asarray(s, F32)
+    d = np.asarray(d, F32)
+    n = len(s)
+    oon = F32(1.0) / F32(n)
+    ms = np.array([np.cumsum(s[:, k], dtype=F32)[-1] * oon for k in range(3)], F32)
+    md = np.array([np.cumsum(d[:, k], dtype=F32)[-1] * oon for k in range(3)], F32)
+    sd = s - ms
+    dd = d - md
+    kc = eigen_gemm_kc(n) if kc is None else kc
+    sigma = np.zeros(9, F32)
+    for k0 in range(0, n, kc):
+        k1 = min(n, k0 + kc)
+        for a in range(3):
+            for b in range(3):
+                prod = dd[k0:k1, a] * sd[k0:k1, b]
+                chain = np.cumsum(np.concatenate([np.zeros(1, F32), prod]), dtype=F32)[-1]
+                sigma[a * 3 + b] = sigma[a * 3 + b] + oon * chain
+    return sigma.reshape(3, 3), ms, md
+
+
 def mat4_mul_f32(A: np.ndarray, B: np.ndarray) -> np.ndarray:
     """Matrix4f product, k-ordered unfused float32 accumulation (Eigen lazy product)."""
     A = np.asarray(A, F32)

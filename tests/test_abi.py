@@ -77,7 +77,7 @@ def test_params_default_matches_pcl():
     assert math.isinf(p.huber_delta)
     assert p.fitness_max_range == sys.float_info.max
     L = icp4r.load()
-    assert L.icp4r_abi_version() == 3
+    assert L.icp4r_abi_version() == 4
     assert b"gfx950" in L.icp4r_version()
 
 

@@ -127,6 +127,55 @@ def test_icp_random_pairs_pcl_defaults(gpu_ctx, oracle_mod, i):
     assert (out[:, 3] == src[:, 3]).all()
 
 
+# The sigma GEMM's depth blocking (Eigen 3.3: panels of kc correspondences): one panel
+# up to 680 correspondences, 2-13 panels at the benchmark sizes, more than one panel group (> 14
+# panels) past ~9k, panel starts counted in accepted correspondences when some are rejected, Huber
+# products, the unblocked form, and every plan (solo, multi-launch, batched).
+@pytest.mark.parametrize("n,m,kw", [
+    (681, 700, {}),                                          # 2 panels of 344 / 337
+    (2048, 2048, {"max_iterations": 20}),                    # 4 panels (C1 shape)
+    (8192, 8192, {"max_iterations": 20}),                    # 13 panels (C2 shape)
+    (16384, 8192, {"max_iterations": 6}),                    # 25 panels: two panel groups
+    (4096, 4096, {"max_correspondence_distance": 0.6}),      # rejected correspondences: ranked starts
+    (20000, 6000, {"max_correspondence_distance": 0.5, "max_iterations": 5}),  # ... over two groups
+    (3000, 3000, {"huber_delta": 0.4}),                      # Huber products, 5 panels
+    (8192, 8192, {"eigen_l1_bytes": -1}),                    # unblocked: one chain of |C|
+    (8192, 8192, {"eigen_l1_bytes": 49152, "eigen_gebp_mr": 16}),  # other host facts
+])
+def test_sigma_panels_vs_oracle(gpu_ctx, oracle_mod, n, m, kw):
+    import icp4r
+
+    src, tgt = _pair(700 + n % 97, n, m)
+    r, out = gpu_ctx.align(src, tgt, icp4r.default_params(**kw), want_aligned=True)
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True, **kw)
+    assert r.status == o["status"] == 0
+    assert r.iterations == o["iterations"] and r.convergence_state == o["convergence_state"]
+    assert r.n_correspondences == o["n_correspondences"]
+    if "max_correspondence_distance" in kw:
+        assert 0 < r.n_correspondences < n  # the ranked panel starts were exercised
+    assert (r.matrix() == o["T"]).all() and r.fitness == o["fitness"]
+    assert (out == o["aligned"]).all()
+
+
+@pytest.mark.parametrize("solo", ["0", "1"])
+def test_sigma_panels_batch_and_solo(gpu_ctx, oracle_mod, solo, monkeypatch):
+    """Panels in the one-workgroup registration (solo_kernel, forced up to 16k sources) and in a
+    batch of ragged pairs, against the oracle pair by pair."""
+    import icp4r
+
+    monkeypatch.setenv("ICP4R_SOLO", solo)
+    shapes = [(1024, 1024), (2048, 1500), (700, 2048), (5000, 4000), (681, 681)]
+    pairs = [_pair(800 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    p = icp4r.default_params(max_iterations=12)
+    res = gpu_ctx.align_batch_host(*_batch(pairs), params=p)
+    for k, (s, t) in enumerate(pairs):
+        o = oracle_mod.align(s, t, numerics=oracle_mod.NUM_F32, max_iterations=12)
+        T = np.array(res[k]["T"], np.float32).reshape(4, 4).T
+        assert res[k]["iterations"] == o["iterations"], k
+        assert (T == o["T"]).all(), k
+        assert res[k]["fitness"] == o["fitness"], k
+
+
 def test_known_answers(gpu_ctx, golden):
     import icp4r
 

@@ -55,6 +55,29 @@ def test_icp_f64_matches_numpy_twin(oracle_mod, golden, which):
 
 
 @pytest.mark.parametrize("which", [0, 1])
+def test_pcl_float_sigma_matches_numpy_twin(oracle_mod, golden, which):
+    """The oracle's float Umeyama moments of the first iteration — sequential centroids and Eigen's
+    depth-blocked sigma GEMM (13 panels of 632 at 8k, 4 of 520 at 2k) — equal an independent numpy
+    restatement bit for bit.  Also the unblocked form (eigen_l1_bytes < 0: one chain of n)."""
+    import sys
+    sys.path.insert(0, GOLDEN_DIR)
+    import numpy_twin as tw
+
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    idx, _ = tw.nearest(src[:, :3], tgt[:, :3])
+    n = len(src)
+    assert tw.eigen_gemm_kc(n) == {2048: 520, 8192: 632}[n]
+    for l1, kc in ((0, None), (-1, n)):
+        r = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=1, trace=True,
+                             eigen_l1_bytes=l1)
+        sigma, ms, md = tw.umeyama_sigma_f32(src[:, :3], tgt[idx, :3], kc=kc)
+        assert (r["trace"]["sigma"][0].astype(np.float32) == sigma).all(), l1
+        assert (r["trace"]["mu_src"][0].astype(np.float32) == ms).all()
+        assert (r["trace"]["mu_dst"][0].astype(np.float32) == md).all()
+
+
+@pytest.mark.parametrize("which", [0, 1])
 def test_icp_pcl_float_within_bar_of_f64(oracle_mod, golden, which):
     """PCL's float Umeyama vs the exact solve: the reference's own float noise (documented)."""
     case = golden["cases"][which]
