@@ -268,6 +268,24 @@ CHAIN_CYCLES_PER_ADD = 6.4
 CLOCK_GHZ = 2.4
 
 
+def sigma_panels(n: int, max_kc: int = 680) -> dict:
+    """Eigen 3.3's GEMM panels of umeyama's sigma for |C| = n (icp4r_math.hpp sigma_kc, default host
+    facts: L1d 32 KiB, gebp mr 8 -> max_kc 680)."""
+    if n < 48 or n <= max_kc:
+        kc = n
+    else:
+        r = n % max_kc
+        kc = max_kc if r == 0 else max_kc - 8 * ((max_kc - 1 - r) // (8 * (n // max_kc + 1)))
+    return {"kc": kc, "panels": -(-n // kc) if kc else 0}
+
+
+def update_chain_floor_ms(n: int) -> float:
+    """Dependent-add floor of one PCL-numerics update: pass A's n-long centroid chains, then pass B's
+    panel chains (kc long, all panels at once) and the panel adds into sigma."""
+    sp = sigma_panels(n)
+    return (n + sp["kc"] + sp["panels"]) * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
+
+
 def single_pair_cpu(src, tgt, oparams: dict, budget_s: float, fitness_passes: int) -> dict:
     """The oracle on one pinned core, the node's call: align (+ its getFitnessScore) and, for the
     icp4radar node, the second getFitnessScore (`iterative_closest_point.cpp:516,:520`)."""
@@ -355,20 +373,36 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
     if hbm_formula:
         # SURVEY §8(d) hash-grid formula per NN launch: queries in (16 B) + key out (8 B) + 16 B per
         # examined target (sum_q K_q) + 24 B per box tested (lo/hi xyz) — every examination priced as a
-        # fresh read.  nn_tile_kernel stages each target tile in LDS once per workgroup, so these are
-        # algorithmic bytes, not traffic: `traffic` above is the measured HBM bytes.
+        # fresh read.  nn_tile_kernel stages each target tile in LDS once per workgroup and re-reads it
+        # from there, so these are candidate bytes, not HBM traffic: the HBM fraction is `hbm_counter`
+        # (the FETCH / WRITE counters of this build), this one is labelled as what it is.
         b = n * (16 + 8) + 16 * evals + 24 * tests
         a = b / (nn_ms * 1e-3) / 1e9 if nn_ms > 0 else 0.0
-        roof["hbm_formula"] = {"bytes_per_launch": b, "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                               "frac": a / PEAK_HBM_GBS}
-    floor_ms = 2 * n * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
+        roof["candidate_bytes_lds_reused"] = {"bytes_per_launch": b, "rate_gbs": a,
+                                              "note": "SURVEY 8(d) hash-grid formula; LDS re-reads, not HBM"}
+    if traffic is not None and nn_ms > 0:
+        roof["hbm_counter"] = {"achieved": traffic / (nn_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": traffic / (nn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+    floor_ms = update_chain_floor_ms(n)
+    update = {"bound": "latency", "kernel": "fold_update_kernel", "achieved": floor_ms, "peak": upd_ms, "unit": "ms",
+              "frac": floor_ms / upd_ms if upd_ms > 0 else None, "chain_floor_ms": floor_ms, "avg_launch_ms": upd_ms,
+              "launches_per_registration": upd_launches / max(calls, 1),
+              "share_of_device_time": upd_ms * upd_launches / max(calls, 1) / dev_ms if dev_ms > 0 else None,
+              "sigma_panels": sigma_panels(n),
+              "note": "PCL's summation order: pass A's n-long sequential centroid chains, then pass B's "
+                      "sigma chains of one Eigen GEMM panel (kc) each plus the panel adds; achieved / peak = "
+                      "that dependent-add floor / the launch's time (DESIGN.md §5)"}
+    upd_traffic, upd_note = pmc_traffic(name, "fold_update_kernel", sha)
+    update["traffic"], update["traffic_source"] = upd_traffic, upd_note
+    roof["share_of_device_time"] = nn_ms * nn_launches / max(calls, 1) / dev_ms if dev_ms > 0 else None
+    # `roofline` prices the kernel with the larger share of the registration's device time (the top row
+    # of profiles/<round>/kernel_stats_<config>.csv), the other one sits beside it
+    nn_first = (roof["share_of_device_time"] or 0) >= (update["share_of_device_time"] or 0)
     out = {"workload": workload, "value": 1e3 / dev_ms if dev_ms > 0 else None, "unit": "pairs/s",
            "registration_device_ms": dev_ms, "registration_wall_ms_incl_pcie": 1e3 * float(np.median(walls)),
-           "status": int(r.status), "iterations": iters, "plan": plan, "roofline": roof,
-           "update_kernel": {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms,
-                             "launches_per_registration": upd_launches / max(calls, 1),
-                             "bound": "latency: sequential float fold chains (PCL's summation order)",
-                             "chain_floor_ms": floor_ms, "frac_of_floor": floor_ms / upd_ms if upd_ms > 0 else None},
+           "status": int(r.status), "iterations": iters, "plan": plan,
+           "roofline": roof if nn_first else update,
+           ("update_kernel" if nn_first else "nn_kernel"): update if nn_first else roof,
            "nn_plus_update_share_of_device_time": (nn_ms * nn_launches + upd_ms * upd_launches) / max(calls, 1) / dev_ms
            if dev_ms > 0 else None}
     _check_and_cpu(ctx, out, r, src, tgt, params, oparams, cpu_budget_s, fitness_passes, check)
@@ -408,7 +442,7 @@ def _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_
     evals = st["evaluations"] / per
     tests = st["box_tests"] / per
     flops = evals * FLOP_PER_PAIR_EVAL + tests * FLOP_PER_BOX_TEST
-    floor_ms = (2 * n * iters + n) * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
+    floor_ms = iters * update_chain_floor_ms(n) + n * CHAIN_CYCLES_PER_ADD / (CLOCK_GHZ * 1e6)
     tflops = flops / (solo_ms * 1e-3) / 1e12 if solo_ms > 0 else 0.0
     roof = {"bound": "latency", "kernel": "solo_kernel", "achieved": floor_ms, "peak": solo_ms, "unit": "ms",
             "frac": floor_ms / solo_ms if solo_ms > 0 else None, "chain_floor_ms": floor_ms,

@@ -545,6 +545,9 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // nn_order_kernel)
     const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
     const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
+    // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
+    // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)
+    const bool wide = pcl && !fuse && npairs <= ctx->ncu && env_int("ICP4R_WIDE_UPDATE", 1) != 0;
     char pass_name[48];
     for (int it = 0; it < iters; ++it) {
         snprintf(pass_name, sizeof(pass_name), "icp4r ICP pass %d", it + 1);
@@ -560,7 +563,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
                 HIP_TRY(hipEventRecord(ue->start, gs[g]));
             }
             HIP_TRY(launch_update(ag[g], wg[g], gn[g], mn, pcl && !pl.pruned, gs[g], fuse && it + 1 < iters,
-                                  ford && it + 1 < iters ? ncu_g : 0));
+                                  ford && it + 1 < iters ? ncu_g : 0, wide));
             if (kev) HIP_TRY(hipEventRecord(ue->stop, gs[g]));
         }
     }

@@ -198,9 +198,12 @@ constexpr int kLdsMaxTargets = 8192;  // nn_lds_kernel: whole target set in LDS
 constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this many pairs
 constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
 constexpr int kSoloMaxN = 1024;           // solo_kernel by default for single pairs of at most this many sources
+// wide: one 1024-thread workgroup per pair (fold_update_wide_kernel) — plans with at most one pair
+// per CU and neither the fused test nor the fused work list
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr,
                          hipStream_t st, int tail_test = 0,
-                         int order_ncu = 0);  // > 0: the launch also builds the next pass's work list
+                         int order_ncu = 0,  // > 0: the launch also builds the next pass's work list
+                         bool wide = false);
 // solo_kernel: every iteration and the fitness pass of each pair in one workgroup (PCL numerics,
 // targets <= kLdsMaxTargets, sources <= kCacheMaxN; after launch_init and launch_index)
 hipError_t launch_solo(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, int iters, hipStream_t st);

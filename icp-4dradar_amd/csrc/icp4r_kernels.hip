@@ -2844,6 +2844,36 @@ __device__ __forceinline__ void load_group(float4 (&g)[8], const float* f) {
     for (int u = 0; u < 8; ++u) g[u] = *reinterpret_cast<const float4*>(f + 4 * u);
 }
 
+// The last < 32 elements of a chain segment: groups of 8 loaded one group ahead, then up to 7 loaded
+// together (a dependent scalar loop would wait out one LDS round trip per element — the panel ends of
+// pass B cut segments at arbitrary positions).  f needs no alignment.
+template <typename TAcc>
+__device__ __forceinline__ TAcc fold_tail(const float* f, int len, TAcc acc) {
+    int k = 0;
+    if (len >= 4) {
+        float a0 = f[0], a1 = f[1], a2 = f[2], a3 = f[3];
+        for (; k + 4 <= len; k += 4) {
+            const int nx = (k + 8 <= len) ? k + 4 : k;  // the next group, or a harmless re-read
+            const float b0 = f[nx], b1 = f[nx + 1], b2 = f[nx + 2], b3 = f[nx + 3];
+            __builtin_amdgcn_sched_barrier(0);
+            acc = acc + (TAcc)a0;
+            acc = acc + (TAcc)a1;
+            acc = acc + (TAcc)a2;
+            acc = acc + (TAcc)a3;
+            a0 = b0;
+            a1 = b1;
+            a2 = b2;
+            a3 = b3;
+        }
+    }
+    const int r = len - k;  // 0..3, loaded together
+    const float v0 = f[k], v1 = f[k + (r > 1 ? 1 : 0)], v2 = f[k + (r > 2 ? 2 : 0)];
+    if (r > 0) acc = acc + (TAcc)v0;
+    if (r > 1) acc = acc + (TAcc)v1;
+    if (r > 2) acc = acc + (TAcc)v2;
+    return acc;
+}
+
 #ifndef ICP4R_FOLD_AHEAD
 #define ICP4R_FOLD_AHEAD 2  // groups of 32 floats in flight ahead of the adds (1 or 2)
 #endif
@@ -2878,8 +2908,7 @@ __device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
                 k += 32;
             }
         }
-        for (; k < len; ++k) acc = acc + (TAcc)f[k];
-        return acc;
+        return k < len ? fold_tail<TAcc>(f + k, len - k, acc) : acc;
     }
     if (len >= 32) {
         float4 a[8], b[8];
@@ -2902,8 +2931,100 @@ __device__ __forceinline__ TAcc fold_seq(const float* f, int len, TAcc acc) {
             k += 32;
         }
     }
-    for (; k < len; ++k) acc = acc + (TAcc)f[k];
+    return k < len ? fold_tail<TAcc>(f + k, len - k, acc) : acc;
+}
+
+// fold_seq with the chain switched at element xa (a wave-uniform multiple of 32): groups before it go
+// to acc, the rest to acc2 — a panel end of pass B inside a chunk (the fillers padded the ending
+// panel to xa with +0).  One three-group rotation over the whole row: the loads stay in flight across
+// the switch, which is a scalar branch per group.
+template <typename TAcc>
+__device__ __forceinline__ void fold_seq_switch(const float* f, int len, int xa, TAcc& acc, TAcc& acc2) {
+    xa = __builtin_amdgcn_readfirstlane(xa);
+    auto add = [&](int k, const float4 (&g)[8]) __attribute__((always_inline)) {
+        if (k < xa)
+            add_group(acc, g);
+        else
+            add_group(acc2, g);
+    };
+    int k = 0;
+    if (len >= 96) {
+        float4 a[8], b[8], c[8];
+        load_group(a, f);
+        load_group(b, f + 32);
+        for (; k + 96 <= len; k += 96) {
+            const int n1 = (k + 128 <= len) ? k + 96 : 0, n2 = (k + 160 <= len) ? k + 128 : 0;
+            load_group(c, f + k + 64);
+            __builtin_amdgcn_sched_barrier(0);
+            add(k, a);
+            load_group(a, f + n1);
+            __builtin_amdgcn_sched_barrier(0);
+            add(k + 32, b);
+            load_group(b, f + n2);
+            __builtin_amdgcn_sched_barrier(0);
+            add(k + 64, c);
+        }
+        if (k + 32 <= len) {
+            add(k, a);
+            k += 32;
+            if (k + 32 <= len) {
+                add(k, b);
+                k += 32;
+            }
+        }
+    } else {
+        for (; k + 32 <= len; k += 32) {
+            float4 a[8];
+            load_group(a, f + k);
+            add(k, a);
+        }
+    }
+    if (k < len) {  // the last < 32 elements belong to the second chain (xa <= the last group's start)
+        if (k < xa)
+            acc = fold_tail<TAcc>(f + k, len - k, acc);
+        else
+            acc2 = fold_tail<TAcc>(f + k, len - k, acc2);
+    }
+}
+
+// Elements [lo, hi) (0 <= lo <= hi <= 32, wave-uniform) of the 32-float window g (16-B aligned), in
+// order: the window in one round trip, the adds behind scalar branches.
+template <typename TAcc>
+__device__ __forceinline__ TAcc fold_window(const float* g, int lo, int hi, TAcc acc) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(g + 4 * u);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        if (4 * u + 0 >= lo && 4 * u + 0 < hi) acc = acc + (TAcc)v[u].x;
+        if (4 * u + 1 >= lo && 4 * u + 1 < hi) acc = acc + (TAcc)v[u].y;
+        if (4 * u + 2 >= lo && 4 * u + 2 < hi) acc = acc + (TAcc)v[u].z;
+        if (4 * u + 3 >= lo && 4 * u + 3 < hi) acc = acc + (TAcc)v[u].w;
+    }
     return acc;
+}
+
+// fold_seq over row[a, b) of a 16-B aligned LDS row (a, b wave-uniform): the partial 32-float windows
+// at either end in one round trip each, the whole windows between them by fold_seq.
+#ifndef ICP4R_SPAN_WINDOW
+#define ICP4R_SPAN_WINDOW 0
+#endif
+template <typename TAcc>
+__device__ __forceinline__ TAcc fold_span(const float* row, int a, int b, TAcc acc) {
+    if (!ICP4R_SPAN_WINDOW) {  // up to 3 leading elements until row + a is aligned, then fold_seq
+        const int a4 = min(b, (a + 3) & ~3);
+        if (a < a4) acc = fold_tail<TAcc>(row + a, a4 - a, acc);
+        return a4 < b ? fold_seq<TAcc>(row + a4, b - a4, acc) : acc;
+    }
+    if (b <= a) return acc;
+    const int w0 = a & ~31;
+    if (b <= w0 + 32) return fold_window<TAcc>(row + w0, a - w0, b - w0, acc);
+    if (a > w0) acc = fold_window<TAcc>(row + w0, a - w0, 32, acc);
+    const int m0 = a > w0 ? w0 + 32 : w0, m1 = b & ~31;
+    if (m1 > m0) acc = fold_seq<TAcc>(row + m0, m1 - m0, acc);
+    return b > m1 ? fold_window<TAcc>(row + m1, 0, b - m1, acc) : acc;
 }
 
 // The double chains (PCL's MSE sum and getFitnessScore) over values the fillers stored as doubles:
@@ -2977,6 +3098,7 @@ struct SolveShared {
     float mean[6];
     float one_over_n;
     int32_t bnd[16];  // pass B with rejected correspondences: the group's panel starts (point index)
+    int32_t wsum[16];  // (its scan's per-wave counts)
     double mse_sum;
     float T_inc[16];
     int32_t flag;  // 0 continue, 1 error (no transform), 2 converged after this transform
@@ -3636,34 +3758,37 @@ __device__ __forceinline__ void fold_bounds(int n, int kc, int S, int s0, int G,
     __syncthreads();
 }
 
-// A panel chain's step over one chunk row (len <= T floats, 16-B aligned): groups of 8 floats, the
-// next group's two ds_read_b128 issued before this group's adds (few registers: the fold lanes of the
-// panel groups share their waves' allocation with the fillers).
+// A panel chain's step over one chunk row (len <= T floats, T a multiple of 8; 16-B aligned): groups
+// of 16 floats, the next group's four ds_read_b128 issued before this group's 16 dependent adds (as
+// long as the LDS round trip), the rest through fold_tail — half fold_seq's registers: the panel fold
+// lanes share their waves' allocation with the fillers.
 __device__ __forceinline__ float fold_row(const float* f, int len, float acc) {
     int k = 0;
-    if (len >= 8) {
-        float4 a0 = *reinterpret_cast<const float4*>(f), a1 = *reinterpret_cast<const float4*>(f + 4);
-        for (; k + 8 <= len; k += 8) {
-            const int nx = (k + 16 <= len) ? k + 8 : k;  // the next group, or a harmless re-read
-            const float4 b0 = *reinterpret_cast<const float4*>(f + nx), b1 = *reinterpret_cast<const float4*>(f + nx + 4);
+    if (len >= 16) {
+        float4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
+        for (; k + 16 <= len; k += 16) {
+            const int nx = (k + 32 <= len) ? k + 16 : k;  // the next group, or a harmless re-read
+            float4 b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + nx + 4 * u);
             __builtin_amdgcn_sched_barrier(0);
-            acc = acc + a0.x;
-            acc = acc + a0.y;
-            acc = acc + a0.z;
-            acc = acc + a0.w;
-            acc = acc + a1.x;
-            acc = acc + a1.y;
-            acc = acc + a1.z;
-            acc = acc + a1.w;
-            a0 = b0;
-            a1 = b1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = acc + a[u].x;
+                acc = acc + a[u].y;
+                acc = acc + a[u].z;
+                acc = acc + a[u].w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = b[u];
         }
     }
-    for (; k < len; ++k) acc = acc + f[k];
-    return acc;
+    return k < len ? fold_tail<float>(f + k, len - k, acc) : acc;
 }
 
-template <int WG, int CH, int ROW>
+template <int WG, int CH, int ROW, bool PAR>
 __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], SolveShared& s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool weighted = kp.huber_delta < INFINITY;
@@ -3709,54 +3834,178 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
 #pragma unroll
             for (int rb = 0; rb < 3; ++rb) pr[ra * 3 + rb] = weighted ? (wt * dv[ra]) * sv[rb] : dv[ra] * sv[rb];
     };
-    if (S <= 1) {
-        // one panel: the 9 chains over every point, wave 0 lanes 0..8
-        const int nch = (n + CH - 1) / CH;
-        constexpr int kFillB = WG - 64, kPerB = (CH + kFillB - 1) / kFillB;
-        auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
-            const int base = c * CH, len = min(CH, n - base);
+    // every correspondence kept and unweighted (PCL's defaults): the products need no distance
+    const bool plain = !weighted && !(kp.max_d2 < INFINITY);
+    auto products_plain = [&](const float4& r0, const float4& r1, float (&pr)[9]) __attribute__((always_inline)) {
+        const float sv[3] = {r0.x - ms[0], r0.y - ms[1], r0.z - ms[2]};
+        const float dv[3] = {r1.x - md[0], r1.y - md[1], r1.z - md[2]};
 #pragma unroll
-            for (int e = 0; e < kPerB; ++e) {
-                const int i = base + min(tid - 64 + e * kFillB, len - 1);
-                rec(i, r[e][0], r[e][1]);
-            }
-        };
-        auto store_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {  // waves 1..
-            float(*b)[ROW] = buf[c & 1];
-            const int base = c * CH, len = min(CH, n - base);
+        for (int ra = 0; ra < 3; ++ra)
 #pragma unroll
-            for (int e = 0; e < kPerB; ++e) {
-                const int o = tid - 64 + e * kFillB;
-                if (o >= len) break;
-                float pr[9];
-                products(r[e][0], r[e][1], pr);
+            for (int rb = 0; rb < 3; ++rb) pr[ra * 3 + rb] = dv[ra] * sv[rb];
+    };
+    if (!PAR || S <= 1) {
+        // SEQ: wave 0 lanes 0..8 fold the 9 chains over the points of panels [0, npe) of the range
+        // (panel k: [pb(k), pb(k + 1))) in point order, in chunks of CB from pb(0); at each panel end
+        // sigma += one_over_n * chain and the chain restarts from +0 — Eigen's panel order with one
+        // lane per coefficient, the chain as long as the old single chain and the chunks about as many
+        // (a chunk's staging costs a round trip: chunks are not cut at panel ends).  A panel end
+        // inside a chunk: the fillers pad the ending panel's rows with +0 up to the next multiple of 32
+        // and shift the new panel's products behind it, so both chains run fold_seq from aligned
+        // offsets in whole groups (a remainder would wait out an LDS round trip per few elements).
+        // Two panel ends in one chunk (kc < CB only) take the unpadded slow path (fold_span).
+        constexpr int CB = ROW - kFoldPad - 32;  // points per chunk: room for the pad
+        constexpr int kFillB = WG - 64, kPerB = (CB + kFillB - 1) / kFillB;
+        float sig = 0.0f, sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b) and the open panel's chain
+        auto seq = [&](auto pb, int npe) __attribute__((always_inline)) {
+            const int p0 = pb(0), p1 = pb(npe);
+            const int nch = (p1 - p0 + CB - 1) / CB;
+            // the chunk's first panel end strictly inside it (xs, relative; INT_MAX: none) and whether
+            // a second one follows inside it; (k, nb): the next panel end >= the chunk's start
+            auto split_of = [&](int c0, int c1, int k, int nb, int& xs, bool& multi) {
+                xs = nb < c1 ? nb - c0 : INT_MAX;
+                multi = nb < c1 && k + 1 <= npe && pb(k + 1) < c1;
+            };
+            auto past = [&](int c1, int& k, int& nb) {  // the cursor past every panel end <= c1
+                while (nb <= c1) {
+                    ++k;
+                    nb = k <= npe ? pb(k) : INT_MAX;
+                }
+            };
+            auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
+                const int base = p0 + c * CB, len = min(CB, p1 - base);
 #pragma unroll
-                for (int k = 0; k < 9; ++k) b[k][o] = pr[k];
-            }
-        };
-        float sacc = 0.0f;  // lane a*3+b of wave 0: the chain of sigma(a, b)
-        if (wv == 0) {
-            for (int c = 0; c < nch; ++c) {
-                __syncthreads();
-                if (lane < 9) sacc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), sacc);
-            }
-        } else {
-            if (nch > 0) {
-                float4 r[kPerB][2];
-                load_b(0, r);
-                store_b(0, r);
-            }
-            for (int c = 0; c < nch; ++c) {
-                __syncthreads();
-                if (c + 1 < nch) {
+                for (int e = 0; e < kPerB; ++e) {
+                    const int i = base + min(tid - 64 + e * kFillB, len - 1);
+                    rec(i, r[e][0], r[e][1]);
+                }
+            };
+            auto store_b = [&](int c, float4 (&r)[kPerB][2], int xs, bool multi) __attribute__((always_inline)) {
+                float(*b)[ROW] = buf[c & 1];
+                const int base = p0 + c * CB, len = min(CB, p1 - base);
+                const int padx = (!multi && xs != INT_MAX) ? ((xs + 31) & ~31) - xs : 0;
+                if (plain) {
+#pragma unroll
+                    for (int e = 0; e < kPerB; ++e) {
+                        const int o = tid - 64 + e * kFillB;
+                        if (o >= len) break;
+                        float pr[9];
+                        products_plain(r[e][0], r[e][1], pr);
+                        const int at = o < xs ? o : o + padx;
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) b[k][at] = pr[k];
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < kPerB; ++e) {
+                        const int o = tid - 64 + e * kFillB;
+                        if (o >= len) break;
+                        float pr[9];
+                        products(r[e][0], r[e][1], pr);
+                        const int at = o < xs ? o : o + padx;
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) b[k][at] = pr[k];
+                    }
+                }
+                if (tid - 64 < padx)
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) b[k][xs + tid - 64] = 0.0f;
+            };
+            if (wv == 0) {
+                int k = 1, nb = pb(1);  // the next panel end
+                for (int c = 0; c < nch; ++c) {
+                    __syncthreads();
+                    const int c0 = p0 + c * CB, c1 = min(c0 + CB, p1);
+                    const float* row = buf[c & 1][lane < 9 ? lane : 0];
+                    int xs;
+                    bool multi;
+                    split_of(c0, c1, k, nb, xs, multi);
+                    if (!multi) {
+                        if (xs == INT_MAX) {
+                            if (lane < 9) sacc = fold_seq<float>(row, c1 - c0, sacc);
+                        } else {
+                            const int xa = (xs + 31) & ~31;
+                            if (lane < 9) {
+                                // [0, xs) and the +0 pad into the ending chain, the rest into a new one
+                                float acc2 = 0.0f;
+                                fold_seq_switch<float>(row, xa + (c1 - c0 - xs), xa, sacc, acc2);
+                                sig = sig + oon * sacc;  // res(i, j) += alpha * C0 into the zeroed sigma
+                                sacc = acc2;
+                            }
+                            ++k;
+                            nb = k <= npe ? pb(k) : INT_MAX;
+                        }
+                        if (nb == c1) {  // a panel ends with the chunk
+                            if (lane < 9) sig = sig + oon * sacc;
+                            sacc = 0.0f;
+                            ++k;
+                            nb = k <= npe ? pb(k) : INT_MAX;
+                        }
+                    } else {
+                        int q = c0;
+                        while (nb <= c1) {
+                            if (lane < 9) {
+                                sacc = fold_span<float>(row, q - c0, nb - c0, sacc);
+                                sig = sig + oon * sacc;
+                            }
+                            sacc = 0.0f;
+                            q = nb;
+                            ++k;
+                            nb = k <= npe ? pb(k) : INT_MAX;
+                        }
+                        if (q < c1 && lane < 9) sacc = fold_span<float>(row, q - c0, c1 - c0, sacc);
+                    }
+                }
+            } else {
+                int k = 1, nb = pb(1);  // the cursor at the start of the chunk being staged
+                if (nch > 0) {
+                    int xs;
+                    bool multi;
+                    split_of(p0, min(p0 + CB, p1), k, nb, xs, multi);
                     float4 r[kPerB][2];
-                    load_b(c + 1, r);
-                    store_b(c + 1, r);
+                    load_b(0, r);
+                    store_b(0, r, xs, multi);
+                }
+                for (int c = 0; c < nch; ++c) {
+                    __syncthreads();
+                    if (c + 1 < nch) {
+                        const int c0 = p0 + (c + 1) * CB, c1 = min(c0 + CB, p1);
+                        past(c0, k, nb);
+                        int xs;
+                        bool multi;
+                        split_of(c0, c1, k, nb, xs, multi);
+                        float4 r[kPerB][2];
+                        load_b(c + 1, r);
+                        store_b(c + 1, r, xs, multi);
+                    }
                 }
             }
+            __syncthreads();  // (the buffers are reused by the next range)
+        };
+        // the panels kSliceGroup at a time: their starts in s.bnd — (s0 + k) kc when every
+        // correspondence is kept, else counted in accepted correspondences (fold_bounds)
+        const bool rejected = cnt < n && S > 1;
+        if (tid == 0) s.bnd[0] = 0;
+        __syncthreads();
+        for (int s0 = 0; s0 < S; s0 += kSliceGroup) {
+            const int G = min(kSliceGroup, S - s0);
+            if (rejected) {
+                auto accepted = [&](int i) {
+                    float4 r0, r1;
+                    rec(i, r0, r1);
+                    rec_fix(r0, r1);
+                    return !(r1.w > kp.max_d2);
+                };
+                fold_bounds<WG>(n, kc, S, s0, G, accepted, s.bnd, s.wsum);
+            } else {
+                if (tid >= 1 && tid <= G) s.bnd[tid] = (s0 + tid >= S) ? n : (s0 + tid) * kc;
+                __syncthreads();
+            }
+            seq([&](int k) { return s.bnd[k]; }, G);
+            if (tid == 0) s.bnd[0] = s.bnd[G];
+            __syncthreads();
         }
-        // res(i, j) += alpha * C0 into the zeroed sigma
-        if (wave == 0 && lane < 9) s.sigmaf[lane] = 0.0f + oon * sacc;
+        if (wave == 0 && lane < 9) s.sigmaf[lane] = sig;
         __syncthreads();
         return;
     }
@@ -3775,6 +4024,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
         const int T = stride - 4;                                 // steps per chunk (a multiple of 8)
         const int FW = (R + 63) / 64;                             // fold waves (1 or 2)
         const int nF = WG - 64 * FW;                              // fillers
+        const float invT = 1.0f / (float)T;
         if (rejected) {
             auto accepted = [&](int i) {
                 float4 r0, r1;
@@ -3782,7 +4032,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
                 rec_fix(r0, r1);
                 return !(r1.w > kp.max_d2);
             };
-            fold_bounds<WG>(n, kc, S, s0, G, accepted, s.bnd, reinterpret_cast<int32_t*>(bufs(0)));
+            fold_bounds<WG>(n, kc, S, s0, G, accepted, s.bnd, s.wsum);
         }
         // panel sl of the group covers points [start(sl), start(sl + 1))
         auto start = [&](int sl) -> int {
@@ -3802,7 +4052,10 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
 #pragma unroll
                 for (int e = 0; e < kFillBatch; ++e) {
                     const int q = me + (e0 + e) * nF;
-                    const int sl = q / T, t = q - sl * T;
+                    // q / T by a float reciprocal, corrected (exact for these small q)
+                    int sl = (int)((float)q * invT), t = q - sl * T;
+                    if (t >= T) { ++sl; t -= T; }
+                    if (t < 0) { --sl; t += T; }
                     const int i0 = sl < G ? start(sl) : n;
                     const int i1 = sl < G ? (s0 + sl + 1 >= S ? n : start(sl + 1)) : n;
                     const int i = i0 + c * T + t;
@@ -3881,7 +4134,7 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
     fold_pass_a<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
     if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(1);
-    fold_pass_b<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.s);
+    fold_pass_b<kFoldWG, kFoldChunkP, kFoldRow, false>(kp, fin, sh.buf, sh.s);
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(2);
     // the fused test's first point group is loaded, and its LDS bitmap cleared, while thread 0 solves
@@ -3945,6 +4198,16 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __shared__ FoldShared sh;
     __shared__ OrderShared osh;
     __shared__ int32_t last;
+#if ICP4R_FOLD_LDS_PAD
+    // experiment: fewer resident workgroups per CU (LDS-limited), so a pair's passes re-read its
+    // records from the Infinity Cache
+    __shared__ float lds_pad[ICP4R_FOLD_LDS_PAD];
+    if (order_ncu == -12345) {  // never true: keeps the array allocated
+        lds_pad[threadIdx.x] = (float)blockIdx.x;
+        __syncthreads();
+        w.ticks[threadIdx.x] = (uint64_t)lds_pad[ICP4R_FOLD_LDS_PAD - 1 - threadIdx.x];
+    }
+#endif
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     const int nwork = fold_update_pair(a, w, tail_test, p, sh);
     if (order_ncu <= 0) return;
@@ -3957,6 +4220,52 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __syncthreads();
     if (!last) return;
     order_items<kFoldWG, true>(a, w, (int)gridDim.x, 0, 0, order_ncu, osh);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fold_update_wide_kernel: the update of plans with at most one pair per CU (single pairs — the node's
+// per-frame call, C1 / C2 / C5 — and small batches; no fused cache test, no fused work list): one
+// 1024-thread workgroup and most of the CU's LDS per pair.  Pass A is the same sequential centroid
+// chains over larger chunks; pass B runs the sigma panels side by side (fold_pass_b<PAR>: up to 14
+// panels, 9 chains each, over chunks of 128 steps per panel), so its chain is one panel (kc) long
+// instead of |C|, and the 14 filler waves stage a chunk in one round trip.  Same results bit for bit
+// as fold_update_kernel (the parity tests run both; ICP4R_WIDE_UPDATE=0 selects the narrow one).
+constexpr int kWideWG = 1024;
+constexpr int kWideChunkP = 1792;  // points per pass-A chunk; pass B: 9 x 14 panel rows of 128 steps
+constexpr int kWideRow = kWideChunkP + kFoldPad;
+struct WideShared {
+    alignas(16) float buf[2][9][kWideRow];
+    float res[8];
+    int32_t cnt[kWideWG / 64];
+    SolveShared s;
+};
+
+__global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, WorkArgs w) {
+    __shared__ WideShared sh;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return;
+    const int tid = threadIdx.x;
+    const int n = a.src_n[p];
+    clear_need(w, p, n, tid, kWideWG);
+    const int64_t xs = w.x_stride;
+    const KParams& kp = a.kp;
+    const float4* C = w.corr ? w.corr + (int64_t)p * xs * 2 : nullptr;
+    const float4* Xp = w.X + (int64_t)p * xs;
+    const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
+    const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
+    if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
+    const FoldIn fin{C, Xp, NT, n};
+    fold_pass_a<kWideWG, kWideChunkP, kWideRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
+    if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
+    fold_pass_b<kWideWG, kWideChunkP, kWideRow, true>(kp, fin, sh.buf, sh.s);
+    if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) solve_pair<kNumericsPCL>(sh.s, st, kp);
+    __syncthreads();
+    if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
+    if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
+    if (!w.defer_xform) transform_pair<kWideWG>(w, p, n, sh.s.T_inc, w.seed_next && w.corr);
+    if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -4464,7 +4773,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
             const FoldIn fin{nullptr, w.X + xs0, w.nn_t + xs0, n};
             fold_pass_a<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, SOLO_F(sh).buf, SOLO_F(sh).res, SOLO_F(sh).cnt, SOLO_F(sh).sv);
             tick(3);
-            fold_pass_b<kSoloWG, kSoloChunk, kSoloRow>(kp, fin, SOLO_F(sh).buf, SOLO_F(sh).sv);
+            fold_pass_b<kSoloWG, kSoloChunk, kSoloRow, false>(kp, fin, SOLO_F(sh).buf, SOLO_F(sh).sv);
             tick(4);
             if (tid == 0) solve_pair<kNumericsPCL>(SOLO_F(sh).sv, st, kp);
             __syncthreads();
@@ -4719,13 +5028,16 @@ hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, 
 }
 
 hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int max_n, bool need_corr, hipStream_t st,
-                         int tail_test, int order_ncu) {
+                         int tail_test, int order_ncu, bool wide) {
     if (order_ncu > 0 && (!tail_test || !w.owork || !w.plist || !w.plist_n || !w.nn_u || a.kp.numerics != kNumericsPCL))
         return hipErrorInvalidValue;
     if (a.kp.numerics == kNumericsPCL) {
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
-        hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test, order_ncu);
+        if (wide && !tail_test && order_ncu <= 0)
+            hipLaunchKernelGGL(fold_update_wide_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+        else
+            hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test, order_ncu);
     } else {
         hipLaunchKernelGGL(update_f64_kernel, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
     }

@@ -34,7 +34,8 @@ def ticks(ctx) -> list[float]:
 
 def main():
     ctx = icp4r.Context(0)
-    p = icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+    p = icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
+                             eigen_l1_bytes=int(os.environ.get("EIGEN_L1", "0")))
     for n in (2048, 8192):
         pr = synth.make_pair(7, n)
         ctx.align(pr.src_xyzi(), pr.tgt_xyzi(), p)
