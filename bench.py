@@ -384,7 +384,8 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
         roof["hbm_counter"] = {"achieved": traffic / (nn_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": traffic / (nn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
     floor_ms = update_chain_floor_ms(n)
-    update = {"bound": "latency", "kernel": "fold_update_kernel", "achieved": floor_ms, "peak": upd_ms, "unit": "ms",
+    update = {"bound": "latency", "kernel": "fold_update_wide_kernel" if plan.get("wide_update") else "fold_update_kernel",
+              "achieved": floor_ms, "peak": upd_ms, "unit": "ms",
               "frac": floor_ms / upd_ms if upd_ms > 0 else None, "chain_floor_ms": floor_ms, "avg_launch_ms": upd_ms,
               "launches_per_registration": upd_launches / max(calls, 1),
               "share_of_device_time": upd_ms * upd_launches / max(calls, 1) / dev_ms if dev_ms > 0 else None,
@@ -392,7 +393,7 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
               "note": "PCL's summation order: pass A's n-long sequential centroid chains, then pass B's "
                       "sigma chains of one Eigen GEMM panel (kc) each plus the panel adds; achieved / peak = "
                       "that dependent-add floor / the launch's time (DESIGN.md §5)"}
-    upd_traffic, upd_note = pmc_traffic(name, "fold_update_kernel", sha)
+    upd_traffic, upd_note = pmc_traffic(name, update["kernel"], sha)
     update["traffic"], update["traffic_source"] = upd_traffic, upd_note
     roof["share_of_device_time"] = nn_ms * nn_launches / max(calls, 1) / dev_ms if dev_ms > 0 else None
     # `roofline` prices the kernel with the larger share of the registration's device time (the top row

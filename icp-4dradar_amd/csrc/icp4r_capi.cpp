@@ -1013,7 +1013,9 @@ int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_
     const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode, true, true);
     out->pruned = pl.pruned ? 1 : 0;
     out->solo = pl.solo ? 1 : 0;
-    out->reserved = 0;
+    // run_pairs' choice (PCL numerics, 256 CUs): no solo plan, no fused cache test, <= 1 pair per CU
+    const bool fuse = pl.lds && pl.cache && env_int("ICP4R_FUSE_TEST", 1) != 0;
+    out->wide_update = (!pl.solo && !fuse && npairs <= 256 && env_int("ICP4R_WIDE_UPDATE", 1) != 0) ? 1 : 0;
     out->q = pl.q;
     out->splits = pl.splits;
     out->leaf = pl.leaf;

@@ -131,7 +131,7 @@ class Batch(C.Structure):
 class PlanInfo(C.Structure):
     _fields_ = [("pruned", C.c_int32), ("q", C.c_int32), ("splits", C.c_int32), ("leaf", C.c_int32),
                 ("lds", C.c_int32), ("cache", C.c_int32), ("nn_blocks", C.c_int64), ("solo", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("wide_update", C.c_int32)]
 
 
 assert C.sizeof(Result) == 96
@@ -369,7 +369,8 @@ def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO) ->
     info = PlanInfo()
     _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, nn_mode, C.byref(info)), "icp4r_plan")
     return {"pruned": bool(info.pruned), "lds": bool(info.lds), "cache": bool(info.cache), "q": info.q, "splits": info.splits,
-            "leaf": info.leaf, "nn_blocks": info.nn_blocks, "solo": bool(info.solo)}
+            "leaf": info.leaf, "nn_blocks": info.nn_blocks, "solo": bool(info.solo),
+            "wide_update": bool(info.wide_update)}
 
 
 _default_ctx: Context | None = None

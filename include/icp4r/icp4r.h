@@ -238,7 +238,9 @@ typedef struct icp4r_plan_info {
                            1024 by default (ICP4R_SOLO=1: up to 16384), and a plan that
                            does not take the batched LDS search (fewer than 256 pairs,
                            or ICP4R_NN_LDS=0); ICP4R_SOLO=0: never                    */
-    int32_t reserved;
+    int32_t wide_update; /* 1: the PCL-numerics update runs one 1024-thread workgroup per pair
+                           (fold_update_wide_kernel: at most one pair per CU, no fused cache
+                           test); off with ICP4R_WIDE_UPDATE=0                          */
 } icp4r_plan_info;
 int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);
 
