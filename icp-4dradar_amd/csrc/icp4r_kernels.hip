@@ -3846,49 +3846,73 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
     };
     if (!PAR || S <= 1) {
         // SEQ: wave 0 lanes 0..8 fold the 9 chains over the points of panels [0, npe) of the range
-        // (panel k: [pb(k), pb(k + 1))) in point order, in chunks of CB from pb(0); at each panel end
+        // (panel k: [pb(k), pb(k + 1))) in point order, in chunks of up to CB; at each panel end
         // sigma += one_over_n * chain and the chain restarts from +0 — Eigen's panel order with one
-        // lane per coefficient, the chain as long as the old single chain and the chunks about as many
-        // (a chunk's staging costs a round trip: chunks are not cut at panel ends).  A panel end
-        // inside a chunk: the fillers pad the ending panel's rows with +0 up to the next multiple of 32
-        // and shift the new panel's products behind it, so both chains run fold_seq from aligned
-        // offsets in whole groups (a remainder would wait out an LDS round trip per few elements).
-        // Two panel ends in one chunk (kc < CB only) take the unpadded slow path (fold_span).
-        constexpr int CB = ROW - kFoldPad - 32;  // points per chunk: room for the pad
+        // lane per coefficient, the chain as long as the old single chain.  Chunks are not cut at
+        // panel ends (a chunk's staging costs a round trip).  A panel end inside a chunk: the fillers
+        // pad the ending panel's rows with +0 up to the next multiple of 32 and shift the new panel's
+        // products behind it, so one fold_seq_switch rotation runs the row in whole groups (a
+        // remainder would wait out an LDS round trip per few elements); such a chunk holds up to
+        // CB - pad points.  Two panel ends in one chunk (only when kc < CB) take the unpadded slow
+        // path (fold_span).  The chunk sequence is computed identically by the fold lanes and the
+        // fillers (uniform arithmetic), so both run the same number of barriers.
+        constexpr int CB = ROW - kFoldPad;  // row capacity (points + pad)
         constexpr int kFillB = WG - 64, kPerB = (CB + kFillB - 1) / kFillB;
         float sig = 0.0f, sacc = 0.0f;  // lane a*3+b of wave 0: sigma(a, b) and the open panel's chain
+        struct Chunk {
+            int c0, len, xs, k, nb;  // start, points, inner panel end (relative; INT_MAX: none), cursor
+            bool multi;
+        };
         auto seq = [&](auto pb, int npe) __attribute__((always_inline)) {
             const int p0 = pb(0), p1 = pb(npe);
-            const int nch = (p1 - p0 + CB - 1) / CB;
-            // the chunk's first panel end strictly inside it (xs, relative; INT_MAX: none) and whether
-            // a second one follows inside it; (k, nb): the next panel end >= the chunk's start
-            auto split_of = [&](int c0, int c1, int k, int nb, int& xs, bool& multi) {
-                xs = nb < c1 ? nb - c0 : INT_MAX;
-                multi = nb < c1 && k + 1 <= npe && pb(k + 1) < c1;
+            // chunk at c0 with the cursor (k, nb: the next panel end > c0)
+            auto make = [&](int c0, int k, int nb) -> Chunk {
+                Chunk ch;
+                ch.c0 = c0;
+                ch.k = k;
+                ch.nb = nb;
+                ch.len = min(CB, p1 - c0);
+                ch.xs = INT_MAX;
+                ch.multi = false;
+                if (nb < c0 + ch.len) {
+                    const int xs = nb - c0, xa = (xs + 31) & ~31;
+                    ch.multi = k + 1 <= npe && pb(k + 1) < c0 + ch.len;
+                    if (!ch.multi) {
+                        if (xa >= CB) {
+                            ch.len = xs;  // no room for the pad: the chunk ends with the panel
+                        } else {
+                            ch.xs = xs;
+                            ch.len = min(ch.len, CB - (xa - xs));
+                        }
+                    }
+                }
+                return ch;
             };
-            auto past = [&](int c1, int& k, int& nb) {  // the cursor past every panel end <= c1
+            auto next = [&](const Chunk& ch) -> Chunk {  // the chunk after ch (past its panel ends)
+                const int c1 = ch.c0 + ch.len;
+                int k = ch.k, nb = ch.nb;
                 while (nb <= c1) {
                     ++k;
                     nb = k <= npe ? pb(k) : INT_MAX;
                 }
+                return make(c1, k, nb);
             };
-            auto load_b = [&](int c, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
-                const int base = p0 + c * CB, len = min(CB, p1 - base);
+            auto load_b = [&](const Chunk& ch, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int e = 0; e < kPerB; ++e) {
-                    const int i = base + min(tid - 64 + e * kFillB, len - 1);
+                    const int i = ch.c0 + min(tid - 64 + e * kFillB, ch.len - 1);
                     rec(i, r[e][0], r[e][1]);
                 }
             };
-            auto store_b = [&](int c, float4 (&r)[kPerB][2], int xs, bool multi) __attribute__((always_inline)) {
+            auto store_b = [&](int c, const Chunk& ch, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
                 float(*b)[ROW] = buf[c & 1];
-                const int base = p0 + c * CB, len = min(CB, p1 - base);
-                const int padx = (!multi && xs != INT_MAX) ? ((xs + 31) & ~31) - xs : 0;
+                const int xs = ch.multi ? INT_MAX : ch.xs;
+                const int padx = xs != INT_MAX ? ((xs + 31) & ~31) - xs : 0;
                 if (plain) {
 #pragma unroll
                     for (int e = 0; e < kPerB; ++e) {
                         const int o = tid - 64 + e * kFillB;
-                        if (o >= len) break;
+                        if (o >= ch.len) break;
                         float pr[9];
                         products_plain(r[e][0], r[e][1], pr);
                         const int at = o < xs ? o : o + padx;
@@ -3899,7 +3923,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
 #pragma unroll
                     for (int e = 0; e < kPerB; ++e) {
                         const int o = tid - 64 + e * kFillB;
-                        if (o >= len) break;
+                        if (o >= ch.len) break;
                         float pr[9];
                         products(r[e][0], r[e][1], pr);
                         const int at = o < xs ? o : o + padx;
@@ -3911,24 +3935,22 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
 #pragma unroll
                     for (int k = 0; k < 9; ++k) b[k][xs + tid - 64] = 0.0f;
             };
+            Chunk ch = make(p0, 1, npe >= 1 ? pb(1) : INT_MAX);
             if (wv == 0) {
-                int k = 1, nb = pb(1);  // the next panel end
-                for (int c = 0; c < nch; ++c) {
+                int k = 1, nb = ch.nb;  // the next panel end
+                for (int c = 0; ch.c0 < p1; ++c) {
                     __syncthreads();
-                    const int c0 = p0 + c * CB, c1 = min(c0 + CB, p1);
+                    const int c0 = ch.c0, c1 = c0 + ch.len;
                     const float* row = buf[c & 1][lane < 9 ? lane : 0];
-                    int xs;
-                    bool multi;
-                    split_of(c0, c1, k, nb, xs, multi);
-                    if (!multi) {
-                        if (xs == INT_MAX) {
-                            if (lane < 9) sacc = fold_seq<float>(row, c1 - c0, sacc);
+                    if (!ch.multi) {
+                        if (ch.xs == INT_MAX) {
+                            if (lane < 9) sacc = fold_seq<float>(row, ch.len, sacc);
                         } else {
-                            const int xa = (xs + 31) & ~31;
+                            const int xa = (ch.xs + 31) & ~31;
                             if (lane < 9) {
                                 // [0, xs) and the +0 pad into the ending chain, the rest into a new one
                                 float acc2 = 0.0f;
-                                fold_seq_switch<float>(row, xa + (c1 - c0 - xs), xa, sacc, acc2);
+                                fold_seq_switch<float>(row, xa + (ch.len - ch.xs), xa, sacc, acc2);
                                 sig = sig + oon * sacc;  // res(i, j) += alpha * C0 into the zeroed sigma
                                 sacc = acc2;
                             }
@@ -3955,28 +3977,21 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
                         }
                         if (q < c1 && lane < 9) sacc = fold_span<float>(row, q - c0, c1 - c0, sacc);
                     }
+                    ch = next(ch);
                 }
             } else {
-                int k = 1, nb = pb(1);  // the cursor at the start of the chunk being staged
-                if (nch > 0) {
-                    int xs;
-                    bool multi;
-                    split_of(p0, min(p0 + CB, p1), k, nb, xs, multi);
+                if (ch.c0 < p1) {
                     float4 r[kPerB][2];
-                    load_b(0, r);
-                    store_b(0, r, xs, multi);
+                    load_b(ch, r);
+                    store_b(0, ch, r);
                 }
-                for (int c = 0; c < nch; ++c) {
+                for (int c = 0; ch.c0 < p1; ++c) {
                     __syncthreads();
-                    if (c + 1 < nch) {
-                        const int c0 = p0 + (c + 1) * CB, c1 = min(c0 + CB, p1);
-                        past(c0, k, nb);
-                        int xs;
-                        bool multi;
-                        split_of(c0, c1, k, nb, xs, multi);
+                    ch = next(ch);  // the chunk to stage: c + 1
+                    if (ch.c0 < p1) {
                         float4 r[kPerB][2];
-                        load_b(c + 1, r);
-                        store_b(c + 1, r, xs, multi);
+                        load_b(ch, r);
+                        store_b(c + 1, ch, r);
                     }
                 }
             }
