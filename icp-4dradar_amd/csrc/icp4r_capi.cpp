@@ -544,6 +544,15 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // ... and the work list of those passes is built by the update's last workgroup (ICP4R_FUSE_ORDER=0:
     // nn_order_kernel)
     const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
+    // ... and folds the next pass A's source centroid sums over the X it writes, so that pass A reads
+    // nn_t only (every correspondence kept, unweighted, no MSE criterion).  Off unless ICP4R_SUMS_TAIL=1:
+    // the three n-long chains are serial, and in pass A they run beside the other chains for free, while
+    // in the tail they lengthen the pair's critical path (C3: update 177 -> 190 us)
+    for (int g = 0; g < groups; ++g)
+        wg[g].sums_tail = (fuse && a.kp.huber_delta == INFINITY && a.kp.max_d2 >= FLT_MAX && !a.kp.need_mse &&
+                           env_int("ICP4R_SUMS_TAIL", 0) != 0)
+                              ? 1
+                              : 0;
     const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
     // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
     // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)

@@ -84,6 +84,12 @@ struct PairState {
     int32_t phase;
     int32_t status;
     int32_t ncorr;
+    // Σs of the next update's pass A (Eigen's rowwise().sum() of the moved source, in index order),
+    // folded by the previous update's fused tail over the X it wrote (fold_update_kernel: eligible
+    // registrations only — every correspondence kept, unweighted, no MSE criterion); sums_ok = 1 while
+    // they are valid for the next pass A, which then reads nn_t only
+    float sum_s[3];
+    int32_t sums_ok;
 };
 
 // NN result of one query: (float bits of d² << 32) | target index.  d² >= 0, so the unsigned order
@@ -145,6 +151,7 @@ struct WorkArgs {
     // moves X_i.
     float* nn_u;        // [npairs * x_stride] U_i
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
+    int32_t sums_tail;    // 1: the fused tail also folds the next pass A's Σs (eligible pairs: PairState)
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |
                         // the query's sorted position << 14 (nt_pack)
     float4* sq;         // [npairs * x_stride] the pass's miss list in the order the test found them: a

@@ -205,6 +205,10 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     const bool id = ident != 0;
     const int nc = min(n, (int)w.x_stride);
     int bad = 0;
+    // coordinates beyond 1e17 could square into an overflowing (inf) distance, which PCL rejects: such
+    // a pair never skips pass A's distance check (PairState::sums_ok = -1)
+    constexpr float kBig = 1e17f;
+    int big = 0;
     // (the target is only validated: 16 points per thread in flight — a scan-to-map target of 65k
     // points had taken 64 dependent rounds of 1024, ~65 us of a single registration)
     // (and its bounding box, for the Morton index of a large target: w.tbb)
@@ -217,6 +221,7 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
 #pragma unroll
         for (int e = 0; e < kTgtPer; ++e) {  // (a clamped duplicate of point m - 1 changes no extent)
             bad |= !(isfinite(t[e].x) && isfinite(t[e].y) && isfinite(t[e].z));
+            big |= fmaxf(fabsf(t[e].x), fmaxf(fabsf(t[e].y), fabsf(t[e].z))) > kBig;
             bl[0] = fminf(bl[0], t[e].x); bl[1] = fminf(bl[1], t[e].y); bl[2] = fminf(bl[2], t[e].z);
             bh[0] = fmaxf(bh[0], t[e].x); bh[1] = fmaxf(bh[1], t[e].y); bh[2] = fmaxf(bh[2], t[e].z);
         }
@@ -252,6 +257,7 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
             bad |= !(isfinite(v[e].x) && isfinite(v[e].y) && isfinite(v[e].z));
             float4 o = v[e];
             if (!id) xform_pt(Tg, v[e].x, v[e].y, v[e].z, o.x, o.y, o.z);
+            big |= fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z))) > kBig;
             if (i < nc) X[i] = o;
         }
     }
@@ -265,6 +271,7 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     if (tid == 0 && w.miss_cnt) w.miss_cnt[p] = 0;
     if (tid < 4 && p == 0 && w.plist_n) w.plist_n[tid] = 0;
     bad = __syncthreads_or(bad);
+    big = __syncthreads_or(big);
     if (tid == 0) {
         mat4_identity(st.T_inc);
         st.prev_mse = DBL_MAX;
@@ -272,6 +279,7 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
         st.conv_state = 0;
         st.iterations = 0;
         st.ncorr = 0;
+        st.sums_ok = big ? -1 : 0;
         // counts above the batch's declared max_src_n / max_tgt_n would overrun the workspace strides
         const bool too_big = n > w.x_stride || (w.leaf > 0 && m > w.t_stride);
         if (m <= 0 || bad || too_big) {
@@ -2874,6 +2882,36 @@ __device__ __forceinline__ TAcc fold_tail(const float* f, int len, TAcc acc) {
     return acc;
 }
 
+// A panel chain's step over one chunk row (len <= T floats, T a multiple of 8; 16-B aligned): groups
+// of 16 floats, the next group's four ds_read_b128 issued before this group's 16 dependent adds (as
+// long as the LDS round trip), the rest through fold_tail — half fold_seq's registers: the panel fold
+// lanes share their waves' allocation with the fillers.
+__device__ __forceinline__ float fold_row(const float* f, int len, float acc) {
+    int k = 0;
+    if (len >= 16) {
+        float4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
+        for (; k + 16 <= len; k += 16) {
+            const int nx = (k + 32 <= len) ? k + 16 : k;  // the next group, or a harmless re-read
+            float4 b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + nx + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = acc + a[u].x;
+                acc = acc + a[u].y;
+                acc = acc + a[u].z;
+                acc = acc + a[u].w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = b[u];
+        }
+    }
+    return k < len ? fold_tail<float>(f + k, len - k, acc) : acc;
+}
+
 #ifndef ICP4R_FOLD_AHEAD
 #define ICP4R_FOLD_AHEAD 2  // groups of 32 floats in flight ahead of the adds (1 or 2)
 #endif
@@ -3256,44 +3294,61 @@ struct TailFirst {
     float4 v[kPer], t[kPer];
     float U[kPer];
 };
-template <int WG, int kPer>
+// SUMS: the tail also folds the next pass A's Σs (pair_cache_test); wave 0 folds, waves 1.. test, in
+// index order.
+template <int WG, int kPer, bool SUMS = false>
 __device__ __forceinline__ int tail_group0(int n) {  // first (last-to-first) group's start
-    const int kStep = WG * kPer, ngrp = (n + kStep - 1) / kStep;
-    return (ICP4R_TAIL_REV ? ngrp - 1 : 0) * kStep;
+    constexpr int WW = SUMS ? WG - 64 : WG;
+    const int kStep = WW * kPer, ngrp = (n + kStep - 1) / kStep;
+    return (ICP4R_TAIL_REV && !SUMS ? ngrp - 1 : 0) * kStep;
 }
-template <int WG, int kPer>
+template <int WG, int kPer, bool SUMS = false>
 __device__ __forceinline__ void tail_prefetch(const WorkArgs& w, int p, int n, TailFirst<kPer>& f) {
+    constexpr int WW = SUMS ? WG - 64 : WG;
+    if (SUMS && threadIdx.x < 64) return;  // (the fold wave)
+    const int wt = SUMS ? (int)threadIdx.x - 64 : (int)threadIdx.x;
     const int64_t xs = (int64_t)p * w.x_stride;
-    const int i0 = tail_group0<WG, kPer>(n);
+    const int i0 = tail_group0<WG, kPer, SUMS>(n);
 #pragma unroll
     for (int e = 0; e < kPer; ++e) {
-        const int i = min(i0 + e * WG + (int)threadIdx.x, n - 1);
+        const int i = min(i0 + e * WW + wt, n - 1);
         f.v[e] = w.X[xs + i];
         f.t[e] = w.nn_t[xs + i];
         f.U[e] = w.nn_u[xs + i];
     }
 }
 
-template <int WG, int kPer, bool FROM_SRC>
+// SUMS (the update's tail, eligible pairs): the next pass A's Σs folded here, in index order, over the X
+// the test writes — wave 0 lanes 0..2 fold, waves 1.. test (groups of (WG - 64) * kPer points, first
+// to last, each group's new coordinates staged in `stg`: 3 rows of kSumRow floats); the sums go to
+// sums_out[0..2] (the pair state) with *sums_ok = 1.
+constexpr int kSumRow = 3 * 256 + 4;  // staged points per group (192 workers x 4) + pad
+template <int WG, int kPer, bool FROM_SRC, bool SUMS = false>
 __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
                                                 uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
                                                 int32_t* mcount, int32_t* wcnt, bool fitness, uint64_t* stamp = nullptr,
-                                                const TailFirst<kPer>* first = nullptr) {
+                                                const TailFirst<kPer>* first = nullptr, float* stg = nullptr,
+                                                float* sums_out = nullptr, int32_t* sums_ok = nullptr) {
+    static_assert(!SUMS || (WG - 64) * kPer <= kSumRow - 4, "staging rows");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int WW = SUMS ? WG - 64 : WG;  // threads that test
+    const bool worker = !SUMS || wave >= 1;
+    const int wt = SUMS ? tid - 64 : tid;
     const int64_t xs = (int64_t)p * w.x_stride;
     float4* X = w.X + xs;
     float* uu = w.nn_u + xs;
     const float4* nt = w.nn_t + xs;
     const float4* src = FROM_SRC ? a.src + a.src_off[p] : nullptr;
     NNKey* key = w.nn_key + xs;
-    constexpr int kStep = WG * kPer;
+    constexpr int kStep = WW * kPer;
     int hits = 0, misses = 0;
+    float fs = -0.0f;  // SUMS: wave 0 lane k's Σs chain (Eigen's rowwise().sum(): from the first element)
     float4 v[kPer], t[kPer], sv[kPer];
     float U[kPer];
     auto load = [&](int i0, float4 (&vv)[kPer], float4 (&tt)[kPer], float (&UU)[kPer], float4 (&ss)[kPer]) {
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
-            const int i = min(i0 + e * WG + tid, n - 1);
+            const int i = min(i0 + e * WW + wt, n - 1);
             vv[e] = X[i];
             tt[e] = nt[i];
             UU[e] = uu[i];
@@ -3305,8 +3360,8 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
     // L2 / MALL — are the pair's last ones.  (The folds must run in index order; the test may run in
     // any.)
     const int ngrp = (n + kStep - 1) / kStep;
-    auto grp0 = [&](int g) { return (ICP4R_TAIL_REV ? ngrp - 1 - g : g) * kStep; };
-    if (ngrp > 0) {
+    auto grp0 = [&](int g) { return (ICP4R_TAIL_REV && !SUMS ? ngrp - 1 - g : g) * kStep; };
+    if (ngrp > 0 && worker) {
         if (first && !FROM_SRC) {
 #pragma unroll
             for (int e = 0; e < kPer; ++e) {
@@ -3320,12 +3375,19 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
     }
     for (int g = 0; g < ngrp; ++g) {
         const int i0 = grp0(g);
+        if (SUMS && !worker) {  // the fold wave: the group's staged coordinates, in index order
+            __syncthreads();    // (B) the staging is free
+            __syncthreads();    // (A) group g staged
+            if (lane < 3) fs = fold_row(stg + lane * kSumRow, min(kStep, n - i0), fs);
+            continue;
+        }
         float4 vn[kPer], tn[kPer], sn[kPer];
         float Un[kPer];
         if (g + 1 < ngrp) load(grp0(g + 1), vn, tn, Un, sn);
+        if (SUMS) __syncthreads();  // (B) the fold wave is done with group g - 1's staging
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
-            const int i = i0 + e * WG + tid;
+            const int i = i0 + e * WW + wt;
             const bool valid = i < n;
             float4 o = v[e];
             if (FROM_SRC)
@@ -3340,6 +3402,11 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
             // the misses' search records carry their own coordinates)
             if (valid && (!fitness || a.aligned)) X[i] = o;
             if (valid && !fitness) uu[i] = Lm.y;
+            if (SUMS && valid) {
+                stg[e * WW + wt] = o.x;
+                stg[kSumRow + e * WW + wt] = o.y;
+                stg[2 * kSumRow + e * WW + wt] = o.z;
+            }
             const int k = wave_append(valid && !hit, mcount);
             if (hit) {
                 // the fitness pass' keys are read for their d² only (finish_kernel): a hit's index
@@ -3365,6 +3432,11 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
             U[e] = Un[e];
             if (FROM_SRC) sv[e] = sn[e];
         }
+        if (SUMS) __syncthreads();  // (A) group g staged
+    }
+    if (SUMS && wave == 0 && lane < 3) {
+        sums_out[lane] = fs;
+        if (lane == 0 && *sums_ok != -1) *sums_ok = 1;
     }
     hits = wave_sum(hits);
     misses = wave_sum(misses);
@@ -3488,6 +3560,8 @@ constexpr int kFoldRow = kFoldChunkP + kFoldPad;
 
 // the fused test's LDS miss records (24 B each) after the bitmap and its prefixes, in the fold buffers
 constexpr int kFoldRecs = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4) / 24) & ~15;
+// ... and with the Σs staging rows (pair_cache_test<SUMS>) at the buffers' end
+constexpr int kFoldRecsSums = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4 - 3 * kSumRow * 4) / 24) & ~15;
 struct FoldShared {
     alignas(16) float buf[2][9][kFoldRow];
     float res[8];
@@ -3546,9 +3620,12 @@ __device__ __forceinline__ void wave_exact_total(uint64_t& S, int& E) {  // ever
 // rowwise().sum(): from the first element == from -0.0f; Huber: w·x from +0) and Σw; wave 1 lane 0
 // the double MSE chain when an MSE criterion is live (else it fills); the other waves stage the next
 // chunk.  Leaves |C|, 1/n and the centroids in s.
+// sums (fold_update_kernel, eligible pairs: every correspondence kept, unweighted, no MSE criterion):
+// Σs as the previous update's tail folded it over the X it wrote — the fillers read nn_t only, and
+// lanes 0..2 do not fold.
 template <int WG, int CH, int ROW>
 __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], float* res,
-                                            int32_t* wcnt, SolveShared& s) {
+                                            int32_t* wcnt, SolveShared& s, const float* sums = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool weighted = kp.huber_delta < INFINITY;
     auto rec = [&](int i, float4& r0, float4& r1) {
@@ -3584,7 +3661,10 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int i = base + min(tid - fill0 + e * nf, len - 1);
-            rec(i, r[e][0], r[e][1]);
+            if (sums)  // nn_t only (X's centroid is known)
+                r[e][1] = f.NT[i];
+            else
+                rec(i, r[e][0], r[e][1]);
         }
     };
     auto store_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {  // waves 2, 3 (and 1 without the MSE chain)
@@ -3594,6 +3674,13 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
         for (int e = 0; e < kPerA; ++e) {
             const int o = tid - fill0 + e * nf;
             if (o >= len) break;
+            if (sums) {  // every correspondence kept, unweighted: Σd and Σw rows only
+#pragma unroll
+                for (int k = 0; k < 3; ++k) b[3 + k][o] = (&r[e][1].x)[k];
+                b[6][o] = 1.0f;
+                ++cnt;
+                continue;
+            }
             rec_fix(r[e][0], r[e][1]);
             const float d2 = r[e][1].w;
             const float sv[6] = {r[e][0].x, r[e][0].y, r[e][0].z, r[e][1].x, r[e][1].y, r[e][1].z};
@@ -3619,9 +3706,10 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     // fold lanes' register groups and the fillers' in-flight records are never live together.
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     if (wv == 0) {
+        const int lane0 = sums ? 3 : 0;
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (lane < 7) acc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), acc);
+            if (lane >= lane0 && lane < 7) acc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), acc);
         }
     } else if (wv * 64 < fill0) {  // the MSE sum: its exact form, the whole wave per chunk
         uint64_t xs = 0;
@@ -3654,7 +3742,7 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
     if (lane == 0) wcnt[wave] = cnt;
-    if (wave == 0 && lane < 7) res[lane] = acc;
+    if (wave == 0 && lane < 7) res[lane] = (sums && lane < 3) ? sums[lane] : acc;
     if (wave == 1 && lane == 0) s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
     __syncthreads();
     if (tid == 0) {
@@ -3758,36 +3846,6 @@ __device__ __forceinline__ void fold_bounds(int n, int kc, int S, int s0, int G,
     __syncthreads();
 }
 
-// A panel chain's step over one chunk row (len <= T floats, T a multiple of 8; 16-B aligned): groups
-// of 16 floats, the next group's four ds_read_b128 issued before this group's 16 dependent adds (as
-// long as the LDS round trip), the rest through fold_tail — half fold_seq's registers: the panel fold
-// lanes share their waves' allocation with the fillers.
-__device__ __forceinline__ float fold_row(const float* f, int len, float acc) {
-    int k = 0;
-    if (len >= 16) {
-        float4 a[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
-        for (; k + 16 <= len; k += 16) {
-            const int nx = (k + 32 <= len) ? k + 16 : k;  // the next group, or a harmless re-read
-            float4 b[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + nx + 4 * u);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                acc = acc + a[u].x;
-                acc = acc + a[u].y;
-                acc = acc + a[u].z;
-                acc = acc + a[u].w;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = b[u];
-        }
-    }
-    return k < len ? fold_tail<float>(f + k, len - k, acc) : acc;
-}
-
 template <int WG, int CH, int ROW, bool PAR>
 __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, float (*buf)[9][ROW], SolveShared& s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3835,7 +3893,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
             for (int rb = 0; rb < 3; ++rb) pr[ra * 3 + rb] = weighted ? (wt * dv[ra]) * sv[rb] : dv[ra] * sv[rb];
     };
     // every correspondence kept and unweighted (PCL's defaults): the products need no distance
-    const bool plain = !weighted && !(kp.max_d2 < INFINITY);
+    const bool plain = !weighted && cnt >= n;  // (nothing rejected in this iteration)
     auto products_plain = [&](const float4& r0, const float4& r1, float (&pr)[9]) __attribute__((always_inline)) {
         const float sv[3] = {r0.x - ms[0], r0.y - ms[1], r0.z - ms[2]};
         const float dv[3] = {r1.x - md[0], r1.y - md[1], r1.z - md[2]};
@@ -4146,7 +4204,12 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
 #define WG_TICK(k)
 #endif
     const FoldIn fin{C, Xp, NT, n};
-    fold_pass_a<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
+    // the previous tail folded this pass A's Σs (w.sums_tail: eligible registrations; the flag is the
+    // pair's, set only by a tail that ran)
+    const bool sums_tail = w.sums_tail && tail_test && w.nn_u && !C;  // (launch-uniform)
+    const bool use_sums = sums_tail && uload(&st.sums_ok) == 1;
+    fold_pass_a<kFoldWG, kFoldChunkP, kFoldRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s, use_sums ? st.sum_s : nullptr);
+    if (use_sums && tid == 0) st.sums_ok = 0;
     if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(1);
     fold_pass_b<kFoldWG, kFoldChunkP, kFoldRow, false>(kp, fin, sh.buf, sh.s);
@@ -4158,7 +4221,9 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
     TailFirst<ICP4R_TAIL_PER> tf;
     uint32_t* need = reinterpret_cast<uint32_t*>(&sh.buf[0][0][0]);  // the fold buffers are free now
     if (tail) {
-        tail_prefetch<kFoldWG, ICP4R_TAIL_PER>(w, p, n, tf);
+        // (the Σs-folding tail loads its first group itself: a second prefetch layout held across the
+        // solve spilled to scratch)
+        if (!sums_tail) tail_prefetch<kFoldWG, ICP4R_TAIL_PER>(w, p, n, tf);
         for (int k = tid; k < ((n + 31) >> 5); k += kFoldWG) need[k] = 0u;
         if (tid == 0) sh.mcount = 0;
     }
@@ -4177,7 +4242,7 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
         // the fold buffers: the bitmap (cleared above), its word prefixes and the LDS miss records
         int32_t* pre = reinterpret_cast<int32_t*>(need + kNeedWords);
         float4* lv = reinterpret_cast<float4*>(pre + kNeedWords);
-        uint2* lm = reinterpret_cast<uint2*>(lv + kFoldRecs);
+        uint2* lm = reinterpret_cast<uint2*>(lv + (sums_tail ? kFoldRecsSums : kFoldRecs));
         float T[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) T[q] = sh.s.T_inc[q];
@@ -4186,8 +4251,16 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
 #else
         uint64_t* stamp = nullptr;
 #endif
-        nwork = pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs, &sh.mcount,
-                                                                sh.cnt, false, stamp, &tf);
+        if (sums_tail) {
+            // the staging rows of the Σs fold at the end of the fold buffers, the miss records before
+            float* stg = reinterpret_cast<float*>(&sh.buf[0][0][0]) + (2 * 9 * kFoldRow - 3 * kSumRow);
+            nwork = pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false, true>(
+                a, w, p, n, T, need, pre, lv, lm, kFoldRecsSums, &sh.mcount, sh.cnt, false, stamp, nullptr, stg,
+                st.sum_s, &st.sums_ok);
+        } else {
+            nwork = pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false>(a, w, p, n, T, need, pre, lv, lm, kFoldRecs,
+                                                                    &sh.mcount, sh.cnt, false, stamp, &tf);
+        }
     }
     if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
     WG_TICK(4);

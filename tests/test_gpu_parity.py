@@ -384,6 +384,30 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
         assert out["1"][k]["iterations"] == o["iterations"]
 
 
+@pytest.mark.parametrize("kw", [{}, {"max_correspondence_distance": 1.0}, {"huber_delta": 0.5}])
+def test_sums_tail_identical(gpu_ctx, oracle_mod, kw, monkeypatch):
+    """The fused tail folding the next pass A's source centroid sums (ICP4R_SUMS_TAIL, eligible
+    registrations: every correspondence kept, unweighted, no MSE criterion; the other two
+    parametrisations are ineligible and must take the normal pass A): bit-identical batches either
+    way, and the oracle on sampled pairs."""
+    import icp4r
+
+    shapes = [(2048, 2048)] * 240 + [(3000, 2500), (700, 2048), (2048, 900)] * 8
+    pairs = [_pair(1700 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    args = _batch(pairs)
+    assert icp4r.plan(len(pairs), 3000, 2500)["lds"]
+    fixed = dict(max_iterations=15, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, **kw)
+    p = icp4r.default_params(**fixed)
+    out = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("ICP4R_SUMS_TAIL", on)
+        out[on] = gpu_ctx.align_batch_host(*args, params=p)
+    assert out["1"].tobytes() == out["0"].tobytes()
+    for k in (0, 239, 240, 242):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, **fixed)
+        assert (out["1"][k]["T"].reshape(4, 4).T == o["T"]).all() and out["1"][k]["fitness"] == o["fitness"]
+
+
 @pytest.mark.parametrize("npairs", [1, 300])
 def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
     """Sources ordered by descending their target's kd tree (src_order_kernel; the batched plan's default) or by their
