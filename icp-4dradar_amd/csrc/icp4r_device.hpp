@@ -88,6 +88,29 @@ __device__ __forceinline__ float wave_maxf(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
+// Write-through stores (experiment, ICP4R_WT bit mask: 1 = the fused test's stores, 2 = the batched
+// search's result stores): `sc1` vector stores leave no dirty line in the XCD's L2, so the kernel
+// boundary has less to write back (MI355X_MICROARCH.md §kernel boundary: + dirty bytes / 6 TB/s).
+#ifndef ICP4R_WT
+#define ICP4R_WT 0
+#endif
+template <int BIT>
+__device__ __forceinline__ void st_v4(float4* p, const float4 v) {
+    if constexpr ((ICP4R_WT & BIT) != 0) {
+        const v4f x = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+    } else {
+        *p = v;
+    }
+}
+template <int BIT, typename T>
+__device__ __forceinline__ void st_sc(T* p, const T v) {  // 4 or 8 bytes
+    if constexpr ((ICP4R_WT & BIT) != 0)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 // Box pruning is conservative in float: a box lower bound is shrunk by 2^-16 before its `<=` test
 // against a d², which covers the few-ulp rounding of both the bound and l2_simple.
 constexpr float kLbShrink = 1.0f - 1.0f / 65536.0f;

@@ -1756,6 +1756,7 @@ __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, const float 
 #define ICP4R_SB_BATCH 1  // candidate superblocks tested together per traversal step
 #endif
 constexpr int kSbBatch = ICP4R_SB_BATCH;
+
 static_assert(kSbBatch >= 1 && kSbBatch <= 5, "six bits per superblock in a 32-bit pack");
 struct LdsNN {
     v4f tl[kLdsTargets];                               // 128 KB: the pair's targets, index order
@@ -2082,16 +2083,21 @@ struct LdsTile {
 // and load lane l's superblock box into isl / ish (kept in registers for every run).  Every load is
 // issued before the first store: a load-store loop waited out one global round trip per target (8
 // per thread, ~10-20 us per item under load).  The caller's barrier makes the LDS visible.
+// A pair's tile in registers (every load issued, nothing waited for): tile_load, then tile_store.
 template <int WG>
-__device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w, int p, int nsb, v4f& isl, v4f& ish) {
+struct TileRegs {
+    v4f tv[kLdsTargets / WG];
+    v4f blo, bhi, isl, ish;
+};
+template <int WG>
+__device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, TileRegs<WG>& r) {
     const int tid = threadIdx.x, lane = tid & 63;
     const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
     const int nt = nsb * kSuper * kLdsLeaf;
     constexpr int kPerT = kLdsTargets / WG;
     static_assert(kLdsTargets % WG == 0, "targets per thread");
-    v4f tv[kPerT];
 #pragma unroll
-    for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * WG, nt - 1)];
+    for (int k = 0; k < kPerT; ++k) r.tv[k] = tsg[min(tid + k * WG, nt - 1)];
     const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
     const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
     static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= WG, "one box per thread");
@@ -2099,24 +2105,47 @@ __device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w,
     const int bq = min(tid, nbx - 1);
     const bool blk = bq < nsb * kSuper;
     const int kb = blk ? bq : bq - nsb * kSuper;
-    const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
+    r.blo = blk ? tb[2 * kb] : sbg[2 * kb];
+    r.bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
+    const int sbl = min(lane, nsb - 1);  // (in flight across the caller's barrier)
+    r.isl = sbg[2 * sbl];
+    r.ish = sbg[2 * sbl + 1];
+}
+template <int WG>
+__device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const TileRegs<WG>& r) {
+    const int tid = threadIdx.x;
+    const int nt = nsb * kSuper * kLdsLeaf;
+    constexpr int kPerT = kLdsTargets / WG;
 #pragma unroll
     for (int k = 0; k < kPerT; ++k) {
         int i = tid + k * WG;
         // (opaque: the slot addresses are formed here, not hoisted out of a caller's item loop as
         // invariants — kept live across the search they pushed its other values into scratch)
         asm volatile("" : "+v"(i));
-        if (i < nt) sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
+        if (i < nt) sh.tl[lds_swz(i)] = tl_slot(r.tv[k], (__float_as_uint(r.tv[k].w) << kLdsPosBits) | (uint32_t)i);
     }
+    const int nbx = nsb * (kSuper + 1);
     if (tid < nbx) {
-        const bool empty = !(blo.x <= bhi.x);  // (+inf, -inf): a box no point reaches
+        const bool blk = tid < nsb * kSuper;
+        const int kb = blk ? tid : tid - nsb * kSuper;
+        const bool empty = !(r.blo.x <= r.bhi.x);  // (+inf, -inf): a box no point reaches
         float* d = blk ? sh.bx[kb] : sh.sbx[kb];
-        d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
-        d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
+        d[0] = empty ? FLT_MAX : r.blo.x; d[1] = empty ? FLT_MAX : r.blo.y; d[2] = empty ? FLT_MAX : r.blo.z;
+        d[3] = empty ? FLT_MAX : r.bhi.x; d[4] = empty ? FLT_MAX : r.bhi.y; d[5] = empty ? FLT_MAX : r.bhi.z;
     }
-    const int sbl = min(lane, nsb - 1);  // (in flight across the caller's barrier)
-    isl = sbg[2 * sbl];
-    ish = sbg[2 * sbl + 1];
+}
+
+// Stage pair p's sorted targets and boxes for an LDS search (every superblock of the pair: nsb <= 64)
+// and load lane l's superblock box into isl / ish (kept in registers for every run).  Every load is
+// issued before the first store: a load-store loop waited out one global round trip per target (8
+// per thread, ~10-20 us per item under load).  The caller's barrier makes the LDS visible.
+template <int WG>
+__device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w, int p, int nsb, v4f& isl, v4f& ish) {
+    TileRegs<WG> r;
+    tile_load<WG>(w, p, nsb, r);
+    tile_store<WG>(sh, nsb, r);
+    isl = r.isl;
+    ish = r.ish;
 }
 
 // The exact LDS search of one query list [0, nlist) of pair p (qv / qm: {x, y, z, U}, {source index |
@@ -2414,12 +2443,12 @@ __device__ __forceinline__ void lds_runs(const LdsTile& sh, unsigned long long* 
         const v4f t = sh.tl[lds_swz((int)tpos)];
         if (live) {
             const NNKey ko = make_key(key_d2(kb), lk_idx(kb));  // (d², original index): PCL's answer
-            if (want_key) key[orig] = ko;
+            if (want_key) st_sc<2>(&key[orig], ko);
             if (CACHE) {  // the update reads X, nn_t: no correspondence record
                 const float2 lu = lu_from_sec(__uint_as_float(secl[lane]));
-                X[orig] = make_float4(x, y, z, lu.x);  // .w = L
-                w.nn_u[xs0 + orig] = lu.y;
-                w.nn_t[xs0 + orig] = make_float4(tl_x(t), tl_y(t), tl_z(t), nt_pack((int)tpos, spos));
+                st_v4<2>(&X[orig], make_float4(x, y, z, lu.x));  // .w = L
+                st_sc<2>(&w.nn_u[xs0 + orig], lu.y);
+                st_v4<2>(&w.nn_t[xs0 + orig], make_float4(tl_x(t), tl_y(t), tl_z(t), nt_pack((int)tpos, spos)));
             } else if (corr) {
                 write_corr_t(w, a, p, orig, x, y, z, key_d2(kb), make_float4(tl_x(t), tl_y(t), tl_z(t), 0.f));
             }
@@ -3400,8 +3429,8 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
             const bool hit = valid & cache_hit(Lm.x, d2);
             // (the fitness pass: no later pass reads the bounds, and X only for the aligned output —
             // the misses' search records carry their own coordinates)
-            if (valid && (!fitness || a.aligned)) X[i] = o;
-            if (valid && !fitness) uu[i] = Lm.y;
+            if (valid && (!fitness || a.aligned)) st_v4<1>(&X[i], o);
+            if (valid && !fitness) st_sc<1>(&uu[i], Lm.y);
             if (SUMS && valid) {
                 stg[e * WW + wt] = o.x;
                 stg[kSumRow + e * WW + wt] = o.y;
@@ -3513,8 +3542,9 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
     auto put = [&](const float4& r, const uint2& m) {
         const uint32_t sp = min(m.y, (uint32_t)(n - 1));
         const int rk = pre[sp >> 5] + __builtin_popcount(need[sp >> 5] & ((1u << (sp & 31)) - 1u));
-        qv[rk] = r;
-        qm[rk] = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
+        st_v4<1>(&qv[rk], r);
+        const uint2 mm = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
+        st_sc<1>(reinterpret_cast<uint64_t*>(&qm[rk]), (uint64_t)mm.x | ((uint64_t)mm.y << 32));
     };
     for (int k0 = tid; k0 < tot; k0 += 4 * WG) {
         float4 r0, r1, r2, r3;  // (named, not an array: an array went to scratch)
