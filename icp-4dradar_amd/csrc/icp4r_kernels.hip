@@ -3347,11 +3347,31 @@ __device__ __forceinline__ void tail_prefetch(const WorkArgs& w, int p, int n, T
     }
 }
 
+// A fold wave's issue priority (ICP4R_FOLD_PRIO): its sequential chain is one dependent add after
+// another, and the SIMD's other waves (fillers, the fused test's workers) otherwise take the issue
+// slots between them.
+#ifndef ICP4R_FOLD_PRIO
+#define ICP4R_FOLD_PRIO 1
+#endif
+__device__ __forceinline__ void fold_prio(bool hi) {
+    if (ICP4R_FOLD_PRIO) {
+        if (hi)
+            __builtin_amdgcn_s_setprio(3);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    }
+}
+
 // SUMS (the update's tail, eligible pairs): the next pass A's Σs folded here, in index order, over the X
 // the test writes — wave 0 lanes 0..2 fold, waves 1.. test (groups of (WG - 64) * kPer points, first
-// to last, each group's new coordinates staged in `stg`: 3 rows of kSumRow floats); the sums go to
+// to last, each group's new coordinates staged in `stg`: two buffers of 3 rows of kSumRow floats); the sums go to
 // sums_out[0..2] (the pair state) with *sums_ok = 1.
-constexpr int kSumRow = 3 * 256 + 4;  // staged points per group (192 workers x 4) + pad
+#ifndef ICP4R_SUMS_PER
+#define ICP4R_SUMS_PER 2  // the Σs tail's points per worker and group (4: 185 vs 179.5 us per update)
+#endif
+constexpr int kSumPer = ICP4R_SUMS_PER;
+constexpr int kSumRow = 192 * kSumPer + 4;  // staged points per group (192 workers x kSumPer) + pad
+constexpr int kSumBuf = 3 * kSumRow;        // one group's staging; two alternate (double buffer)
 template <int WG, int kPer, bool FROM_SRC, bool SUMS = false>
 __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
                                                 uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
@@ -3404,16 +3424,19 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
     }
     for (int g = 0; g < ngrp; ++g) {
         const int i0 = grp0(g);
+        // SUMS: group g is staged in buffer g & 1 while the fold wave folds group g - 1 from the other;
+        // the fold wave reaches barrier g only after folding g - 2, whose buffer group g reuses
+        float* sg = stg + (g & 1) * kSumBuf;
         if (SUMS && !worker) {  // the fold wave: the group's staged coordinates, in index order
-            __syncthreads();    // (B) the staging is free
-            __syncthreads();    // (A) group g staged
-            if (lane < 3) fs = fold_row(stg + lane * kSumRow, min(kStep, n - i0), fs);
+            __syncthreads();    // group g staged
+            fold_prio(true);
+            if (lane < 3) fs = fold_row(sg + lane * kSumRow, min(kStep, n - i0), fs);
+            fold_prio(false);
             continue;
         }
         float4 vn[kPer], tn[kPer], sn[kPer];
         float Un[kPer];
         if (g + 1 < ngrp) load(grp0(g + 1), vn, tn, Un, sn);
-        if (SUMS) __syncthreads();  // (B) the fold wave is done with group g - 1's staging
 #pragma unroll
         for (int e = 0; e < kPer; ++e) {
             const int i = i0 + e * WW + wt;
@@ -3432,9 +3455,9 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
             if (valid && (!fitness || a.aligned)) st_v4<1>(&X[i], o);
             if (valid && !fitness) st_sc<1>(&uu[i], Lm.y);
             if (SUMS && valid) {
-                stg[e * WW + wt] = o.x;
-                stg[kSumRow + e * WW + wt] = o.y;
-                stg[2 * kSumRow + e * WW + wt] = o.z;
+                sg[e * WW + wt] = o.x;
+                sg[kSumRow + e * WW + wt] = o.y;
+                sg[2 * kSumRow + e * WW + wt] = o.z;
             }
             const int k = wave_append(valid && !hit, mcount);
             if (hit) {
@@ -3461,7 +3484,7 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
             U[e] = Un[e];
             if (FROM_SRC) sv[e] = sn[e];
         }
-        if (SUMS) __syncthreads();  // (A) group g staged
+        if (SUMS) __syncthreads();  // group g staged
     }
     if (SUMS && wave == 0 && lane < 3) {
         sums_out[lane] = fs;
@@ -3591,7 +3614,7 @@ constexpr int kFoldRow = kFoldChunkP + kFoldPad;
 // the fused test's LDS miss records (24 B each) after the bitmap and its prefixes, in the fold buffers
 constexpr int kFoldRecs = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4) / 24) & ~15;
 // ... and with the Σs staging rows (pair_cache_test<SUMS>) at the buffers' end
-constexpr int kFoldRecsSums = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4 - 3 * kSumRow * 4) / 24) & ~15;
+constexpr int kFoldRecsSums = ((2 * 9 * kFoldRow * 4 - 2 * kNeedWords * 4 - 2 * kSumBuf * 4) / 24) & ~15;
 struct FoldShared {
     alignas(16) float buf[2][9][kFoldRow];
     float res[8];
@@ -3737,10 +3760,12 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     if (wv == 0) {
         const int lane0 = sums ? 3 : 0;
+        fold_prio(true);
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
             if (lane >= lane0 && lane < 7) acc = fold_seq<float>(buf[c & 1][lane], min(CH, n - c * CH), acc);
         }
+        fold_prio(false);
     } else if (wv * 64 < fill0) {  // the MSE sum: its exact form, the whole wave per chunk
         uint64_t xs = 0;
         int xe = INT_MAX;
@@ -4026,6 +4051,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
             Chunk ch = make(p0, 1, npe >= 1 ? pb(1) : INT_MAX);
             if (wv == 0) {
                 int k = 1, nb = ch.nb;  // the next panel end
+                fold_prio(true);
                 for (int c = 0; ch.c0 < p1; ++c) {
                     __syncthreads();
                     const int c0 = ch.c0, c1 = c0 + ch.len;
@@ -4067,6 +4093,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
                     }
                     ch = next(ch);
                 }
+                fold_prio(false);
             } else {
                 if (ch.c0 < p1) {
                     float4 r[kPerB][2];
@@ -4283,8 +4310,8 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
 #endif
         if (sums_tail) {
             // the staging rows of the Σs fold at the end of the fold buffers, the miss records before
-            float* stg = reinterpret_cast<float*>(&sh.buf[0][0][0]) + (2 * 9 * kFoldRow - 3 * kSumRow);
-            nwork = pair_cache_test<kFoldWG, ICP4R_TAIL_PER, false, true>(
+            float* stg = reinterpret_cast<float*>(&sh.buf[0][0][0]) + (2 * 9 * kFoldRow - 2 * kSumBuf);
+            nwork = pair_cache_test<kFoldWG, kSumPer, false, true>(
                 a, w, p, n, T, need, pre, lv, lm, kFoldRecsSums, &sh.mcount, sh.cnt, false, stamp, nullptr, stg,
                 st.sum_s, &st.sums_ok);
         } else {
