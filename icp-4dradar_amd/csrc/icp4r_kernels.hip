@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     __shared__ uint32_t bins[kKdMaxN / 16];
     __shared__ uint32_t wsum[kSoWG / 64];
     __shared__ float qz[6];
-    __shared__ uint32_t sl[kKdMaxN];  // stage_first: source index | leaf << kNtPosShift per sorted position
+    __shared__ uint32_t sl[kKdMaxN];  // stage_first: a quarter of the sorted positions' records
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     if (w.state[p].phase == kPhaseInvalid || !src_by_tgt_tree(a, w, p)) return;
     const int n = a.src_n[p], m = a.tgt_n[p];
@@ -1185,11 +1185,12 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     for (int b = tid; b < kKdMaxN / 16; b += kSoWG) bins[b] = 0u;
     __syncthreads();
     const float lo[3] = {qz[0], qz[1], qz[2]}, sc[3] = {qz[3], qz[4], qz[5]};
-    const float4* src = a.src + a.src_off[p];
     // Every thread's points (i = tid + e * kSoWG) descend in groups of kSoGrp: their loads all in
     // flight together and the descents interleaved level by level (independent LDS chains) — a
     // point-at-a-time loop had waited out a global round trip and 9 dependent LDS reads per point.
-    // The leaves stay in registers (two per dword) for the scatter.
+    // The points are X (the guess-transformed sources the first pass searches; init_kernel wrote
+    // them), in index order: the leaves stay in registers (two per dword) for the scatter.
+    const float4* X = w.X + (int64_t)p * w.x_stride;
     constexpr int kSoPer = kKdMaxN / kSoWG, kSoGrp = 8;
     static_assert(kSoPer % kSoGrp == 0 && kSoPer % 2 == 0, "point groups");
     uint32_t lv[kSoPer / 2];
@@ -1197,7 +1198,7 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     for (int g = 0; g < kSoPer; g += kSoGrp) {
         float4 v[kSoGrp];
 #pragma unroll
-        for (int e = 0; e < kSoGrp; ++e) v[e] = src[min(tid + (g + e) * kSoWG, n - 1)];
+        for (int e = 0; e < kSoGrp; ++e) v[e] = X[min(tid + (g + e) * kSoWG, n - 1)];
         int key3[kSoGrp][3], node[kSoGrp], sp[kSoGrp];
 #pragma unroll
         for (int e = 0; e < kSoGrp; ++e) {
@@ -1265,35 +1266,65 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
         // The batched search's first-pass query records in sorted order: {X_i, U = +inf} and
         // {i | its position << kNtPosShift, the seed = its leaf's first target position} — the
         // search takes them as they are instead of gathering X through sperm at every work item
-        // (a chain of dependent global round trips in front of each pair's first search).  The
-        // scatter goes to LDS (i | leaf << 14 at the position), then every record is written in
-        // position order: scattered 24-B record stores had cost more than the search saved.
+        // (a chain of dependent global round trips in front of each pair's first search).  Every
+        // record is written in position order (scattered 24-B record stores had cost more than the
+        // search saved), from LDS, a quarter of the positions at a time: each thread puts its own
+        // points' records (x, y, z, i | leaf << 14) at their positions in the quarter, then the
+        // quarter is stored coalesced.  (A gather of X by sorted position instead fetched 4x
+        // the cloud: 16-B reads of 64-B lines.)
+        // (the coordinates read again, from the L2: kept from the descent they cost occupancy)
+        float px[kSoPer], py[kSoPer], pz[kSoPer];
+#pragma unroll
+        for (int g = 0; g < kSoPer; ++g) {
+            const float4 v = X[min(tid + g * kSoWG, n - 1)];
+            px[g] = v.x;
+            py[g] = v.y;
+            pz[g] = v.z;
+        }
+        uint32_t pos2[kSoPer / 2];  // the points' sorted positions, two per dword
 #pragma unroll
         for (int g = 0; g < kSoPer; ++g) {
             const int i = tid + g * kSoWG;
-            if (i >= n) continue;
             const uint32_t leaf = (lv[g >> 1] >> (16 * (g & 1))) & 0xffffu;
-            sl[atomicAdd(&bins[leaf], 1u)] = (uint32_t)i | (leaf << kNtPosShift);
+            const uint32_t ps = i < n ? atomicAdd(&bins[leaf], 1u) : 0xffffu;
+            if ((g & 1) == 0)
+                pos2[g >> 1] = ps;
+            else
+                pos2[g >> 1] |= ps << 16;
         }
-        __syncthreads();
-        const float4* X = w.X + (int64_t)p * w.x_stride;
+        constexpr int kQ = kKdMaxN / 4;  // positions per quarter: 4 rows of kQ words in sl's 32 KB
+        float* rx = reinterpret_cast<float*>(sl);  // (rows, not 16-B records: a record's 4-register
+        float* ry = rx + kQ;                       //  tuples, hoisted out of the quarter loop,
+        float* rz = ry + kQ;                       //  took 64 registers)
+        uint32_t* rw = sl + 3 * kQ;
         float4* qv = w.qv + (int64_t)p * w.x_stride;
         uint2* qm = w.qm + (int64_t)p * w.x_stride;
+        for (int q0 = 0; q0 < n; q0 += kQ) {
+            __syncthreads();  // (the previous quarter's records read)
 #pragma unroll
-        for (int g = 0; g < kSoPer; g += kSoGrp) {
-            uint32_t e8[kSoGrp];
-            float4 xv[kSoGrp];
+            for (int k = 0; k < kSoPer / 2; ++k) asm volatile("" : "+v"(pos2[k]), "+v"(lv[k]));  // (nothing derived from them hoisted: registers)
 #pragma unroll
-            for (int e = 0; e < kSoGrp; ++e) e8[e] = sl[min(tid + (g + e) * kSoWG, n - 1)];
+            for (int g = 0; g < kSoPer; ++g) {
+                const uint32_t ps = (pos2[g >> 1] >> (16 * (g & 1))) & 0xffffu;
+                const uint32_t leaf = (lv[g >> 1] >> (16 * (g & 1))) & 0xffffu;
+                const uint32_t r = ps - (uint32_t)q0;
+                if (r < (uint32_t)kQ) {
+                    rx[r] = px[g];
+                    ry[r] = py[g];
+                    rz[r] = pz[g];
+                    rw[r] = (uint32_t)(tid + g * kSoWG) | (leaf << kNtPosShift);
+                }
+            }
+            __syncthreads();
 #pragma unroll
-            for (int e = 0; e < kSoGrp; ++e) xv[e] = X[e8[e] & kNtIdxMask];  // gathers, all in flight
-#pragma unroll
-            for (int e = 0; e < kSoGrp; ++e) {
-                const int pos = tid + (g + e) * kSoWG;
+            for (int e = 0; e < kQ / kSoWG; ++e) {
+                const int pos = q0 + tid + e * kSoWG;
                 if (pos >= n) continue;
-                const uint32_t i = e8[e] & kNtIdxMask, leaf = e8[e] >> kNtPosShift;
+                const int o = tid + e * kSoWG;
+                const uint32_t e8 = rw[o];
+                const uint32_t i = e8 & kNtIdxMask, leaf = e8 >> kNtPosShift;
                 spm[pos] = (int32_t)i;
-                qv[pos] = make_float4(xv[e].x, xv[e].y, xv[e].z, INFINITY);
+                qv[pos] = make_float4(rx[o], ry[o], rz[o], INFINITY);
                 qm[pos] = make_uint2(i | ((uint32_t)pos << kNtPosShift), leaf * (uint32_t)B);
             }
         }
