@@ -1019,15 +1019,6 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
     }
 }
 
-__global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
-    __shared__ IndexShared shu;
-    // grid (pairs, 2): target and source of every pair; (pairs, 1): targets only (every source is
-    // ordered by src_order_kernel — launched alone, the targets spread over every CU)
-    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
-    const int p = gridDim.y == 2 ? g >> 1 : g;
-    const bool is_tgt = gridDim.y == 2 ? (g & 1) == 0 : true;
-    index_cloud(shu, a, w, p, is_tgt);
-}
 
 // Multi-workgroup Morton sort of a large target (the C5 submap: 65k points), for few pairs: the
 // one-workgroup sort above spends ~125 us of a single registration in its three sweeps over the
@@ -1190,13 +1181,19 @@ constexpr int kSoWG = 512;
 constexpr int kNtPosShift = 14;
 constexpr int kNtIdxMask = (1 << kNtPosShift) - 1;
 
-__global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w) {
-    __shared__ uint32_t nodes[kKdNodes];
-    __shared__ uint32_t bins[kKdMaxN / 16];
-    __shared__ uint32_t wsum[kSoWG / 64];
-    __shared__ float qz[6];
-    __shared__ uint32_t sl[kKdMaxN];  // stage_first: a quarter of the sorted positions' records
-    const int p = xcd_remap(blockIdx.x, gridDim.x);
+struct SoShared {
+    uint32_t nodes[kKdNodes];
+    uint32_t bins[kKdMaxN / 16];
+    uint32_t wsum[kSoWG / 64];
+    float qz[6];
+    uint32_t sl[kKdMaxN];  // stage_first: a quarter of the sorted positions' records
+};
+__device__ void src_order_pair(const PairArgs& a, const WorkArgs& w, int p, SoShared& so) {
+    uint32_t* nodes = so.nodes;
+    uint32_t* bins = so.bins;
+    uint32_t* wsum = so.wsum;
+    float* qz = so.qz;
+    uint32_t* sl = so.sl;
     if (w.state[p].phase == kPhaseInvalid || !src_by_tgt_tree(a, w, p)) return;
     const int n = a.src_n[p], m = a.tgt_n[p];
     if (n <= 0) return;
@@ -1394,6 +1391,30 @@ __global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w
     __syncthreads();
     if (it) it[1] = __builtin_amdgcn_s_memrealtime();
 #endif
+}
+
+__global__ __launch_bounds__(kSoWG) void src_order_kernel(PairArgs a, WorkArgs w) {
+    __shared__ SoShared so;
+    src_order_pair(a, w, xcd_remap(blockIdx.x, gridDim.x), so);
+}
+
+#ifndef ICP4R_FUSE_SRC_ORDER
+#define ICP4R_FUSE_SRC_ORDER 1  // targets-only grids order the pair's source in the same workgroup
+#endif
+static_assert(sizeof(SoShared) <= sizeof(IndexShared) && kSoWG == kIdxWG, "the source order reuses the index build's workgroup");
+__global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w) {
+    __shared__ IndexShared shu;
+    // grid (pairs, 2): target and source of every pair; (pairs, 1): targets only, every source
+    // ordered by its target's tree — by this workgroup right after the build (ICP4R_FUSE_SRC_ORDER:
+    // one launch and one kernel boundary fewer, the tree read back while it is in this XCD's L2)
+    const int g = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const int p = gridDim.y == 2 ? g >> 1 : g;
+    const bool is_tgt = gridDim.y == 2 ? (g & 1) == 0 : true;
+    index_cloud(shu, a, w, p, is_tgt);
+    if (ICP4R_FUSE_SRC_ORDER && gridDim.y == 1) {
+        __syncthreads();  // the tree (kdn) and sorted targets written; the LDS free
+        src_order_pair(a, w, p, *reinterpret_cast<SoShared*>(&shu));
+    }
 }
 
 // index_refine_kernel: targets too large for the in-LDS kd build (the C5 scan-to-map submap) are
@@ -5147,7 +5168,7 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
         return hipGetLastError();
     }
     hipLaunchKernelGGL(index_kernel, dim3(npairs, tgt_only ? 1 : 2), dim3(kIdxWG), 0, st, a, w);
-    if (w.src_by_tgt && w.kdn)
+    if (w.src_by_tgt && w.kdn && !(ICP4R_FUSE_SRC_ORDER && tgt_only))
         hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);
     if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))
         hipLaunchKernelGGL(index_refine_kernel, dim3(nch, npairs), dim3(kIdxWG), 0, st, a, w);
