@@ -1,3 +1,2 @@
 set -u
-timeout -k 10 900 bash tools/profile_round.sh round4 > gpurun_out/profile_round.log 2>&1 || { tail -5 gpurun_out/profile_round.log; exit 3; }
-timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench_err.log || exit 4
+timeout -k 10 900 tools/experiments/env_ab.sh 2 "-" "ICP4R_GROUPS=3" "ICP4R_GROUPS=4" "ICP4R_GROUPS=3 ICP4R_SEARCH_CU_DIV=2" "ICP4R_PART=2048" "ICP4R_PART=512" > gpurun_out/groups_ab.log 2>&1 || exit 3
