@@ -449,7 +449,8 @@ __device__ __forceinline__ int kd_split(int S, int leaf) {
 // KPER: list positions per thread in the levels (16 covers kKdMaxN; 8 for clouds of at most
 // kKdMaxN / 2 points, so that a level's per-thread LDS work halves).
 template <int KPER, typename Get>  // Get: int -> float4, point i of the cloud
-__device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, uint32_t* kdn = nullptr) {
+__device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, uint32_t* kdn = nullptr,
+                         uint16_t* gk = nullptr) {
     static_assert(KPER % 8 == 0 && KPER <= 16 && KPER * kIdxWG >= kKdMaxN / 2, "list positions per thread");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tk) tk[0] = __builtin_amdgcn_s_memrealtime();
@@ -547,6 +548,11 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         if (i >= n) continue;
         const float4 v = make_float4(px[k], py[k], pz[k], 0.0f);
         const int bx = bin(v.x, 0), by = bin(v.y, 1), bz = bin(v.z, 2);
+        if (gk) {  // (coalesced: the levels read them back from this XCD's L2)
+            gk[i] = (uint16_t)bx;
+            gk[kKdMaxN + i] = (uint16_t)by;
+            gk[2 * kKdMaxN + i] = (uint16_t)bz;
+        }
         sh.L[0][atomicAdd(&sh.u.hist[0][bx], 1u)] = (uint16_t)i;
         sh.L[1][atomicAdd(&sh.u.hist[1][by], 1u)] = (uint16_t)i;
         sh.L[2][atomicAdd(&sh.u.hist[2][bz], 1u)] = (uint16_t)i;
@@ -568,21 +574,37 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
                 // list, re-quantised from the (cache-resident) cloud: no per-point key array in LDS
                 // (keeping the small clouds' bins in LDS instead was measured: no faster)
                 float ext[3];
-                float4 pf[3], pl[3];
+                if (gk) {  // the quantised keys written above: 2-B reads of an L2-resident 48 KB
+                    int kf[3], kl[3];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    pf[a] = pts(sh.L[a][s]);
-                    pl[a] = pts(sh.L[a][e - 1]);
+                    for (int a = 0; a < 3; ++a) {
+                        kf[a] = gk[a * kKdMaxN + sh.L[a][s]];
+                        kl[a] = gk[a * kKdMaxN + sh.L[a][e - 1]];
+                    }
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) ext[a] = (float)(kl[a] - kf[a]) / sc[a];
+                } else {
+                    float4 pf[3], pl[3];
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        pf[a] = pts(sh.L[a][s]);
+                        pl[a] = pts(sh.L[a][e - 1]);
+                    }
+                    ext[0] = (float)(bin(pl[0].x, 0) - bin(pf[0].x, 0)) / sc[0];
+                    ext[1] = (float)(bin(pl[1].y, 1) - bin(pf[1].y, 1)) / sc[1];
+                    ext[2] = (float)(bin(pl[2].z, 2) - bin(pf[2].z, 2)) / sc[2];
                 }
-                ext[0] = (float)(bin(pl[0].x, 0) - bin(pf[0].x, 0)) / sc[0];
-                ext[1] = (float)(bin(pl[1].y, 1) - bin(pf[1].y, 1)) / sc[1];
-                ext[2] = (float)(bin(pl[2].z, 2) - bin(pf[2].z, 2)) / sc[2];
                 ax = ext[0] >= ext[1] && ext[0] >= ext[2] ? 0 : (ext[1] >= ext[2] ? 1 : 2);
                 any = true;
                 if (kdn && node < kKdNodes) {
-                    const float4 pm = pts(sh.L[ax][s + h]);
-                    kdn[8 + node] = 0x80000000u | ((uint32_t)(s + h) << 13) | ((uint32_t)ax << 11) |
-                                    (uint32_t)bin(ax == 0 ? pm.x : (ax == 1 ? pm.y : pm.z), ax);
+                    uint32_t km;
+                    if (gk) {
+                        km = gk[ax * kKdMaxN + sh.L[ax][s + h]];
+                    } else {
+                        const float4 pm = pts(sh.L[ax][s + h]);
+                        km = (uint32_t)bin(ax == 0 ? pm.x : (ax == 1 ? pm.y : pm.z), ax);
+                    }
+                    kdn[8 + node] = 0x80000000u | ((uint32_t)(s + h) << 13) | ((uint32_t)ax << 11) | km;
                 }
             }
             sh.seg_mid[tid] = (uint16_t)(s + h);
@@ -767,6 +789,10 @@ __device__ void index_boxes(const WorkArgs& w, int p, int n) {
     }
 }
 
+#ifndef ICP4R_KD_KEYS
+#define ICP4R_KD_KEYS 1  // kd levels read the quantised keys from a scratch copy, not the points
+#endif
+
 // The source of pair p is ordered by its target's kd tree (src_order_kernel) rather than its own.
 __device__ __forceinline__ bool src_by_tgt_tree(const PairArgs& a, const WorkArgs& w, int p) {
     const int m = a.tgt_n[p];
@@ -797,10 +823,16 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
         uint32_t* kdn = (is_tgt && w.kdn && w.src_by_tgt) ? w.kdn + (int64_t)p * kKdnStride : nullptr;
         if (kdn)
             for (int k = tid; k < kKdnStride; k += kIdxWG) kdn[k] = 0u;  // (kd_order syncs before writing)
+        // the quantised keys' scratch (3 x kKdMaxN u16): the pair's query-record area, unused until
+        // the source order / first search writes it (ICP4R_KD_KEYS=0: the levels re-read the points)
+        // (targets only: a pair's source build may run beside it on the same area)
+        uint16_t* gk = (ICP4R_KD_KEYS && is_tgt && w.qv && (int64_t)w.x_stride * (int64_t)sizeof(float4) >= 3 * kKdMaxN * 2)
+                           ? reinterpret_cast<uint16_t*>(w.qv + (int64_t)p * w.x_stride)
+                           : nullptr;
         if (n <= kKdMaxN / 2)
-            kd_order<8>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
+            kd_order<8>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn, gk);
         else
-            kd_order<16>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn);
+            kd_order<16>(shu.kd, [&](int i) { return pts[i]; }, n, is_tgt ? w.leaf : 16, tk, kdn, gk);
         const uint16_t* ord = shu.kd.L[0];
         if (is_tgt) {
             // sorted targets, padding (+inf coordinates, .w = the last target's index: never a match,
