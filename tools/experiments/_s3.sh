@@ -1,3 +1,4 @@
 set -u
-timeout -k 10 900 bash tools/profile_round.sh round4 > gpurun_out/profile_round.log 2>&1 || { tail -5 gpurun_out/profile_round.log; exit 3; }
-timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench_err.log || exit 4
+for r in 1 2; do
+timeout -k 10 400 tools/experiments/env_ab.sh 1 "ICP4R_SUMS_TAIL=0" "ICP4R_SUMS_TAIL=1" "ICP4R_SUMS_TAIL=1 ICP4R_LIBRARY=_var/ab/sp1/libicp4r.so" "ICP4R_SUMS_TAIL=1 ICP4R_LIBRARY=_var/ab/sp3/libicp4r.so" >> gpurun_out/sums3_ab.log 2>&1 || exit 5
+done
