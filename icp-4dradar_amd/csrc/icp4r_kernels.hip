@@ -3282,7 +3282,6 @@ struct SolveShared {
     double mom[20];
     double sigma[9], ms[3], md[3];
     SvdWork svd;
-    SvdWorkF svdf;
     float sigmaf[9];  // PCL numerics: sigma as Eigen's GEMM leaves it (one_over_n applied per panel)
     float mean[6];
     float one_over_n;
@@ -5136,11 +5135,14 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
 
 // Test hook: the device float Umeyama rotation for k sigma matrices (one thread each).
 __global__ void rot_f32_kernel(const float* sigma, float* R, int k) {
-    __shared__ SvdWorkF ws[64];
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= k) return;
-    umeyama_rotation_f32(sigma + 9 * i, ws[threadIdx.x]);
-    for (int e = 0; e < 9; ++e) R[9 * i + e] = ws[threadIdx.x].R[e];
+    float sg[9], Ri[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) sg[e] = sigma[9 * i + e];
+    umeyama_rotation_f32_reg(sg, Ri);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) R[9 * i + e] = Ri[e];
 }
 
 hipError_t launch_rot_f32(const float* sigma, float* R, int k, hipStream_t st) {

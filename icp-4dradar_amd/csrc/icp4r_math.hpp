@@ -5,10 +5,11 @@
 //   * L2_Simple<float> distance  (FLANN, used by pcl::KdTreeFLANN):  ((dx*dx + dy*dy) + dz*dz)
 //   * transformCloud             (icp.hpp, Eigen lazy packet product): ((r0*x + r1*y) + r2*z) + t
 //   * final = T_inc * final      (Matrix4f * Matrix4f, k-ordered)
-// The rigid solve (Eigen umeyama, with_scaling = false) runs in double here; DESIGN.md §Numerics
-// explains why that stays within the parity bar of PCL's float solve.
+//   * the rigid solve: Eigen umeyama (with_scaling = false) over JacobiSVD<Matrix3f>, in float
+//     (PCL numerics, the default), or the product's own double solve (F64 numerics).
 #pragma once
 
+#include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -202,242 +203,182 @@ __device__ inline void umeyama_rotation(const double* sigma, SvdWork& w) {
             w.R[i * 3 + j] = w.U[i * 3 + 0] * w.V[j * 3 + 0] + w.U[i * 3 + 1] * w.V[j * 3 + 1] + d2 * w.U[i * 3 + 2] * w.V[j * 3 + 2];
 }
 
-// ---- 3x3 SVD + Umeyama rotation in FLOAT (PCL numerics) -------------------------------------
-// Same one-sided Jacobi as svd3() with every operation in float and in the operation order of
-// oracle/icp_oracle.c svd3_f32 / rot_f32 / det3_f32, so the rotation the PCL-numerics path produces
-// is bit-identical to the float restatement of PCL's TransformationEstimationSVD (Scalar = float).
+// ---- PCL's float rotation: Eigen 3.3 JacobiSVD<Matrix3f> + umeyama (PCL numerics) -----------
+// pcl::umeyama -> Eigen::umeyama (Geometry/Umeyama.h, with_scaling = false), Scalar = float:
+//   JacobiSVD<Matrix3f> svd(sigma, ComputeFullU | ComputeFullV)       (SVD/JacobiSVD.h compute())
+//   S = (1, 1, 1); if (det(U) * det(V) < 0) S(2) = -1;  R = U * S.asDiagonal() * V^T
+// Square input: no QR preconditioner.  The matrix is divided by its largest |coefficient|; two-sided
+// 2x2 Jacobi steps over (p, q) = (1, 0), (2, 0), (2, 1) repeat until no off-diagonal pair exceeds
+// max(FLT_MIN, 2 eps * the largest |diagonal| seen).  A step is real_2x2_jacobi_svd
+// (misc/RealSvd2x2.h: a rotation symmetrising the 2x2 block, then JacobiRotation::makeJacobi,
+// j_left = rot1 * j_right^T) applied to the work matrix's rows (j_left) and columns (j_right) and
+// accumulated into U's and V's columns; apply_rotation_in_the_plane is x' = c x + s y,
+// y' = -s x + c y, a no-op for (c, s) = (1, 0).  Then a negative diagonal entry flips U's column,
+// the singular values are scaled back and sorted by swaps (the first maximum; a zero maximum stops
+// the sort).  R's coefficients: the lazy product's unrolled redux, x0 + (x1 + x2), with
+// x_k = (U(i,k) * S(k)) * V(j,k).  Every operation in float, unfused, in this order: the same bits
+// as oracle/icp_oracle.c rot_f32 and tests/golden/numpy_twin.py umeyama_rotation_f32.  Static
+// indices only, so the whole working set stays in registers (thread 0's serial solve).
 // float '/' and sqrtf are correctly rounded on the device (HIP default), like SSE on the host.
-struct SvdWorkF {
-    float W[9], V[9], U[9], S[3], Vs[9], Ws[9], R[9];
-    int ord[3];
-};
-
-__host__ __device__ inline void svd3_f32(const float* A, SvdWorkF& w) {
-    float* W = w.W;
-    float* V = w.V;
-    float* U = w.U;
-    float* S = w.S;
-    for (int k = 0; k < 9; ++k) W[k] = A[k];
-    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
-#pragma nounroll
-    for (int sweep = 0; sweep < 40; ++sweep) {
-        float off = 0;
-#pragma nounroll
-        for (int r = 0; r < 3; ++r) {
-            const int p = r == 2 ? 1 : 0, q = r == 0 ? 1 : 2;
-            float al = 0, be = 0, ga = 0;
-            for (int k = 0; k < 3; ++k) {
-                al += W[k * 3 + p] * W[k * 3 + p];
-                be += W[k * 3 + q] * W[k * 3 + q];
-                ga += W[k * 3 + p] * W[k * 3 + q];
-            }
-            if (ga == 0) continue;
-            float nrm = sqrtf(al * be);
-            if (nrm == 0) continue;
-            float rel = fabsf(ga) / nrm;
-            if (rel > off) off = rel;
-            if (rel <= 1e-7f) continue;
-            float zeta = (be - al) / (2 * ga);
-            float t = (zeta >= 0 ? 1.0f : -1.0f) / (fabsf(zeta) + sqrtf(1.0f + zeta * zeta));
-            float c = 1.0f / sqrtf(1.0f + t * t);
-            float s = c * t;
-            for (int k = 0; k < 3; ++k) {
-                float wp = W[k * 3 + p], wq = W[k * 3 + q];
-                W[k * 3 + p] = c * wp - s * wq;
-                W[k * 3 + q] = s * wp + c * wq;
-                float vp = V[k * 3 + p], vq = V[k * 3 + q];
-                V[k * 3 + p] = c * vp - s * vq;
-                V[k * 3 + q] = s * vp + c * vq;
-            }
-        }
-        if (off <= 1e-7f) break;
-    }
-    float sv[3];
-    for (int c = 0; c < 3; ++c)
-        sv[c] = sqrtf(W[0 * 3 + c] * W[0 * 3 + c] + W[1 * 3 + c] * W[1 * 3 + c] + W[2 * 3 + c] * W[2 * 3 + c]);
-    int* ord = w.ord;
-    for (int c = 0; c < 3; ++c) ord[c] = c;
-    for (int i = 0; i < 3; ++i)
-        for (int j = i + 1; j < 3; ++j)
-            if (sv[ord[j]] > sv[ord[i]]) {
-                int tt = ord[i];
-                ord[i] = ord[j];
-                ord[j] = tt;
-            }
-    for (int c = 0; c < 3; ++c) {
-        S[c] = sv[ord[c]];
-        for (int k = 0; k < 3; ++k) {
-            w.Vs[k * 3 + c] = V[k * 3 + ord[c]];
-            w.Ws[k * 3 + c] = W[k * 3 + ord[c]];
-        }
-    }
-    for (int k = 0; k < 9; ++k) V[k] = w.Vs[k];
-    int rank = 0;
-    for (int c = 0; c < 3; ++c)
-        if (S[c] > 1e-6f * (S[0] > 0 ? S[0] : 1.0f) && S[c] > 0) rank = c + 1;
-    for (int c = 0; c < rank; ++c)
-        for (int k = 0; k < 3; ++k) U[k * 3 + c] = w.Ws[k * 3 + c] / S[c];
-    if (rank == 0) {
-        for (int k = 0; k < 9; ++k) U[k] = (k % 4 == 0) ? 1.0f : 0.0f;
-        return;
-    }
-    if (rank == 1) {
-        int ax = 0;
-        float amin = fabsf(U[0]);
-        for (int k = 1; k < 3; ++k)
-            if (fabsf(U[k * 3]) < amin) {
-                amin = fabsf(U[k * 3]);
-                ax = k;
-            }
-        const float e0 = ax == 0 ? 1.0f : 0.0f, e1 = ax == 1 ? 1.0f : 0.0f, e2 = ax == 2 ? 1.0f : 0.0f;
-        float c0 = U[1 * 3] * e2 - U[2 * 3] * e1;
-        float c1 = U[2 * 3] * e0 - U[0 * 3] * e2;
-        float c2 = U[0 * 3] * e1 - U[1 * 3] * e0;
-        float nn = sqrtf(c0 * c0 + c1 * c1 + c2 * c2);
-        U[0 * 3 + 1] = c0 / nn;
-        U[1 * 3 + 1] = c1 / nn;
-        U[2 * 3 + 1] = c2 / nn;
-    }
-    if (rank <= 2) {  // complete U only when sigma is rank-deficient
-        U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
-        U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
-        U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
-    }
+__host__ __device__ __forceinline__ void plane_rot3(float& x0, float& x1, float& x2, float& y0, float& y1, float& y2,
+                                                    float c, float s) {
+    if (c == 1.0f && s == 0.0f) return;
+    float xi = x0, yi = y0;
+    x0 = c * xi + s * yi;
+    y0 = -s * xi + c * yi;
+    xi = x1, yi = y1;
+    x1 = c * xi + s * yi;
+    y1 = -s * xi + c * yi;
+    xi = x2, yi = y2;
+    x2 = c * xi + s * yi;
+    y2 = -s * xi + c * yi;
 }
 
-__host__ __device__ inline float det3_f32(const float* M) {
+// real_2x2_jacobi_svd of the block (p, q) = [[a, b], [e, f]] = [[W(p,p), W(p,q)], [W(q,p), W(q,q)]]
+__host__ __device__ __forceinline__ void real_2x2_jacobi_f32(float a, float b, float e, float f, float& cl, float& sl,
+                                                             float& cr, float& sr) {
+    float c1, s1;
+    const float t = a + f;
+    const float d = e - b;
+    if (fabsf(d) < FLT_MIN) {
+        s1 = 0.0f;
+        c1 = 1.0f;
+    } else {
+        const float u = t / d;
+        const float tmp = sqrtf(1.0f + u * u);
+        s1 = 1.0f / tmp;
+        c1 = u / tmp;
+    }
+    if (!(c1 == 1.0f && s1 == 0.0f)) {  // m.applyOnTheLeft(0, 1, rot1)
+        const float x0 = a, y0 = e, x1 = b, y1 = f;
+        a = c1 * x0 + s1 * y0;
+        e = -s1 * x0 + c1 * y0;
+        b = c1 * x1 + s1 * y1;
+        f = -s1 * x1 + c1 * y1;
+    }
+    const float deno = 2.0f * fabsf(b);  // makeJacobi(m(0,0), m(0,1), m(1,1))
+    if (deno < FLT_MIN) {
+        cr = 1.0f;
+        sr = 0.0f;
+    } else {
+        const float tau = (a - f) / deno;
+        const float w = sqrtf(tau * tau + 1.0f);
+        float tt;
+        if (tau > 0.0f)
+            tt = 1.0f / (tau + w);
+        else
+            tt = 1.0f / (tau - w);
+        const float sign_t = tt > 0.0f ? 1.0f : -1.0f;
+        const float n = 1.0f / sqrtf(tt * tt + 1.0f);
+        sr = -sign_t * (b / fabsf(b)) * fabsf(tt) * n;
+        cr = n;
+    }
+    const float c2 = cr, s2 = -sr;  // j_left = rot1 * j_right^T
+    cl = c1 * c2 - s1 * s2;
+    sl = c1 * s2 + s1 * c2;
+}
+
+__host__ __device__ __forceinline__ float det3_f32(const float (&M)[9]) {  // LU/Determinant.h, row-major M
     return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
 }
 
-__host__ __device__ inline void umeyama_rotation_f32(const float* sigma, SvdWorkF& w) {
-    svd3_f32(sigma, w);
-    float d[3] = {1.0f, 1.0f, 1.0f};
-    if (det3_f32(w.U) * det3_f32(w.V) < 0) d[2] = -1.0f;
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            float acc = 0;
-            for (int k = 0; k < 3; ++k) acc += w.U[i * 3 + k] * d[k] * w.V[j * 3 + k];
-            w.R[i * 3 + j] = acc;
-        }
+// One Jacobi step on the pair (P, Q) (P > Q) of W, U, V (row-major): returns whether it ran.
+template <int P, int Q>
+__host__ __device__ __forceinline__ bool jacobi_step_f32(float (&W)[9], float (&U)[9], float (&V)[9], float& max_diag) {
+    const float pm = (2.0f * FLT_EPSILON) * max_diag;
+    const float threshold = FLT_MIN < pm ? pm : FLT_MIN;
+    if (!(fabsf(W[P * 3 + Q]) > threshold || fabsf(W[Q * 3 + P]) > threshold)) return false;
+    float cl, sl, cr, sr;
+    real_2x2_jacobi_f32(W[P * 3 + P], W[P * 3 + Q], W[Q * 3 + P], W[Q * 3 + Q], cl, sl, cr, sr);
+    plane_rot3(W[P * 3 + 0], W[P * 3 + 1], W[P * 3 + 2], W[Q * 3 + 0], W[Q * 3 + 1], W[Q * 3 + 2], cl, sl);  // rows
+    plane_rot3(U[0 * 3 + P], U[1 * 3 + P], U[2 * 3 + P], U[0 * 3 + Q], U[1 * 3 + Q], U[2 * 3 + Q], cl, sl);  // cols
+    plane_rot3(W[0 * 3 + P], W[1 * 3 + P], W[2 * 3 + P], W[0 * 3 + Q], W[1 * 3 + Q], W[2 * 3 + Q], cr, -sr);
+    plane_rot3(V[0 * 3 + P], V[1 * 3 + P], V[2 * 3 + P], V[0 * 3 + Q], V[1 * 3 + Q], V[2 * 3 + Q], cr, -sr);
+    const float ap = fabsf(W[P * 3 + P]), aq = fabsf(W[Q * 3 + Q]);
+    const float mpq = ap < aq ? aq : ap;
+    max_diag = max_diag < mpq ? mpq : max_diag;
+    return true;
 }
 
-// The same float SVD + Umeyama rotation as umeyama_rotation_f32, every operation in the same order,
-// with all indices static so the arrays live in registers: on the device the LDS-resident work
-// struct put a dependent LDS round trip on every access of thread 0's serial solve.
-__host__ __device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
-    float W[9], V[9];
+template <int I, int J>
+__host__ __device__ __forceinline__ void svd_swap_f32(float (&S)[3], float (&U)[9], float (&V)[9]) {
+    float t = S[I];
+    S[I] = S[J];
+    S[J] = t;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) W[k] = A[k];
+    for (int k = 0; k < 3; ++k) {
+        t = U[k * 3 + I];
+        U[k * 3 + I] = U[k * 3 + J];
+        U[k * 3 + J] = t;
+        t = V[k * 3 + I];
+        V[k * 3 + I] = V[k * 3 + J];
+        V[k * 3 + J] = t;
+    }
+}
+
+// JacobiSVD<Matrix3f>(A, ComputeFullU | ComputeFullV); A, U, V row-major.  Returns false (U = V = I,
+// S = 0) for a non-finite A (Eigen: InvalidInput).
+__host__ __device__ inline bool eigen_jacobi_svd3_f32(const float (&A)[9], float (&U)[9], float (&S)[3], float (&V)[9]) {
+    float scale = fabsf(A[0]);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+    for (int k = 1; k < 9; ++k) scale = scale < fabsf(A[k]) ? fabsf(A[k]) : scale;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) U[k] = V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+    S[0] = S[1] = S[2] = 0.0f;
+    if (!(scale <= FLT_MAX)) return false;  // !isfinite (scale >= 0 or NaN)
+    if (scale == 0.0f) scale = 1.0f;
+    float W[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) W[k] = A[k] / scale;
+    float max_diag = fabsf(W[0]);
+    max_diag = max_diag < fabsf(W[4]) ? fabsf(W[4]) : max_diag;
+    max_diag = max_diag < fabsf(W[8]) ? fabsf(W[8]) : max_diag;
+    bool finished = false;
 #pragma nounroll
-    for (int sweep = 0; sweep < 40; ++sweep) {
-        float off = 0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int p = r == 2 ? 1 : 0, q = r == 0 ? 1 : 2;
-            float al = 0, be = 0, ga = 0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                al += W[k * 3 + p] * W[k * 3 + p];
-                be += W[k * 3 + q] * W[k * 3 + q];
-                ga += W[k * 3 + p] * W[k * 3 + q];
-            }
-            if (ga == 0) continue;
-            float nrm = sqrtf(al * be);
-            if (nrm == 0) continue;
-            float rel = fabsf(ga) / nrm;
-            if (rel > off) off = rel;
-            if (rel <= 1e-7f) continue;
-            float zeta = (be - al) / (2 * ga);
-            float t = (zeta >= 0 ? 1.0f : -1.0f) / (fabsf(zeta) + sqrtf(1.0f + zeta * zeta));
-            float c = 1.0f / sqrtf(1.0f + t * t);
-            float s = c * t;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float wp = W[k * 3 + p], wq = W[k * 3 + q];
-                W[k * 3 + p] = c * wp - s * wq;
-                W[k * 3 + q] = s * wp + c * wq;
-                float vp = V[k * 3 + p], vq = V[k * 3 + q];
-                V[k * 3 + p] = c * vp - s * vq;
-                V[k * 3 + q] = s * vp + c * vq;
-            }
-        }
-        if (off <= 1e-7f) break;
+    while (!finished) {
+        const bool a = jacobi_step_f32<1, 0>(W, U, V, max_diag);
+        const bool b = jacobi_step_f32<2, 0>(W, U, V, max_diag);
+        const bool c = jacobi_step_f32<2, 1>(W, U, V, max_diag);
+        finished = !(a || b || c);
     }
-    float sv[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-        sv[c] = sqrtf(W[0 * 3 + c] * W[0 * 3 + c] + W[1 * 3 + c] * W[1 * 3 + c] + W[2 * 3 + c] * W[2 * 3 + c]);
-    // the column order by descending singular value: the same three compare-and-swaps, on registers
-    int o0 = 0, o1 = 1, o2 = 2;
-    auto svo = [&](int i) { return i == 0 ? sv[0] : (i == 1 ? sv[1] : sv[2]); };
-    if (svo(o1) > svo(o0)) { const int tt = o0; o0 = o1; o1 = tt; }
-    if (svo(o2) > svo(o0)) { const int tt = o0; o0 = o2; o2 = tt; }
-    if (svo(o2) > svo(o1)) { const int tt = o1; o1 = o2; o2 = tt; }
-    const int ord[3] = {o0, o1, o2};
-    auto col = [&](const float (&M)[9], int k, int c) {  // M[k][c] for a runtime column c in 0..2
-        return c == 0 ? M[k * 3 + 0] : (c == 1 ? M[k * 3 + 1] : M[k * 3 + 2]);
-    };
-    float S[3], Vs[9], Ws[9], U[9];
+    for (int i = 0; i < 3; ++i) {
+        const float a = W[i * 3 + i];
+        S[i] = fabsf(a);
+        if (a < 0.0f) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        S[c] = svo(ord[c]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            Vs[k * 3 + c] = col(V, k, ord[c]);
-            Ws[k * 3 + c] = col(W, k, ord[c]);
+            for (int k = 0; k < 3; ++k) U[k * 3 + i] = -U[k * 3 + i];
         }
     }
-    int rank = 0;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-        if (S[c] > 1e-6f * (S[0] > 0 ? S[0] : 1.0f) && S[c] > 0) rank = c + 1;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) U[k] = 0.0f;
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-        if (c < rank)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) U[k * 3 + c] = Ws[k * 3 + c] / S[c];
-    if (rank == 0) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) U[k] = (k % 4 == 0) ? 1.0f : 0.0f;
-    } else {
-        if (rank == 1) {
-            int ax = 0;
-            float amin = fabsf(U[0]);
-#pragma unroll
-            for (int k = 1; k < 3; ++k)
-                if (fabsf(U[k * 3]) < amin) {
-                    amin = fabsf(U[k * 3]);
-                    ax = k;
-                }
-            const float e0 = ax == 0 ? 1.0f : 0.0f, e1 = ax == 1 ? 1.0f : 0.0f, e2 = ax == 2 ? 1.0f : 0.0f;
-            float c0 = U[1 * 3] * e2 - U[2 * 3] * e1;
-            float c1 = U[2 * 3] * e0 - U[0 * 3] * e2;
-            float c2 = U[0 * 3] * e1 - U[1 * 3] * e0;
-            float nn = sqrtf(c0 * c0 + c1 * c1 + c2 * c2);
-            U[0 * 3 + 1] = c0 / nn;
-            U[1 * 3 + 1] = c1 / nn;
-            U[2 * 3 + 1] = c2 / nn;
-        }
-        if (rank <= 2) {
-            U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
-            U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
-            U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
-        }
-    }
-    float d[3] = {1.0f, 1.0f, 1.0f};
-    if (det3_f32(U) * det3_f32(Vs) < 0) d[2] = -1.0f;
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    // the sort: for i = 0, 1 the first maximum of S[i..2] swapped to i; a zero maximum stops it
+    int pos = 0;
+    float mx = S[0];
+    if (S[1] > mx) { mx = S[1]; pos = 1; }
+    if (S[2] > mx) { mx = S[2]; pos = 2; }
+    if (mx == 0.0f) return true;
+    if (pos == 1) svd_swap_f32<0, 1>(S, U, V);
+    if (pos == 2) svd_swap_f32<0, 2>(S, U, V);
+    if (S[2] > S[1]) svd_swap_f32<1, 2>(S, U, V);  // (both zero: the sort stops, nothing to swap)
+    return true;
+}
+
+// Eigen::umeyama's rotation (with_scaling = false), Scalar = float; sigma and R row-major.
+__host__ __device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
+    float U[9], S[3], V[9];
+    eigen_jacobi_svd3_f32(A, U, S, V);
+    float d2 = 1.0f;
+    if (det3_f32(U) * det3_f32(V) < 0) d2 = -1.0f;
+    const float d[3] = {1.0f, 1.0f, d2};
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            float acc = 0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) acc += U[i * 3 + k] * d[k] * Vs[j * 3 + k];
-            R[i * 3 + j] = acc;
+            const float x0 = (U[i * 3 + 0] * d[0]) * V[j * 3 + 0];
+            const float x1 = (U[i * 3 + 1] * d[1]) * V[j * 3 + 1];
+            const float x2 = (U[i * 3 + 2] * d[2]) * V[j * 3 + 2];
+            R[i * 3 + j] = x0 + (x1 + x2);
         }
 }
 
@@ -465,8 +406,11 @@ __device__ inline int has_converged(const ConvParams& p, int32_t iterations, con
         cs.state = 1;  // CONVERGENCE_CRITERIA_ITERATIONS
         return 1;
     }
-    double cos_angle = 0.5 * ((double)Tinc[0] + (double)Tinc[5] + (double)Tinc[10] - 1);
-    double tsq = (double)Tinc[12] * Tinc[12] + (double)Tinc[13] * Tinc[13] + (double)Tinc[14] * Tinc[14];
+    // transformation_ is the ICP's Matrix4f: both expressions in float, only the results widened
+    const float tr = Tinc[0] + Tinc[5] + Tinc[10] - 1;
+    const double cos_angle = 0.5 * tr;
+    const float tsqf = Tinc[12] * Tinc[12] + Tinc[13] * Tinc[13] + Tinc[14] * Tinc[14];
+    const double tsq = tsqf;
     if (cos_angle >= p.rot_thr && tsq <= p.trans_thr) {
         if (cs.similar < p.max_similar) {
             ++cs.similar;

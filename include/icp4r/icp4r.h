@@ -93,6 +93,10 @@ typedef struct icp4r_params {
      * added into sigma in order.  kc follows from two facts of the reference's host:   */
     int32_t eigen_l1_bytes;                    /* L1d size Eigen queried: 0 = 32768; < 0 = no panels    */
     int32_t eigen_gebp_mr;                     /* gebp_traits<float>::mr: 0 = 8 (SSE, no FMA)           */
+    /* Known deviation: with fewer than 14 correspondences Eigen evaluates sigma coefficient by
+     * coefficient (lazyproduct, an alignment-dependent vectorised redux); the GEMM panel form above is
+     * used for every |C|.  Both host facts are assumptions about the node's build: parity with PCL
+     * itself is unpinned (the reference holds no fixtures).                            */
     int32_t reserved[6];
 } icp4r_params;
 

@@ -445,7 +445,6 @@ static void mat4_identity(float T[16]) {
     }
 
 DEFINE_SVD3(svd3_f64, double, sqrt, fabs, 1e-15, 1e-12)
-DEFINE_SVD3(svd3_f32, float, sqrtf, fabsf, 1e-7f, 1e-6f)
 
 #define DEFINE_DET3(NAME, REAL)                                                                     \
     static REAL NAME(const REAL M[9]) {                                                             \
@@ -453,7 +452,6 @@ DEFINE_SVD3(svd3_f32, float, sqrtf, fabsf, 1e-7f, 1e-6f)
                M[2] * (M[3] * M[7] - M[4] * M[6]);                                                  \
     }
 DEFINE_DET3(det3_f64, double)
-DEFINE_DET3(det3_f32, float)
 
 /* R = U * diag(1,1,s) * V^T with s = -1 iff det(U)*det(V) < 0 (Eigen 3.3 umeyama). */
 #define DEFINE_ROT(NAME, REAL, SVD, DET)                                                            \
@@ -470,7 +468,170 @@ DEFINE_DET3(det3_f32, float)
             }                                                                                       \
     }
 DEFINE_ROT(rot_f64, double, svd3_f64, det3_f64)
-DEFINE_ROT(rot_f32, float, svd3_f32, det3_f32)
+
+/* ------------------------------------------------------------------------------------------ */
+/* PCL's float rotation, restated from Eigen 3.3 (the reference's PCL 1.8.1 / Eigen 3.3.4, SURVEY  */
+/* §8c; iterative_closest_point.cpp:514 -> TransformationEstimationSVD -> pcl::umeyama ->          */
+/* Eigen::umeyama, Geometry/Umeyama.h):                                                            */
+/*   JacobiSVD<Matrix3f> svd(sigma, ComputeFullU | ComputeFullV)   (SVD/JacobiSVD.h compute())    */
+/*   S = (1, 1, 1); if (det(U) * det(V) < 0) S(2) = -1;                                            */
+/*   R = U * S.asDiagonal() * V^T                                                                   */
+/* JacobiSVD for a square matrix takes no QR preconditioner: the matrix is divided by its largest  */
+/* |coefficient|, then two-sided 2x2 Jacobi sweeps over (p, q) = (1, 0), (2, 0), (2, 1) run until  */
+/* no off-diagonal pair exceeds max(FLT_MIN, 2 eps * the largest |diagonal| seen); each step takes  */
+/* real_2x2_jacobi_svd (misc/RealSvd2x2.h): a rotation that symmetrises the 2x2 block, then         */
+/* JacobiRotation::makeJacobi (Jacobi/Jacobi.h) for the symmetric block, j_left = rot1 * j_right^T,  */
+/* applied to the work matrix's rows and columns and accumulated into U's and V's columns          */
+/* (apply_rotation_in_the_plane: x' = c x + s y, y' = -s x + c y; a no-op for c = 1, s = 0).        */
+/* Then negative diagonal entries flip U's column, the singular values are scaled back, and a      */
+/* selection sort by swaps (maxCoeff: the first maximum; stops at a zero maximum) orders them.     */
+/* The product R: Eigen's coefficient-based lazy product of fixed 3x3 operands sums each            */
+/* coefficient with the unrolled redux, x0 + (x1 + x2), with x_k = (U(i,k) * S(k)) * V(j,k).        */
+/* Every operation in float, unfused, in this order (SSE, no FMA).  Matrices row-major M[r*3+c].   */
+typedef struct { float c, s; } jrot_f;
+
+/* apply_rotation_in_the_plane(x, y, (c, s)) over 3 elements of stride `inc` */
+static void plane_rot_f(float* x, float* y, int inc, float c, float s) {
+    if (c == 1.0f && s == 0.0f) return;
+    for (int i = 0; i < 3; ++i) {
+        const float xi = x[i * inc], yi = y[i * inc];
+        x[i * inc] = c * xi + s * yi;
+        y[i * inc] = -s * xi + c * yi;
+    }
+}
+
+/* misc/RealSvd2x2.h real_2x2_jacobi_svd(matrix, p, q, &j_left, &j_right) */
+static void real_2x2_jacobi_svd_f(const float* W, int p, int q, jrot_f* jl, jrot_f* jr) {
+    float m00 = W[p * 3 + p], m01 = W[p * 3 + q], m10 = W[q * 3 + p], m11 = W[q * 3 + q];
+    jrot_f rot1;
+    const float t = m00 + m11;
+    const float d = m10 - m01;
+    if (fabsf(d) < FLT_MIN) {
+        rot1.s = 0.0f;
+        rot1.c = 1.0f;
+    } else {
+        const float u = t / d;
+        const float tmp = sqrtf(1.0f + u * u);
+        rot1.s = 1.0f / tmp;
+        rot1.c = u / tmp;
+    }
+    /* m.applyOnTheLeft(0, 1, rot1) */
+    if (!(rot1.c == 1.0f && rot1.s == 0.0f)) {
+        const float x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+        m00 = rot1.c * x0 + rot1.s * y0;
+        m10 = -rot1.s * x0 + rot1.c * y0;
+        m01 = rot1.c * x1 + rot1.s * y1;
+        m11 = -rot1.s * x1 + rot1.c * y1;
+    }
+    (void)m10;
+    /* j_right->makeJacobi(m, 0, 1): makeJacobi(x = m(0,0), y = m(0,1), z = m(1,1)) */
+    const float deno = 2.0f * fabsf(m01);
+    if (deno < FLT_MIN) {
+        jr->c = 1.0f;
+        jr->s = 0.0f;
+    } else {
+        const float tau = (m00 - m11) / deno;
+        const float w = sqrtf(tau * tau + 1.0f);
+        float tt;
+        if (tau > 0.0f)
+            tt = 1.0f / (tau + w);
+        else
+            tt = 1.0f / (tau - w);
+        const float sign_t = tt > 0.0f ? 1.0f : -1.0f;
+        const float n = 1.0f / sqrtf(tt * tt + 1.0f);
+        jr->s = -sign_t * (m01 / fabsf(m01)) * fabsf(tt) * n;
+        jr->c = n;
+    }
+    /* *j_left = rot1 * j_right->transpose(): (c1 c2 - s1 s2, c1 s2 + s1 c2) with (c2, s2) = (c_r, -s_r) */
+    const float c2 = jr->c, s2 = -jr->s;
+    jl->c = rot1.c * c2 - rot1.s * s2;
+    jl->s = rot1.c * s2 + rot1.s * c2;
+}
+
+static float det3_eigen_f(const float* M) { /* LU/Determinant.h bruteforce_det3_helper */
+    return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+/* JacobiSVD<Matrix3f>(A, ComputeFullU | ComputeFullV).  Returns 0, or -1 for a non-finite A. */
+static int eigen_jacobi_svd3_f(const float A[9], float U[9], float S[3], float V[9]) {
+    const float precision = 2.0f * FLT_EPSILON, consider_as_zero = FLT_MIN;
+    float scale = fabsf(A[0]);
+    for (int k = 1; k < 9; ++k) scale = scale < fabsf(A[k]) ? fabsf(A[k]) : scale;
+    for (int k = 0; k < 9; ++k) U[k] = V[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+    if (!isfinite(scale)) {
+        S[0] = S[1] = S[2] = 0.0f;
+        return -1;
+    }
+    if (scale == 0.0f) scale = 1.0f;
+    float W[9];
+    for (int k = 0; k < 9; ++k) W[k] = A[k] / scale;
+    float max_diag = fabsf(W[0]);
+    max_diag = max_diag < fabsf(W[4]) ? fabsf(W[4]) : max_diag;
+    max_diag = max_diag < fabsf(W[8]) ? fabsf(W[8]) : max_diag;
+    int finished = 0;
+    while (!finished) {
+        finished = 1;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float pm = precision * max_diag;
+                const float threshold = consider_as_zero < pm ? pm : consider_as_zero;
+                if (fabsf(W[p * 3 + q]) > threshold || fabsf(W[q * 3 + p]) > threshold) {
+                    finished = 0;
+                    jrot_f jl, jr;
+                    real_2x2_jacobi_svd_f(W, p, q, &jl, &jr);
+                    plane_rot_f(W + p * 3, W + q * 3, 1, jl.c, jl.s); /* W.applyOnTheLeft(p, q, j_left) */
+                    plane_rot_f(U + p, U + q, 3, jl.c, jl.s);         /* U.applyOnTheRight(p, q, j_left^T) */
+                    plane_rot_f(W + p, W + q, 3, jr.c, -jr.s);        /* W.applyOnTheRight(p, q, j_right) */
+                    plane_rot_f(V + p, V + q, 3, jr.c, -jr.s);        /* V.applyOnTheRight(p, q, j_right) */
+                    const float ap = fabsf(W[p * 3 + p]), aq = fabsf(W[q * 3 + q]);
+                    const float mpq = ap < aq ? aq : ap;
+                    max_diag = max_diag < mpq ? mpq : max_diag;
+                }
+            }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = W[i * 3 + i];
+        S[i] = fabsf(a);
+        if (a < 0.0f)
+            for (int k = 0; k < 3; ++k) U[k * 3 + i] = -U[k * 3 + i];
+    }
+    for (int i = 0; i < 3; ++i) S[i] *= scale;
+    for (int i = 0; i < 3; ++i) {
+        int pos = i;
+        float mx = S[i];
+        for (int k = i + 1; k < 3; ++k)
+            if (S[k] > mx) {
+                mx = S[k];
+                pos = k;
+            }
+        if (mx == 0.0f) break;
+        if (pos != i) {
+            float t = S[i];
+            S[i] = S[pos];
+            S[pos] = t;
+            for (int k = 0; k < 3; ++k) {
+                t = U[k * 3 + i]; U[k * 3 + i] = U[k * 3 + pos]; U[k * 3 + pos] = t;
+                t = V[k * 3 + i]; V[k * 3 + i] = V[k * 3 + pos]; V[k * 3 + pos] = t;
+            }
+        }
+    }
+    return 0;
+}
+
+/* Eigen::umeyama's rotation (with_scaling = false), Scalar = float. */
+static void rot_f32(const float sigma[9], float R[9]) {
+    float U[9], S[3], V[9];
+    eigen_jacobi_svd3_f(sigma, U, S, V);
+    float d[3] = {1.0f, 1.0f, 1.0f};
+    if (det3_eigen_f(U) * det3_eigen_f(V) < 0) d[2] = -1.0f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const float x0 = (U[i * 3 + 0] * d[0]) * V[j * 3 + 0];
+            const float x1 = (U[i * 3 + 1] * d[1]) * V[j * 3 + 1];
+            const float x2 = (U[i * 3 + 2] * d[2]) * V[j * 3 + 2];
+            R[i * 3 + j] = x0 + (x1 + x2);
+        }
+}
 
 static inline double huber_w(double d2, double delta) {
     if (!(delta < INFINITY)) return 1.0;
@@ -718,9 +879,12 @@ static int has_converged(const oracle_params* p, int32_t iterations, const float
         *state = CONV_ITERATIONS;
         return 1;
     }
-    double cos_angle = 0.5 * ((double)Tinc[0] + (double)Tinc[5] + (double)Tinc[10] - 1);
-    double translation_sqr =
-        (double)Tinc[12] * Tinc[12] + (double)Tinc[13] * Tinc[13] + (double)Tinc[14] * Tinc[14];
+    /* transformation_ is the ICP's Matrix4 (= Matrix4f): both expressions are evaluated in float and
+     * only their results widened to double */
+    const float tr = Tinc[0] + Tinc[5] + Tinc[10] - 1;
+    double cos_angle = 0.5 * tr;
+    const float tsq = Tinc[12] * Tinc[12] + Tinc[13] * Tinc[13] + Tinc[14] * Tinc[14];
+    double translation_sqr = tsq;
     if (cos_angle >= rot_thr && translation_sqr <= trans_thr) {
         if (*similar < p->max_iterations_similar_transforms) {
             ++*similar;

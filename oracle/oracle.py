@@ -102,6 +102,8 @@ def lib():
                                      C.c_void_p, C.c_double, C.c_int32]
         L.oracle_fitness.restype = C.c_double
         L.oracle_kdtree_leaf_visits.restype = C.c_int64
+        L.oracle_rot_f32.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_rot_f32.restype = None
         L.oracle_calc_dist.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_calc_dist.restype = C.c_float
         L.oracle_calc_heading.argtypes = [C.c_void_p, C.c_void_p]
@@ -192,6 +194,14 @@ def align(src: np.ndarray, tgt: np.ndarray, guess: np.ndarray | None = None, tra
     if aligned:
         res["aligned"] = out
     return res
+
+
+def rot_f32(sigma: np.ndarray) -> np.ndarray:
+    """PCL's float Umeyama rotation of a 3x3 sigma (row-major): Eigen's JacobiSVD<Matrix3f> + umeyama."""
+    s = np.ascontiguousarray(np.asarray(sigma, np.float32).reshape(9))
+    R = np.empty(9, np.float32)
+    lib().oracle_rot_f32(s.ctypes.data, R.ctypes.data)
+    return R.reshape(3, 3)
 
 
 def nearest(query: np.ndarray, tgt: np.ndarray, nn: int = NN_BRUTE):

@@ -115,6 +115,157 @@ def umeyama_sigma_f32(s: np.ndarray, d: np.ndarray, kc: int | None = None):
     return sigma.reshape(3, 3), ms, md
 
 
+def _plane(x, y, c, s):
+    """Eigen apply_rotation_in_the_plane on two equal-length float32 lists (in place)."""
+    if c == F32(1) and s == F32(0):
+        return
+    for i in range(len(x)):
+        xi, yi = x[i], y[i]
+        x[i] = c * xi + s * yi
+        y[i] = -s * xi + c * yi
+
+
+def eigen_jacobi_svd3_f32(A):
+    """Eigen 3.3 JacobiSVD<Matrix3f>(A, ComputeFullU | ComputeFullV) in float32 scalars, written from
+    Eigen's SVD/JacobiSVD.h compute(), misc/RealSvd2x2.h and Jacobi/Jacobi.h (square input: no QR
+    preconditioner; scale by the largest |a_ij|; two-sided 2x2 sweeps over (1,0), (2,0), (2,1) until
+    every off-diagonal pair is within max(FLT_MIN, 2 eps * max |diag| seen); sign fix; swap sort).
+    Returns U, S, V as 3x3 / 3 float32 arrays (row-major, U[r][c])."""
+    one, zero = F32(1), F32(0)
+    fmin = F32(np.finfo(np.float32).tiny)
+    precision = F32(2) * F32(np.finfo(np.float32).eps)
+    A = [[F32(A[r][c]) for c in range(3)] for r in range(3)]
+    scale = zero
+    for r in range(3):
+        for c in range(3):
+            scale = abs(A[r][c]) if scale < abs(A[r][c]) else scale
+    U = [[one if r == c else zero for c in range(3)] for r in range(3)]
+    V = [[one if r == c else zero for c in range(3)] for r in range(3)]
+    if not np.isfinite(scale):
+        return np.array(U, F32), np.zeros(3, F32), np.array(V, F32)
+    if scale == zero:
+        scale = one
+    W = [[A[r][c] / scale for c in range(3)] for r in range(3)]
+    maxd = zero
+    for i in range(3):
+        maxd = abs(W[i][i]) if maxd < abs(W[i][i]) else maxd
+    finished = False
+    while not finished:
+        finished = True
+        for p in (1, 2):
+            for q in range(p):
+                pm = precision * maxd
+                thr = pm if fmin < pm else fmin
+                if abs(W[p][q]) > thr or abs(W[q][p]) > thr:
+                    finished = False
+                    # real_2x2_jacobi_svd
+                    m = [[W[p][p], W[p][q]], [W[q][p], W[q][q]]]
+                    t = m[0][0] + m[1][1]
+                    d = m[1][0] - m[0][1]
+                    if abs(d) < fmin:
+                        c1, s1 = one, zero
+                    else:
+                        u = t / d
+                        tmp = np.sqrt(one + u * u)
+                        s1 = one / tmp
+                        c1 = u / tmp
+                    r0, r1 = [m[0][0], m[0][1]], [m[1][0], m[1][1]]
+                    _plane(r0, r1, c1, s1)
+                    m = [r0, r1]
+                    x, y, z = m[0][0], m[0][1], m[1][1]
+                    deno = F32(2) * abs(y)
+                    if deno < fmin:
+                        cr, sr = one, zero
+                    else:
+                        tau = (x - z) / deno
+                        w = np.sqrt(tau * tau + one)
+                        tt = one / (tau + w) if tau > zero else one / (tau - w)
+                        sign_t = one if tt > zero else -one
+                        n = one / np.sqrt(tt * tt + one)
+                        sr = -sign_t * (y / abs(y)) * abs(tt) * n
+                        cr = n
+                    c2, s2 = cr, -sr
+                    cl = c1 * c2 - s1 * s2
+                    sl = c1 * s2 + s1 * c2
+                    # W rows p, q (left); U cols (right, j_left^T^T); W, V cols (right, j_right^T)
+                    _plane(W[p], W[q], cl, sl)
+                    for M, c, s in ((U, cl, sl), (W, cr, -sr), (V, cr, -sr)):
+                        cp, cq = [M[k][p] for k in range(3)], [M[k][q] for k in range(3)]
+                        _plane(cp, cq, c, s)
+                        for k in range(3):
+                            M[k][p], M[k][q] = cp[k], cq[k]
+                    ap, aq = abs(W[p][p]), abs(W[q][q])
+                    mpq = aq if ap < aq else ap
+                    maxd = mpq if maxd < mpq else maxd
+    S = [zero, zero, zero]
+    for i in range(3):
+        a = W[i][i]
+        S[i] = abs(a)
+        if a < zero:
+            for k in range(3):
+                U[k][i] = -U[k][i]
+    S = [s * scale for s in S]
+    for i in range(3):
+        pos, mx = i, S[i]
+        for k in range(i + 1, 3):
+            if S[k] > mx:
+                pos, mx = k, S[k]
+        if mx == zero:
+            break
+        if pos != i:
+            S[i], S[pos] = S[pos], S[i]
+            for k in range(3):
+                U[k][i], U[k][pos] = U[k][pos], U[k][i]
+                V[k][i], V[k][pos] = V[k][pos], V[k][i]
+    return np.array(U, F32), np.array(S, F32), np.array(V, F32)
+
+
+def _det3_f32(M):
+    """Eigen's bruteforce 3x3 determinant, float32."""
+    return (M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0])
+            + M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]))
+
+
+def umeyama_rotation_f32(sigma):
+    """Eigen::umeyama's rotation, Scalar = float: R = U diag(1, 1, +-1) V^T, each coefficient
+    x0 + (x1 + x2) (the lazy product's unrolled redux), x_k = (U[i][k] * S_k) * V[j][k]."""
+    U, _, V = eigen_jacobi_svd3_f32(sigma)
+    Sd = [F32(1), F32(1), F32(1)]
+    if _det3_f32(U) * _det3_f32(V) < F32(0):
+        Sd[2] = F32(-1)
+    R = np.empty((3, 3), F32)
+    for i in range(3):
+        for j in range(3):
+            x = [(U[i, k] * Sd[k]) * V[j, k] for k in range(3)]
+            R[i, j] = x[0] + (x[1] + x[2])
+    return R
+
+
+def umeyama_f32(s: np.ndarray, d: np.ndarray, kc: int | None = None) -> np.ndarray:
+    """pcl::umeyama (= Eigen::umeyama, no scaling) in float: T = [R | mu_d - R mu_s] as Matrix4f;
+    t_i = mu_d_i - ((R_i0 mu_s_0 + R_i1 mu_s_1) + R_i2 mu_s_2) (a dynamic-size block times a vector:
+    the sequential redux)."""
+    sigma, ms, md = umeyama_sigma_f32(s, d, kc)
+    R = umeyama_rotation_f32(sigma)
+    T = np.eye(4, dtype=F32)
+    T[:3, :3] = R
+    for i in range(3):
+        rs = R[i, 0] * ms[0]
+        rs = R[i, 1] * ms[1] + rs
+        rs = R[i, 2] * ms[2] + rs
+        T[i, 3] = md[i] - rs
+    return T, sigma, ms, md
+
+
+def pcl_converged_transform(Tinc) -> tuple[float, float]:
+    """DefaultConvergenceCriteria's cos_angle and translation_sqr: float expressions over the
+    Matrix4f increment, widened to double only at the end."""
+    T = np.asarray(Tinc, F32)
+    tr = T[0, 0] + T[1, 1] + T[2, 2] - F32(1)
+    tsq = T[0, 3] * T[0, 3] + T[1, 3] * T[1, 3] + T[2, 3] * T[2, 3]
+    return 0.5 * float(tr), float(tsq)
+
+
 def mat4_mul_f32(A: np.ndarray, B: np.ndarray) -> np.ndarray:
     """Matrix4f product, k-ordered unfused float32 accumulation (Eigen lazy product)."""
     A = np.asarray(A, F32)
@@ -130,9 +281,20 @@ def mat4_mul_f32(A: np.ndarray, B: np.ndarray) -> np.ndarray:
     return C
 
 
+def _seq_sum_f64(v: np.ndarray) -> float:
+    """A sequential double sum of float terms (PCL's calculateMSE / getFitnessScore loops)."""
+    v = np.asarray(v, np.float64)
+    return float(np.cumsum(v)[-1]) if len(v) else 0.0
+
+
 def icp(src: np.ndarray, tgt: np.ndarray, max_iterations: int = 10, mse_abs: float = 1e-12,
-        max_dist: float = np.sqrt(np.finfo(np.float64).max)):
-    """PCL default ICP with float64 Umeyama.  Returns dict(T, iterations, converged, fitness, trace)."""
+        max_dist: float = np.sqrt(np.finfo(np.float64).max), numerics: str = "f64"):
+    """PCL default ICP.  numerics "f64": the Umeyama solve in float64 (the golden fixtures' form);
+    "f32": PCL's own float path end to end (float centroids, Eigen's blocked sigma GEMM, Eigen's
+    JacobiSVD<Matrix3f>, float R and t; sequential double MSE and fitness sums).
+    Returns dict(T, iterations, converged, fitness, trace)."""
+    if numerics == "f32":
+        return _icp_f32(src, tgt, max_iterations, mse_abs, max_dist)
     src = np.asarray(src, F32)[:, :3]
     tgt = np.asarray(tgt, F32)[:, :3]
     X = src.copy()
@@ -160,8 +322,7 @@ def icp(src: np.ndarray, tgt: np.ndarray, max_iterations: int = 10, mse_abs: flo
         if it >= max_iterations:
             converged, state = True, 1
             break
-        cos_a = 0.5 * (float(Tinc[0, 0]) + float(Tinc[1, 1]) + float(Tinc[2, 2]) - 1)
-        tsq = float(Tinc[0, 3]) ** 2 + float(Tinc[1, 3]) ** 2 + float(Tinc[2, 3]) ** 2
+        cos_a, tsq = pcl_converged_transform(Tinc)
         if cos_a >= 1.0 and tsq <= 0.0:
             converged, state = True, 2
             break
@@ -172,5 +333,45 @@ def icp(src: np.ndarray, tgt: np.ndarray, max_iterations: int = 10, mse_abs: flo
     Y = transform(final, src)
     _, fd = nearest(Y, tgt)
     fitness = float(fd.astype(np.float64).sum() / len(fd)) if len(fd) else np.finfo(np.float64).max
+    return {"T": final, "iterations": it, "converged": converged, "state": state, "fitness": fitness,
+            "trace": trace}
+
+
+def _icp_f32(src, tgt, max_iterations, mse_abs, max_dist):
+    src = np.asarray(src, F32)[:, :3]
+    tgt = np.asarray(tgt, F32)[:, :3]
+    X = src.copy()
+    final = np.eye(4, dtype=F32)
+    prev_mse = np.finfo(np.float64).max
+    max_d2 = max_dist * max_dist
+    it, trace, converged, state = 0, [], False, 0
+    while True:
+        idx, d2 = nearest(X, tgt)
+        keep = d2.astype(np.float64) <= max_d2
+        nk = int(keep.sum())
+        if nk < 3:
+            converged, state = False, 5
+            break
+        Tinc, sigma, ms, md = umeyama_f32(X[keep], tgt[idx[keep]])
+        X = transform(Tinc, X)
+        final = mat4_mul_f32(Tinc, final)
+        it += 1
+        mse = _seq_sum_f64(d2[keep]) / nk
+        trace.append({"T_inc": Tinc, "T_final": final.copy(), "mse": mse, "ncorr": nk, "sigma": sigma,
+                      "mu_src": ms, "mu_dst": md})
+        if it >= max_iterations:
+            converged, state = True, 1
+            break
+        cos_a, tsq = pcl_converged_transform(Tinc)
+        if cos_a >= 1.0 and tsq <= 0.0:
+            converged, state = True, 2
+            break
+        if abs(mse - prev_mse) < mse_abs:
+            converged, state = True, 3
+            break
+        prev_mse = mse
+    Y = transform(final, src)
+    _, fd = nearest(Y, tgt)
+    fitness = _seq_sum_f64(fd) / len(fd) if len(fd) else np.finfo(np.float64).max
     return {"T": final, "iterations": it, "converged": converged, "state": state, "fitness": fitness,
             "trace": trace}

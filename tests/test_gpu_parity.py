@@ -176,6 +176,23 @@ def test_sigma_panels_batch_and_solo(gpu_ctx, oracle_mod, solo, monkeypatch):
         assert res[k]["fitness"] == o["fitness"], k
 
 
+def test_device_eigen_svd_rotation_matches_oracle(gpu_ctx, oracle_mod):
+    """The device's float Umeyama rotation (icp4r_math.hpp: Eigen 3.3 JacobiSVD<Matrix3f> + umeyama,
+    the solve of every PCL-numerics update) equals the oracle's bit for bit, one thread per matrix."""
+    import ctypes as C
+
+    import icp4r
+    from test_oracle import _sigma_cases
+
+    S = np.stack(_sigma_cases(np.random.default_rng(11), 4096)).reshape(-1, 9).astype(np.float32)
+    R = np.zeros_like(S)
+    L = icp4r.load()
+    assert L.icp4r__test_rot_f32(gpu_ctx.handle, C.c_void_p(S.ctypes.data), C.c_void_p(R.ctypes.data), len(S)) == 0
+    Ro = np.stack([oracle_mod.rot_f32(s) for s in S]).reshape(-1, 9)
+    bad = (R.view(np.uint32) != Ro.view(np.uint32)).any(1)
+    assert not bad.any(), f"{int(bad.sum())} of {len(S)} rotations differ"
+
+
 def test_known_answers(gpu_ctx, golden):
     import icp4r
 

@@ -78,6 +78,92 @@ def test_pcl_float_sigma_matches_numpy_twin(oracle_mod, golden, which):
 
 
 @pytest.mark.parametrize("which", [0, 1])
+def test_pcl_float_icp_matches_numpy_twin(oracle_mod, golden, which):
+    """The oracle's whole float registration equals an independent numpy restatement bit for bit at
+    every iteration: sequential float centroids, Eigen's blocked sigma GEMM, Eigen 3.3's
+    JacobiSVD<Matrix3f> and umeyama product order, the float transformCloud and composition, the
+    convergence expressions in float, and the sequential double MSE / fitness sums."""
+    import sys
+    sys.path.insert(0, GOLDEN_DIR)
+    import numpy_twin as tw
+
+    case = golden["cases"][which]
+    src, tgt = load_case_clouds(case)
+    it = case["max_iterations"]
+    t = tw.icp(src, tgt, max_iterations=it, numerics="f32")
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=it, trace=True)
+    assert o["iterations"] == t["iterations"] and o["convergence_state"] == t["state"]
+    for k, tk in enumerate(t["trace"]):
+        assert (o["trace"]["T_inc"][k] == tk["T_inc"]).all(), k
+        assert (o["trace"]["T_final"][k] == tk["T_final"]).all(), k
+        assert o["trace"]["mse"][k] == tk["mse"], k
+    assert (o["T"] == t["T"]).all() and o["fitness"] == t["fitness"]
+
+
+def _sigma_cases(rng, count):
+    """3x3 float32 matrices of the shapes a registration meets and of the SVD's edge cases."""
+    out = []
+    for t in range(count):
+        S = rng.normal(0, 100, (3, 3)).astype(np.float32)
+        if t % 8 == 1:
+            S[2] = S[1] * np.float32(0.5)  # rank 2
+        elif t % 8 == 2:
+            S = (np.eye(3) * 500 + 0.01 * S).astype(np.float32)  # near identity
+        elif t % 8 == 3:
+            a = rng.uniform(-0.2, 0.2)
+            Rz = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+            S = (Rz @ np.diag([400.0, 90.0, 0.5 + t % 3]) + rng.normal(0, 0.01, (3, 3))).astype(np.float32)
+        elif t % 8 == 4:
+            S = (S * np.float32(2.0 ** rng.integers(-20, 20))).astype(np.float32)
+        elif t % 8 == 5:
+            S = np.diag(rng.normal(0, 5, 3)).astype(np.float32)  # diagonal, signs, order
+        elif t % 8 == 6:
+            S = np.outer(rng.normal(size=3), rng.normal(size=3)).astype(np.float32)  # rank 1
+        elif t % 16 == 7:
+            S = np.zeros((3, 3), np.float32)
+        out.append(S)
+    return out
+
+
+def test_eigen_svd_rotation_matches_numpy_twin(oracle_mod):
+    """PCL's float rotation (Eigen 3.3 JacobiSVD<Matrix3f> + umeyama): the C oracle and the numpy
+    restatement agree bit for bit over registration-shaped and edge-case sigmas."""
+    import sys
+    sys.path.insert(0, GOLDEN_DIR)
+    import numpy_twin as tw
+
+    rng = np.random.default_rng(11)
+    for k, S in enumerate(_sigma_cases(rng, 600)):
+        Ro = oracle_mod.rot_f32(S)
+        Rt = tw.umeyama_rotation_f32(S)
+        assert (Ro.view(np.uint32) == Rt.view(np.uint32)).all(), (k, S, Ro, Rt)
+
+
+def test_eigen_svd_known_answers():
+    """JacobiSVD<Matrix3f> semantics on inputs with known decompositions: singular values
+    descending, U S V^T reproduces the input, U and V orthonormal; a diagonal input keeps its
+    axes (with U's column sign fixes); R of a rotated diagonal spread is that rotation."""
+    import sys
+    sys.path.insert(0, GOLDEN_DIR)
+    import numpy_twin as tw
+
+    U, S, V = tw.eigen_jacobi_svd3_f32(np.diag([2.0, -7.0, 3.0]).astype(np.float32))
+    assert list(S) == [7.0, 3.0, 2.0]
+    assert np.allclose(U @ np.diag(S) @ V.T, np.diag([2.0, -7.0, 3.0]), atol=1e-6)
+    rng = np.random.default_rng(2)
+    for _ in range(50):
+        A = rng.normal(0, 10, (3, 3)).astype(np.float32)
+        U, S, V = tw.eigen_jacobi_svd3_f32(A)
+        assert S[0] >= S[1] >= S[2] >= 0
+        assert np.allclose(U @ np.diag(S) @ V.T, A, atol=2e-5 * np.abs(A).max())
+        assert np.allclose(U.T @ U, np.eye(3), atol=2e-6) and np.allclose(V.T @ V, np.eye(3), atol=2e-6)
+    a = 0.1
+    R0 = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+    R = tw.umeyama_rotation_f32((R0 @ np.diag([300.0, 80.0, 2.0])).astype(np.float32))
+    assert np.abs(R - R0).max() < 1e-6
+
+
+@pytest.mark.parametrize("which", [0, 1])
 def test_icp_pcl_float_within_bar_of_f64(oracle_mod, golden, which):
     """PCL's float Umeyama vs the exact solve: the reference's own float noise (documented)."""
     case = golden["cases"][which]

@@ -16,7 +16,7 @@ import os
 import sys
 
 os.environ["ICP4R_PHASE_TICKS"] = "1"
-os.environ["ICP4R_GROUPS"] = "1"
+os.environ.setdefault("ICP4R_GROUPS", "1")  # (group 0's pairs are the ones stamped)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 sys.path.insert(0, ROOT)
@@ -35,6 +35,8 @@ def main():
     from bench import make_shard
 
     P, n = args.pairs, args.points
+    G = max(1, int(os.environ["ICP4R_GROUPS"]))
+    Pg = P // G  # pair group 0 (the stamped one)
     src_h, tgt_h = make_shard(0, P, n)
     dev = torch.device("cuda", 0)
     src = torch.from_numpy(src_h.reshape(-1, 4)).to(dev)
@@ -50,13 +52,13 @@ def main():
     for _ in range(2):
         ctx.align_batch_device(batch, params, results.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    k = 32 + 12 * P
+    k = 32 + 12 * Pg
     buf = (C.c_uint64 * k)()
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
     if lib.icp4r__debug_ticks(ctx._h, buf, k):
         raise RuntimeError(lib.icp4r_last_error())
-    raw = np.array(buf[32 + 4 * P:], dtype=np.uint64).reshape(P, 8)
+    raw = np.array(buf[32 + 4 * Pg:], dtype=np.uint64).reshape(Pg, 8)
     hw = raw[:, 5]
     if hw.any():  # fold-wave placement: per CU, how many fold waves share each SIMD
         hid = (hw & 0xffffffff).astype(np.int64)
@@ -73,7 +75,8 @@ def main():
     ok = (t > 0).all(axis=1)
     t = t[ok]
     t0 = t[:, 0].min()
-    out = {"pairs_stamped": int(ok.sum()), "span_us": float(t[:, 4].max() - t0),
+    out = {"groups": G, "env": {k: v for k, v in os.environ.items() if k.startswith("ICP4R_")},
+           "pairs_stamped": int(ok.sum()), "span_us": float(t[:, 4].max() - t0),
            "start_spread_us": float(t[:, 0].max() - t0)}
     pct = lambda v: {f"p{q}": round(float(np.percentile(v, q)), 1) for q in (0, 10, 50, 90, 100)}
     out["start"] = pct(t[:, 0] - t0)
