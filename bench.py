@@ -76,6 +76,10 @@ def parse(argv=None):
                     help="N>1: the results' all-gather through the library's RCCL communicator "
                          "(icp4r_gather_results, include/icp4r/icp4r_multi.h) or torch.distributed's")
     ap.add_argument("--dry-run", action="store_true", help="launcher/shard/gather only, gloo on CPU (tests)")
+    ap.add_argument("--plan", action="append", default=[], metavar="NAME=VALUE",
+                    help="plan option for the library context (icp4r_set_plan_option; A/B runs, DESIGN.md §6)")
+    ap.add_argument("--plan-from-env", action="store_true",
+                    help="(tools) also take plan options from ICP4R_<NAME> environment variables")
     return ap.parse_args(argv)
 
 
@@ -98,6 +102,18 @@ def launch(args, argv) -> int:
 def _env_rank():
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def user_plan(args) -> dict:
+    """The plan options of this run: --plan NAME=VALUE (and, for the A/B tools, ICP4R_<NAME>
+    variables with --plan-from-env).  The library itself reads no environment."""
+    import icp4r
+
+    out = icp4r.env_plan() if args.plan_from_env else {}
+    for kv in args.plan:
+        k, v = kv.split("=", 1)
+        out[k.strip()] = int(v)
+    return out
 
 
 def _metric():
@@ -354,7 +370,7 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
     calls = kcalls  # (per-registration launch counts below are over the timing calls)
     evals = st["evaluations"] / max(nn_launches, 1)
     tests = st["box_tests"] / max(nn_launches, 1)
-    plan = icp4r.plan(1, n, m)
+    plan = icp4r.plan(1, n, m, ctx=ctx)
     iters = int(r.iterations)
     if plan["solo"]:
         return _solo_measure(ctx, r, name, workload, src, tgt, params, oparams, walls, dev_ms, calls, nn_ms,
@@ -518,8 +534,9 @@ def run_gpu(args) -> int:
 
     sha = library_sha256()
     which = [c for c in args.configs.split(",") if c and not (args.no_c5 and c == "C5")]
+    opts = user_plan(args)
     if args.no_c3:  # the single-pair configs alone (tools/profile_round.sh profiles them this way)
-        ctx = icp4r.Context(dev.index)
+        ctx = icp4r.Context(dev.index, plan=opts)
         out = single_pair_configs(ctx, which, sha, None if args.no_cpu else args.config_cpu_seconds, args.check > 0)
         ctx.close()
         if rank == 0:
@@ -539,7 +556,7 @@ def run_gpu(args) -> int:
     results = torch.zeros((P, 96), dtype=torch.uint8, device=dev)
     gathered = torch.zeros((world * P, 96), dtype=torch.uint8, device=dev)
 
-    ctx = icp4r.Context(dev.index)
+    ctx = icp4r.Context(dev.index, plan=opts)
     # fixed work: 20 iterations for every pair (the |ΔMSE| and exact-identity stops disabled)
     params = icp4r.default_params(max_iterations=args.iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
 
@@ -667,34 +684,32 @@ def run_gpu(args) -> int:
         del slots, slot_batches, src_pin, tgt_pin
 
     # Kernel-level measurements (roofline, test and update kernels): the timed steps run the batch as
-    # pair groups on several streams (icp4r run_pairs, ICP4R_GROUPS), where one group's kernels
+    # pair groups on several streams (icp4r run_pairs, plan option groups), where one group's kernels
     # overlap another's and a launch time is not one kernel's; so the same steps are repeated once
     # more with a single group, outside the timed region, and the per-kernel numbers come from that
     # run (tools/profile_round.sh profiles the single-group configuration, so rocprof's averages
     # match these).
     # (per-kernel events only here: each event record between two kernels costs device time, so the
     # timed steps above run without them — icp4r_set_kernel_timing)
-    groups_env = os.environ.get("ICP4R_GROUPS")
-    os.environ["ICP4R_GROUPS"] = "1"
+    groups_prev, _ = ctx.get_plan_option("groups")
+    ctx.set_plan_option("groups", 1)
     try:
         ctx.set_kernel_timing(True)
         ctx.reset_timers()
         for _ in range(min(args.steps, 5)):
             ctx.align_batch_device(batch, params, results.data_ptr(), stream)
         torch.cuda.synchronize(dev)
+        group1_batch_ms, _ = ctx.batch_time_ms()
     finally:
         ctx.set_kernel_timing(False)
-        if groups_env is None:
-            del os.environ["ICP4R_GROUPS"]
-        else:
-            os.environ["ICP4R_GROUPS"] = groups_env
+        ctx.set_plan_option("groups", groups_prev)
     single_group_equal = bool((results.cpu().numpy() == (timed[rank * P:(rank + 1) * P] if world > 1 else timed)).all())
     nn_ms, nn_launches = ctx.kernel_time_ms()  # the dominant kernel: the batched search
     test_ms, test_launches = ctx.stage_time_ms(icp4r.STAGE_NN_TEST)
     upd_ms, upd_launches = ctx.stage_time_ms(icp4r.STAGE_UPDATE)
     st = ctx.nn_stats()  # work the NN kernels performed in the single-group steps
     evals, tests = st["evaluations"], st["box_tests"]
-    plan = icp4r.plan(P, n, n)
+    plan = icp4r.plan(P, n, n, ctx=ctx)
     kernel = "nn_lds_kernel" if plan["lds"] else "nn_pruned_kernel" if plan["pruned"] else "nn_kernel"
 
     # the single-pair configs C1, C2, C5 (rank 0 at N=1: one GPU each; their CPU baselines too)
@@ -742,9 +757,6 @@ def run_gpu(args) -> int:
     flops_per_launch = evals_per_launch * FLOP_PER_PAIR_EVAL + tests_per_launch * FLOP_PER_BOX_TEST
     achieved_tflops = flops_per_launch / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     brute_equiv_tflops = P * n * n * FLOP_PER_PAIR_EVAL / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    # HBM bytes per launch from the committed PMC passes of THIS kernel, shape and library build
-    traffic, traffic_note = (pmc_traffic("C3", kernel, sha) if (P, n, args.iters) == (1024, 8192, 20)
-                             else (None, "profiles cover the default C3 shape only"))
 
     # cached-neighbour test kernel (HBM-bound; by default only the fitness pass's test runs here, the
     # iteration passes' tests are fused into fold_update_kernel's tail): per tested query X (16, .w =
@@ -761,18 +773,52 @@ def run_gpu(args) -> int:
                       "frac": tb / (test_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                       "hit_rate": st["cache_hits"] / max(st["cache_tested"], 1),
                       "tests_fused_into_update": st["tested_in_update"]}
-    # fold_update_kernel (HBM), one-read algorithmic bytes (never count re-reads): X and
-    # nn_t read once per point (32 B) for the two fold passes; fused, the next pass's test adds U
-    # (4 B) read and X (16) + U (4) written per tested point.  The kernel actually reads X and nn_t
-    # twice more (pass B, the test tail): `bytes_with_rereads` prices those too.
-    update = {"kernel": "fold_update_kernel", "avg_launch_ms": upd_ms, "launches": upd_launches,
-              "cache_hit_rate": st["cache_hits"] / max(st["cache_tested"], 1)}
+    # The two kernels that share the C3 step, each priced against HBM on SURVEY §8(d)'s algorithmic
+    # bytes: every cloud read once per ICP pass, 16 B per point — 16 * (N + M) * pairs per launch (each
+    # launch is one pass over the batch) — with the PMC counter bytes of the same kernel, shape and
+    # library build beside them (`traffic`; profiles/pmc_traffic.json).  `roofline` is the one with
+    # the larger share of the single-group step's device time (the top row of
+    # profiles/<round>/kernel_stats_C3.csv); the other sits beside it.
+    alg_bytes = 16 * (n + n) * P
+    default_shape = (P, n, args.iters) == (1024, 8192, 20)
+
+    def hbm_roof(kname: str, avg_ms: float, launches: int) -> dict:
+        tr, tr_note = (pmc_traffic("C3", kname, sha) if default_shape
+                       else (None, "profiles cover the default C3 shape only"))
+        ach = alg_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        return {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": ach / PEAK_HBM_GBS, "algorithmic_bytes_per_launch": alg_bytes,
+                "traffic": tr, "traffic_source": tr_note,
+                "traffic_gbs": tr / (avg_ms * 1e-3) / 1e9 if tr and avg_ms > 0 else None,
+                "traffic_over_algorithmic": tr / alg_bytes if tr else None,
+                "library_sha256": sha, "avg_launch_ms": avg_ms, "launches": launches,
+                "share_of_device_time": avg_ms * launches / max(min(args.steps, 5), 1) / group1_batch_ms
+                if group1_batch_ms > 0 else None}
+
+    # fold_update_kernel: PCL's sequential float folds (pass A centroids, pass B sigma panels), the solve,
+    # and the next pass's cached-neighbour test fused into its tail.  Per tested point it reads X (16 B,
+    # .w = L), nn_t (16) and U (4) and writes X and U: `one_read_bytes` counts X and nn_t once plus the
+    # test's U / writes; the counters show the passes' re-reads.
+    update = hbm_roof("fold_update_kernel", upd_ms, upd_launches)
+    update["cache_hit_rate"] = st["cache_hits"] / max(st["cache_tested"], 1)
     if upd_launches and upd_ms > 0:
         ub = (P * n * 32 * upd_launches + st["tested_in_update"] * 24) / upd_launches
-        ub_re = (P * n * 64 * upd_launches + st["tested_in_update"] * 56) / upd_launches
-        update.update({"bound": "hbm", "bytes_per_launch": ub, "achieved": ub / (upd_ms * 1e-3) / 1e9,
-                       "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                       "bytes_with_rereads": ub_re, "frac_with_rereads": ub_re / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS})
+        update["one_read_bytes"] = {"bytes_per_launch": ub, "achieved": ub / (upd_ms * 1e-3) / 1e9,
+                                    "frac": ub / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+    # the batched search: HBM on the same §8(d) bytes, and its FP32 VALU work counted on the device
+    search = hbm_roof(kernel, nn_ms, nn_launches)
+    search["valu"] = {
+        "achieved": achieved_tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": achieved_tflops / PEAK_FP32_TFLOPS, "flop_per_launch": flops_per_launch,
+        "evaluations_per_launch": evals_per_launch, "box_tests_per_launch": tests_per_launch,
+        "evaluated_fraction_of_brute_force": evals_per_launch / (P * n * n),
+        "brute_force_equivalent_tflops": brute_equiv_tflops,
+        "note": "distance evaluations x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP of the "
+                "exact pruned search (queries the cached-neighbour test could not resolve), counted on the "
+                "device; compare/select/ballot/LDS not counted. brute_force_equivalent_tflops = n*m*8 per "
+                "pass / search time: exact pruning, so SURVEY 8(d)'s FLOP roofline does not bound it"}
+    update_first = (update["share_of_device_time"] or 0) >= (search["share_of_device_time"] or 0)
+    roofline, beside = (update, search) if update_first else (search, update)
 
     if rank == 0:
         cpu = None
@@ -800,40 +846,13 @@ def run_gpu(args) -> int:
                 "parallelism": f"pairs sharded over {world} rank(s), RCCL all-gather of results" if world > 1
                 else "1 GPU",
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": achieved_tflops,
-                "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-                "traffic": traffic,
-                "traffic_source": traffic_note,
-                "traffic_gbs": traffic / (nn_ms * 1e-3) / 1e9 if traffic and nn_ms > 0 else None,
-                "library_sha256": sha,
-                "kernel": kernel,
-                "flop_per_launch": flops_per_launch,
-                "evaluations_per_launch": evals_per_launch,
-                "box_tests_per_launch": tests_per_launch,
-                "evaluated_fraction_of_brute_force": evals_per_launch / (P * n * n),
-                "brute_force_equivalent_tflops": brute_equiv_tflops,
-                "avg_launch_ms": nn_ms,
-                "launches": nn_launches,
-                "note": "FP32 VALU work of the exact pruned search kernel (nn_lds_kernel: the queries the "
-                        "cached-neighbour test could not resolve), counted on the device: distance evaluations "
-                        "x 8 FLOP (3 sub, 3 mul, 2 add) + point-to-box tests x 11 FLOP (6 sub, 3 mul, 2 add) "
-                        "- since round 2 session 4 only the block tests of queries that reach the superblock, "
-                        "which is all the kernel performs (the ~100M per launch it had spent on lanes that "
-                        "could not reach it were counted before, so the fraction fell as the kernel got faster); "
-                        "compare/select/ballot/LDS not counted. achieved = that / avg launch time (HIP events on "
-                        "the launch stream); peak = dense FP32 (== f32 MFMA dense peak). brute_force_equivalent_"
-                        "tflops = n*m*8 per NN pass / search time. See DESIGN.md §5",
-            },
+            "roofline": roofline,
+            ("nn_kernel" if update_first else "update_kernel"): beside,
             "incl_upload": upload,
             "gather": {"ms": gather_ms, "bytes": world * P * 96,
                        "via": "icp4r_gather_results (library RCCL communicator, ncclAllGather)" if comm is not None
                        else "torch.distributed all_gather_into_tensor (RCCL)"} if world > 1 else None,
             "cache_test_kernel": cache_test,
-            "update_kernel": update,
             **configs,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -29,13 +29,27 @@ struct Plan {
     int64_t blocks;
 };
 
-int env_int(const char* name, int dflt);
+// Plan options (icp4r_set_plan_option): the A/B and diagnostic switches of the
+// pipeline, set per context through the C ABI.  None changes a result (the parity tests assert
+// bit-identical registrations across them); an option never set takes the call site's default, the
+// measured best.  The library reads no environment variable.
+enum PlanOpt : int {
+    kOptNnQ, kOptLeaf, kOptChunkSb, kOptNnLds, kOptNnCache, kOptNnTile, kOptTileRun, kOptSolo, kOptXpad,
+    kOptPhaseTicks, kOptKd, kOptMortonMwg, kOptPart, kOptSrcOrder, kOptFuseSeed, kOptTileOwn, kOptTileDefer,
+    kOptGroups, kOptSearchCuDiv, kOptFuseTest, kOptFuseOrder, kOptSumsTail, kOptWideUpdate, kOptGatherPadded,
+    kOptGicpCovBrute, kNumPlanOpts
+};
+static_assert(kNumPlanOpts <= 32, "icp4r_ctx::plan_set is a 32-bit mask");
+extern const char* const kPlanOptNames[kNumPlanOpts];
+// The context's value of option k, or dflt when it was never set (ctx may be NULL: dflt).
+int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt);
+
 // Geometry of the NN pass for a batch shape.  allow_lds = false keeps the batched LDS search out (a
 // caller whose index strides exceed what it stages, icp4r_gicp.cpp), so every other field of the
 // plan is the one of the plan that runs.
 // registration = true: the plan of run_pairs for PCL numerics (solo_kernel where it applies).
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO, bool allow_lds = true,
-               bool registration = false);
+Plan make_plan(const icp4r_ctx* ctx, int npairs, int max_n, int max_m, int nn_mode = ICP4R_NN_AUTO,
+               bool allow_lds = true, bool registration = false);
 // icp4r_params -> the kernels' KParams (validates).
 int make_kparams(const icp4r_params* p, icp4r::KParams* kp);
 // Size the context's workspace for a plan and fill WorkArgs.

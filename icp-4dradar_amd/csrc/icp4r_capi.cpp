@@ -4,6 +4,7 @@
 // a context owns one device's stream and grow-only device buffers; every entry validates its
 // arguments, launches, and reports a status plus a thread-local message (icp4r_last_error).  There
 // is no CPU fallback: if the device path cannot run, the call fails with ICP4R_E_HIP.
+#include <dlfcn.h>
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -57,6 +58,21 @@ void pack_host(const float* c, int64_t n, int32_t stride_bytes, std::vector<floa
     }
 }
 
+const RoctxApi& roctx() {
+    static const RoctxApi api = [] {
+        RoctxApi a;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            a.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+            a.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+            if (!a.push || !a.pop) a.push = nullptr, a.pop = nullptr;
+        }
+        return a;
+    }();
+    return api;
+}
+
 }  // namespace icp4r_host
 
 using icp4r_host::DevBuf;
@@ -84,9 +100,14 @@ int read_counters(icp4r_ctx* ctx, uint64_t (&out)[kNumCounters]) {
     return ICP4R_OK;
 }
 
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
+const char* const kPlanOptNames[kNumPlanOpts] = {
+    "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad",
+    "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
+    "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
+    "gicp_cov_brute"};
+
+int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
+    return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
 }
 
 // Geometry of the NN pass.
@@ -97,7 +118,8 @@ int env_int(const char* name, int dflt) {
 //    then split the target range until there are >= 2048 workgroups (8 per CU) while each split
 //    keeps >= 256 targets.  Q = 4 scalar measured fastest (tools/experiments/tune_sweep.py, profiles/tune_r01.jsonl).
 // Tuning overrides (tools/experiments/tune_sweep.py): ICP4R_NN_Q caps Q, ICP4R_LEAF = 16 | 32.
-Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bool registration) {
+Plan make_plan(const icp4r_ctx* ctx, int npairs, int max_n, int max_m, int nn_mode, bool allow_lds,
+               bool registration) {
     Plan pl;
     pl.pruned = nn_mode == ICP4R_NN_PRUNED || (nn_mode == ICP4R_NN_AUTO && max_m >= kPrunedMinM);
     pl.packed = false;
@@ -111,13 +133,13 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
     pl.tile_run = 64;
     pl.solo = false;
     pl.max_m = max_m;
-    const int qcap = env_int("ICP4R_NN_Q", pl.pruned ? kDefaultPrunedQ : kDefaultQ);
+    const int qcap = opt(ctx, kOptNnQ, pl.pruned ? kDefaultPrunedQ : kDefaultQ);
     pl.q = (qcap == 1 || qcap == 2 || qcap == 4 || qcap == 8 || qcap == 16) ? qcap
                                                                              : (pl.pruned ? kDefaultPrunedQ : kDefaultQ);
     auto qblocks = [&](int q) { return (int64_t)((max_n + kNNWG * q - 1) / (kNNWG * q)); };
     if (pl.pruned) {
         if (pl.q > 4) pl.q = 4;
-        const int leaf = env_int("ICP4R_LEAF", kDefaultLeaf);
+        const int leaf = opt(ctx, kOptLeaf, kDefaultLeaf);
         pl.leaf = (leaf == 16 || leaf == 32) ? leaf : kDefaultLeaf;
         while (pl.q > 1 && (int64_t)npairs * qblocks(pl.q) * (kNNWG / 64) < 8192) pl.q /= 2;
         pl.blocks = (int64_t)npairs * qblocks(pl.q);
@@ -128,7 +150,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
         const int64_t waves = pl.blocks * (kNNWG / 64);
         int cs = 64;
         while (cs > 16 && waves * ((nsb + cs - 1) / cs) < 1024) cs /= 2;
-        const int cs_env = env_int("ICP4R_CHUNK_SB", 0);
+        const int cs_env = opt(ctx, kOptChunkSb, 0);
         if (cs_env == 16 || cs_env == 32 || cs_env == 64) cs = cs_env;
         pl.chunk_sb = cs;
         pl.chunks = nsb > 0 ? (nsb + cs - 1) / cs : 1;
@@ -136,24 +158,24 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
         // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides).  Its
         // query records pack the source index and sorted position in 14 bits each (kLdsMaxSources),
         // so larger sources take the tiled search instead.
-        const int lds = env_int("ICP4R_NN_LDS", -1);
+        const int lds = opt(ctx, kOptNnLds, -1);
         const bool fits = allow_lds && pl.leaf == 16 && max_m <= kLdsMaxTargets && max_n <= kLdsMaxSources;
         pl.lds = fits && (lds == 1 || (lds < 0 && npairs >= kLdsMinPairs));
         if (pl.lds) {
             pl.q = 2;
             pl.blocks = npairs;
             pl.chunks = 1;
-            pl.cache = env_int("ICP4R_NN_CACHE", 1) != 0;
+            pl.cache = opt(ctx, kOptNnCache, 1) != 0;
         } else {
             // single pairs / small batches: the LDS-tiled search (target tiles of 8192 x query parts)
-            pl.tile = pl.leaf == 16 && max_m < (1 << 19) && env_int("ICP4R_NN_TILE", 1) != 0;
+            pl.tile = pl.leaf == 16 && max_m < (1 << 19) && opt(ctx, kOptNnTile, 1) != 0;
             if (pl.tile) {
                 pl.chunks = (max_m + 8191) / 8192;
                 // queries per wave run: shorter runs (more workgroups, each staging its tile) until the
                 // grid covers the CUs — a single pair's search is latency-bound per run (C2 1.85 ->
                 // 1.75 ms, C5 2.35 -> 2.20 ms at 16; C1 0.457 -> 0.449 ms at 8; ICP4R_TILE_RUN=64 / 32 /
                 // 16 / 8 forces one)
-                const int tr = env_int("ICP4R_TILE_RUN", 0);
+                const int tr = opt(ctx, kOptTileRun, 0);
                 auto parts = [&](int run) { return (int64_t)npairs * ((max_n + 16 * run - 1) / (16 * run)) * pl.chunks; };
                 pl.tile_run = 64;
                 if (tr == 64 || tr == 32 || tr == 16 || tr == 8)
@@ -170,7 +192,7 @@ Plan make_plan(int npairs, int max_n, int max_m, int nn_mode, bool allow_lds, bo
             // solo stays ahead on long fixed runs up to 3k sources, 0.78 vs 0.81 ms at 20 — see
             // tools/experiments/solo_sweep.py, profiles/round3/s4/solo_sweep_r16.jsonl; ICP4R_SOLO=1 forces it up to
             // kCacheMaxN, 0 disables it)
-            const int solo_env = env_int("ICP4R_SOLO", -1);
+            const int solo_env = opt(ctx, kOptSolo, -1);
             pl.solo = registration && pl.tile && pl.chunks == 1 && solo_env != 0 &&
                       max_n <= (solo_env == 1 ? kCacheMaxN : kSoloMaxN);
             if (pl.solo) pl.blocks = npairs;
@@ -242,12 +264,13 @@ int next_event(std::vector<EventPair>& v, size_t& used, EventPair** out) {
 // Size the workspace for a plan and fill WorkArgs.
 int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m, bool corr, hipStream_t st,
                WorkArgs& w) {
-    const int64_t x_stride = (((max_n > 0 ? max_n : 1) + 3) & ~3) + env_int("ICP4R_XPAD", 0);
+    const int64_t x_stride = (((max_n > 0 ? max_n : 1) + 3) & ~3) + opt(ctx, kOptXpad, 0);
     const int64_t slots = (int64_t)npairs * x_stride;
     HIP_TRY(ctx->X.ensure((size_t)slots * sizeof(float4)));
     HIP_TRY(ctx->nn_key.ensure((size_t)slots * sizeof(NNKey)));
     HIP_TRY(ctx->state.ensure((size_t)npairs * sizeof(PairState)));
     memset(&w, 0, sizeof(w));
+    w.tile_own = opt(ctx, kOptTileOwn, 1) != 0 ? 1 : 0;
     w.X = static_cast<float4*>(ctx->X.p);
     w.nn_key = static_cast<NNKey*>(ctx->nn_key.p);
     w.state = static_cast<PairState*>(ctx->state.p);
@@ -258,7 +281,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, kCountBytes, st));
     }
     w.evals = static_cast<unsigned long long*>(ctx->evals.p);
-    if (env_int("ICP4R_PHASE_TICKS", 0)) {
+    if (opt(ctx, kOptPhaseTicks, 0)) {
         // (see the kernels' debug tick slots; then kPassTickSlots per NN pass)
         const size_t nt = (size_t)pass_tick_base(npairs) + (size_t)kMaxTickPasses * kPassTickSlots;
         if (ctx->ticks.cap < nt * sizeof(uint64_t)) {
@@ -274,7 +297,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
     if (pl.pruned) {
         const int64_t span = (int64_t)pl.leaf * kSuper;
         w.leaf = pl.leaf;
-        w.kd_index = env_int("ICP4R_KD", 3);  // bit 0: targets, bit 1: sources (0: Morton for both)
+        w.kd_index = opt(ctx, kOptKd, 3);  // bit 0: targets, bit 1: sources (0: Morton for both)
         w.t_stride = ((max_m > 0 ? max_m : 1) + span - 1) / span * span;
         w.b_stride = w.t_stride / pl.leaf;
         w.sb_stride = w.b_stride / kSuper;
@@ -297,7 +320,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         constexpr int kChunk = 8192;
         const int64_t mog = (w.t_stride + kChunk - 1) / kChunk;
         if ((w.kd_index & 1) && w.t_stride > kChunk && (pl.leaf == 16 || pl.leaf == 32) &&
-            npairs * mog <= 2048 && env_int("ICP4R_MORTON_MWG", 1)) {
+            npairs * mog <= 2048 && opt(ctx, kOptMortonMwg, 1)) {
             HIP_TRY(ctx->mo_hist.ensure((size_t)npairs * mog * (1u << 14) * sizeof(uint16_t)));
             w.mo_hist = static_cast<uint16_t*>(ctx->mo_hist.p);
             w.mo_groups = (int32_t)mog;
@@ -357,7 +380,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
 
             w.need = static_cast<uint32_t*>(ctx->need.p);
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
-            w.part_size = env_int("ICP4R_PART", kDefaultPartSize);
+            w.part_size = opt(ctx, kOptPart, kDefaultPartSize);
             if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
             // (a fresh registration starts from zero: init_kernel clears the pair's bitmap and count —
             // three memset launches per batch, and their boundaries, fewer)
@@ -472,22 +495,22 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     if (npairs <= 0) return ICP4R_OK;
     const int mn = max_n > 0 ? max_n : 1;
     const bool pcl = a.kp.numerics == kNumericsPCL;
-    const Plan pl = make_plan(npairs, mn, max_m, nn_mode, true, pcl);
+    const Plan pl = make_plan(ctx, npairs, mn, max_m, nn_mode, true, pcl);
     WorkArgs w;
     int rc;
     if ((rc = setup_work(ctx, pl, npairs, max_n, max_m, pcl && !pl.solo, st, w))) return rc;
     // sources ordered by their target's kd tree (src_order_kernel) on the batched plan, where its
     // better first-pass seeds and one kd build per pair pay (C3 +2.9 %); a single pair's extra launch
     // does not (C1 0.75 -> 0.80 ms), so the unbatched plans build the source's own tree
-    w.src_by_tgt = (pl.pruned && pl.lds) ? (env_int("ICP4R_SRC_ORDER", 1) != 0 ? 1 : 0)
-                                         : (pl.pruned && env_int("ICP4R_SRC_ORDER", 0) != 0 ? 1 : 0);
+    w.src_by_tgt = (pl.pruned && pl.lds) ? (opt(ctx, kOptSrcOrder, 1) != 0 ? 1 : 0)
+                                         : (pl.pruned && opt(ctx, kOptSrcOrder, 0) != 0 ? 1 : 0);
     w.stage_first = (w.src_by_tgt && (pl.lds || pl.solo) && w.qv && w.qm) ? 1 : 0;
     // multi-tile plan (the scan-to-map target), PCL numerics: seeds written by the update's transform
-    w.seed_next = (pl.tile && pl.chunks > 1 && pcl && w.corr && env_int("ICP4R_FUSE_SEED", 1) != 0) ? 1 : 0;
+    w.seed_next = (pl.tile && pl.chunks > 1 && pcl && w.corr && opt(ctx, kOptFuseSeed, 1) != 0) ? 1 : 0;
     // one-tile plan (C1, C2), PCL numerics: the update's transformCloud(T_inc) deferred into the next
     // search, which reads every query anyway (nn_tile_kernel; ICP4R_TILE_DEFER=0: the update does it)
-    if (pl.tile && pl.chunks == 1 && !pl.solo && pcl && w.corr && env_int("ICP4R_TILE_OWN", 1) != 0 &&
-        env_int("ICP4R_TILE_DEFER", 1) != 0)
+    if (pl.tile && pl.chunks == 1 && !pl.solo && pcl && w.corr && opt(ctx, kOptTileOwn, 1) != 0 &&
+        opt(ctx, kOptTileDefer, 1) != 0)
         w.defer_xform = 1;
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
@@ -507,7 +530,10 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
         HIP_TRY(hipEventRecord(be->stop, st));
         return ICP4R_OK;
     }
-    int groups = pl.lds ? env_int("ICP4R_GROUPS", kDefaultGroups) : 1;
+    // (at most kMaxGroups: a process has GPU_MAX_HW_QUEUES = 4 hardware queues, and a fourth group
+    // shares one with the third, whose kernels then serialise — DESIGN.md §5; icp4r_set_plan_option
+    // refuses more)
+    int groups = pl.lds ? opt(ctx, kOptGroups, kDefaultGroups) : 1;
     if (groups < 1) groups = 1;
     if (groups > kMaxGroups) groups = kMaxGroups;
     while (groups > 1 && npairs / groups < kLdsMinPairs / 2) --groups;
@@ -530,7 +556,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // persistent search grid per group: CUs / groups (ICP4R_SEARCH_CU_DIV overrides), so the other
     // groups' kernels find CUs without a 150-KB search workgroup on them (C3: 2 groups on 128 CUs
     // each 91.5k pairs/s, on 256 CUs each 89.5k, one group 88.4k — measured in one session)
-    const int cdiv = env_int("ICP4R_SEARCH_CU_DIV", groups);
+    const int cdiv = opt(ctx, kOptSearchCuDiv, groups);
     const int search_cu = cdiv > 1 ? (ctx->ncu + cdiv - 1) / cdiv : 0;
     for (int g = 0; g < groups; ++g) {
         HIP_TRY(launch_init(ag[g], wg[g], gn[g], gs[g]));
@@ -540,23 +566,23 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     const int iters = max_iterations > 0 ? max_iterations : 1;
     // the cached-neighbour test of iteration passes 2.. runs in the tail of the previous update
     // (fold_update_kernel, PCL numerics; ICP4R_FUSE_TEST=0: its own kernel)
-    const bool fuse = pl.lds && pl.cache && pcl && env_int("ICP4R_FUSE_TEST", 1) != 0;
+    const bool fuse = pl.lds && pl.cache && pcl && opt(ctx, kOptFuseTest, 1) != 0;
     // ... and the work list of those passes is built by the update's last workgroup (ICP4R_FUSE_ORDER=0:
     // nn_order_kernel)
-    const bool ford = fuse && env_int("ICP4R_FUSE_ORDER", 1) != 0;
+    const bool ford = fuse && opt(ctx, kOptFuseOrder, 1) != 0;
     // ... and folds the next pass A's source centroid sums over the X it writes, so that pass A reads
     // nn_t only (every correspondence kept, unweighted, no MSE criterion).  Off unless ICP4R_SUMS_TAIL=1:
     // the three n-long chains are serial, and in pass A they run beside the other chains for free, while
     // in the tail they lengthen the pair's critical path (C3: update 177 -> 190 us)
     for (int g = 0; g < groups; ++g)
         wg[g].sums_tail = (fuse && a.kp.huber_delta == INFINITY && a.kp.max_d2 >= FLT_MAX && !a.kp.need_mse &&
-                           env_int("ICP4R_SUMS_TAIL", 0) != 0)
+                           opt(ctx, kOptSumsTail, 0) != 0)
                               ? 1
                               : 0;
     const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
     // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
     // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)
-    const bool wide = pcl && !fuse && npairs <= ctx->ncu && env_int("ICP4R_WIDE_UPDATE", 1) != 0;
+    const bool wide = pcl && !fuse && npairs <= ctx->ncu && opt(ctx, kOptWideUpdate, 1) != 0;
     char pass_name[48];
     for (int it = 0; it < iters; ++it) {
         snprintf(pass_name, sizeof(pass_name), "icp4r ICP pass %d", it + 1);
@@ -630,7 +656,7 @@ int nearest_keys(icp4r_ctx* ctx, const float* query, int32_t n, int32_t qstride,
     a.results = static_cast<Result*>(ctx->results.p);
     int rc;
     if ((rc = make_kparams(nullptr, &a.kp))) return rc;
-    const Plan pl = make_plan(1, n, m, ICP4R_NN_AUTO);
+    const Plan pl = make_plan(ctx, 1, n, m, ICP4R_NN_AUTO);
     WorkArgs w;
     if ((rc = setup_work(ctx, pl, 1, n, m, false, st, w))) return rc;
     HIP_TRY(launch_init(a, w, 1, st));
@@ -694,6 +720,12 @@ int icp4r_device_count(int* count) {
 int icp4r_create(icp4r_ctx** out, int device) {
     if (!out) return fail(ICP4R_E_INVALID, "out is NULL");
     *out = nullptr;
+    if (device == ICP4R_NO_DEVICE) {  // plan queries and plan options only: no HIP call, no stream
+        icp4r_ctx* c = new icp4r_ctx();
+        c->device = ICP4R_NO_DEVICE;
+        *out = c;
+        return ICP4R_OK;
+    }
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(ICP4R_E_INVALID, "device %d out of range (%d devices)", device, n);
@@ -702,7 +734,6 @@ int icp4r_create(icp4r_ctx** out, int device) {
     c->device = device;
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
-    c->kernel_timing = env_int("ICP4R_KERNEL_EVENTS", 0) != 0;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -714,6 +745,11 @@ int icp4r_create(icp4r_ctx** out, int device) {
 
 int icp4r_destroy(icp4r_ctx* ctx) {
     if (!ctx) return ICP4R_OK;
+    for (icp4r_comm* c : ctx->comms) icp4r_host::comm_detach(c);
+    if (ctx->device == ICP4R_NO_DEVICE) {
+        delete ctx;
+        return ICP4R_OK;
+    }
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (int g = 0; g < kMaxGroups; ++g) {
@@ -1016,15 +1052,71 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx) {
     return ICP4R_OK;
 }
 
-int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out) {
+// Plan options: per-context values of icp4r_pipe::PlanOpt.  Ranges are checked where a
+// value would pick a wrong plan rather than fall back to a default.
+namespace {
+int plan_opt_index(const char* name) {
+    if (!name) return -1;
+    for (int k = 0; k < kNumPlanOpts; ++k)
+        if (strcmp(name, kPlanOptNames[k]) == 0) return k;
+    return -1;
+}
+}  // namespace
+
+int icp4r_set_plan_option(icp4r_ctx* ctx, const char* name, int32_t value) {
+    if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
+    const int k = plan_opt_index(name);
+    if (k < 0) return fail(ICP4R_E_INVALID, "unknown plan option '%s'", name ? name : "(null)");
+    if (k == kOptGroups && (value < 1 || value > kMaxGroups))
+        return fail(ICP4R_E_INVALID,
+                    "plan option groups = %d: 1..%d (a fourth pair group shares a hardware queue with the third, "
+                    "and its kernels serialise)",
+                    value, kMaxGroups);
+    if (k == kOptXpad && (value < 0 || value > 1 << 20)) return fail(ICP4R_E_INVALID, "plan option xpad = %d", value);
+    if (k == kOptSearchCuDiv && value < 0) return fail(ICP4R_E_INVALID, "plan option search_cu_div = %d", value);
+    ctx->plan_val[k] = value;
+    ctx->plan_set |= 1u << k;
+    return ICP4R_OK;
+}
+
+int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value, int32_t* is_set) {
+    if (!ctx || !value) return fail(ICP4R_E_INVALID, "NULL argument");
+    const int k = plan_opt_index(name);
+    if (k < 0) return fail(ICP4R_E_INVALID, "unknown plan option '%s'", name ? name : "(null)");
+    const bool set = (ctx->plan_set >> k) & 1u;
+    *value = set ? ctx->plan_val[k] : INT32_MIN;
+    if (!set) {  // the default in effect (what the plan code falls back to)
+        static const int32_t dflt[kNumPlanOpts] = {
+            0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
+            -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
+            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0};
+        *value = dflt[k];
+    }
+    if (is_set) *is_set = set ? 1 : 0;
+    return ICP4R_OK;
+}
+
+int icp4r_reset_plan_options(icp4r_ctx* ctx) {
+    if (!ctx) return fail(ICP4R_E_INVALID, "ctx is NULL");
+    ctx->plan_set = 0;
+    return ICP4R_OK;
+}
+
+int icp4r_plan(const icp4r_ctx* ctx, int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode,
+               int32_t numerics, icp4r_plan_info* out) {
     if (npairs <= 0 || max_src_n < 0 || max_tgt_n < 0 || !out) return fail(ICP4R_E_INVALID, "bad shape");
     if (nn_mode < ICP4R_NN_AUTO || nn_mode > ICP4R_NN_PRUNED) return fail(ICP4R_E_INVALID, "unknown nn_mode %d", nn_mode);
-    const Plan pl = make_plan(npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode, true, true);
+    if (numerics != ICP4R_NUMERICS_PCL && numerics != ICP4R_NUMERICS_F64)
+        return fail(ICP4R_E_INVALID, "unknown numerics mode %d", numerics);
+    const bool pcl = numerics == ICP4R_NUMERICS_PCL;
+    const Plan pl = make_plan(ctx, npairs, max_src_n > 0 ? max_src_n : 1, max_tgt_n, nn_mode, true, pcl);
     out->pruned = pl.pruned ? 1 : 0;
     out->solo = pl.solo ? 1 : 0;
-    // run_pairs' choice (PCL numerics, 256 CUs): no solo plan, no fused cache test, <= 1 pair per CU
-    const bool fuse = pl.lds && pl.cache && env_int("ICP4R_FUSE_TEST", 1) != 0;
-    out->wide_update = (!pl.solo && !fuse && npairs <= 256 && env_int("ICP4R_WIDE_UPDATE", 1) != 0) ? 1 : 0;
+    // run_pairs' choice: no solo plan, no fused cache test, at most one pair per CU of the context's
+    // device (256 without a context), PCL numerics
+    const int ncu = ctx ? ctx->ncu : 256;
+    const bool fuse = pl.lds && pl.cache && pcl && opt(ctx, kOptFuseTest, 1) != 0;
+    out->wide_update = (pcl && !pl.solo && !fuse && npairs <= ncu && opt(ctx, kOptWideUpdate, 1) != 0) ? 1 : 0;
     out->q = pl.q;
     out->splits = pl.splits;
     out->leaf = pl.leaf;

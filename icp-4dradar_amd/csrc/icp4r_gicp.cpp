@@ -51,8 +51,9 @@ int check_params(const icp4r_gicp_params* p) {
 // cloud (index_kernel with the cloud as its target; w's index buffers must fit max_n points) when
 // the plan prunes, brute force otherwise (ICP4R_GICP_COV_BRUTE=1 forces brute force).
 int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, const float4* cloud, const int64_t* off,
-             const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st) {
-    if (pl.pruned && !icp4r_pipe::env_int("ICP4R_GICP_COV_BRUTE", 0)) {
+             const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st,
+             bool brute) {
+    if (pl.pruned && !brute) {
         PairArgs ai = a;
         ai.tgt = cloud;
         ai.tgt_off = off;
@@ -80,7 +81,7 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     // pruned plans index the source too (its k-NN covariances): the index strides fit both clouds,
     // and the batched search, which stages t_stride targets, only runs when those fit its LDS
     const int idx_both = max_n > max_m ? max_n : max_m;
-    Plan pl = make_plan(npairs, mn, max_m, ICP4R_NN_AUTO, idx_both <= kLdsMaxTargets);
+    Plan pl = make_plan(ctx, npairs, mn, max_m, ICP4R_NN_AUTO, idx_both <= kLdsMaxTargets);
     pl.cache = false;  // gicp_iter_kernel moves X without maintaining the cached-neighbour bounds
     WorkArgs w;
     int rc;
@@ -118,15 +119,17 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     if (kev && (rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
     double* cs = static_cast<double*>(ctx->gicp_cov_src.p);
     double* ct = static_cast<double*>(ctx->gicp_cov_tgt.p);
+    // (plan option gicp_cov_brute: brute-force k-NN covariances, for A/B and the equality test)
+    const bool cov_brute = opt(ctx, kOptGicpCovBrute, 0) != 0;
     if (kev) HIP_TRY(hipEventRecord(ce->start, st));
     // source covariances first: the target's index (built last) stays for the NN passes
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
-                       st)))
+                       st, cov_brute)))
         return rc;
     if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
-                       st)))
+                       st, cov_brute)))
         return rc;
-    if (pl.pruned && icp4r_pipe::env_int("ICP4R_GICP_COV_BRUTE", 0)) HIP_TRY(launch_index(a, w, npairs, st));
+    if (pl.pruned && cov_brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
     for (int it = 0; it < gp.max_iterations; ++it) {
@@ -309,12 +312,12 @@ int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_
     a.src = a.tgt = static_cast<const float4*>(ctx->src.p);
     a.src_off = a.tgt_off = static_cast<const int64_t*>(ctx->src_off.p);
     a.src_n = a.tgt_n = static_cast<const int32_t*>(ctx->src_n.p);
-    const icp4r_pipe::Plan pl = icp4r_pipe::make_plan(1, n, n, ICP4R_NN_AUTO);
+    const icp4r_pipe::Plan pl = icp4r_pipe::make_plan(ctx, 1, n, n, ICP4R_NN_AUTO);
     WorkArgs w;
     if ((rc = icp4r_pipe::setup_work(ctx, pl, 1, n, n, false, st, w))) return rc;
     HIP_TRY(hipMemsetAsync(w.state, 0, sizeof(PairState), st));  // phase = active: index_kernel runs
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, 1, n, n, k, regularization,
-                       static_cast<double*>(ctx->gicp_cov_src.p), st)))
+                       static_cast<double*>(ctx->gicp_cov_src.p), st, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0) != 0)))
         return rc;
     std::vector<double> h6((size_t)n * 6);
     HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -3,7 +3,6 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
-#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdint.h>
 
 #include <vector>
@@ -47,12 +46,24 @@ struct DevBuf {
     }
 };
 
+// roctx, loaded at first use (dlopen of librocprofiler-sdk-roctx.so.1): the deployed library needs no
+// profiler SDK; without it the ranges are no-ops.
+struct RoctxApi {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+};
+const RoctxApi& roctx();
+
 // A roctx range over a host scope (SURVEY.md §5 "Tracing"): the entry points and every ICP pass show
 // up as named ranges in `rocprofv3 --marker-trace` beside the kernels they launched.  Without a
 // profiler attached a push / pop is a few tens of ns.
 struct Range {
-    explicit Range(const char* name) { roctxRangePushA(name); }
-    ~Range() { roctxRangePop(); }
+    explicit Range(const char* name) {
+        if (roctx().push) roctx().push(name);
+    }
+    ~Range() {
+        if (roctx().pop) roctx().pop();
+    }
     Range(const Range&) = delete;
     Range& operator=(const Range&) = delete;
 };
@@ -69,12 +80,18 @@ void pack_host(const float* c, int64_t n, int32_t stride_bytes, std::vector<floa
 
 }  // namespace icp4r_host
 
+struct icp4r_comm;
+namespace icp4r_host {
+// icp4r_destroy: the context is gone; the communicator keeps working on explicit streams only
+void comm_detach(icp4r_comm* c);
+}  // namespace icp4r_host
+
 struct icp4r_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // run_pairs' pair groups 1.. run on their own streams, joined back into the launch stream
-    hipStream_t aux_stream[4] = {};  // icp4r::kMaxGroups (static_assert in icp4r_capi.cpp)
-    hipEvent_t fork_ev[4] = {};
+    hipStream_t aux_stream[3] = {};  // icp4r::kMaxGroups (static_assert in icp4r_capi.cpp)
+    hipEvent_t fork_ev[3] = {};
     // staging for the host-buffer entry points
     icp4r_host::DevBuf src, tgt, src_off, src_n, tgt_off, tgt_n, guess, aligned, results, T;
     // batch workspace
@@ -82,6 +99,11 @@ struct icp4r_ctx {
         miss_cnt, plist, plist_n, owork, mo_hist, mo_rep;  // nn_lu holds U (float) per source point
     int ncu = 256;  // compute units of the device (persistent launches)
     bool kernel_timing = false;  // per-kernel events (icp4r_set_kernel_timing)
+    // plan options (icp4r_set_plan_option; icp4r_pipe::PlanOpt): values, and which are set
+    int32_t plan_val[32] = {};
+    uint32_t plan_set = 0;
+    // RCCL communicators created on this context (icp4r_multi.cpp): detached by icp4r_destroy
+    std::vector<icp4r_comm*> comms;
     // HIP events on the launch stream: the dominant NN kernel (the batched search, or the whole NN
     // launch of the other plans), the cache-test kernel, the update kernel, whole registrations
     std::vector<icp4r_host::EventPair> nn_events, test_events, upd_events, batch_events;

@@ -16,7 +16,7 @@ constexpr int kMaxQ = 16;         // register-resident queries per lane in nn_ke
 constexpr int kDefaultQ = 4;      // brute force: default cap (tools/tune_sweep.py)
 constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
-constexpr int kMaxGroups = 4;        // batched plans: pair groups on their own streams (run_pairs)
+constexpr int kMaxGroups = 3;        // batched plans: pair groups on their own streams (run_pairs)
 constexpr int kDefaultGroups = 2;
 constexpr int kDefaultPartSize = 1024;  // batched search: misses per work item of a heavy pair
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
@@ -150,6 +150,8 @@ struct WorkArgs {
     // an upper bound of the second-nearest distance.  Set by a search, widened by every kernel that
     // moves X_i.
     float* nn_u;        // [npairs * x_stride] U_i
+    int32_t tile_own;     // 1 (one-tile plan): nn_tile_kernel seeds, searches and writes the records itself
+                          // (plan option tile_own = 0: the three-launch form, for A/B)
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
     int32_t sums_tail;    // 1: the fused tail also folds the next pass A's Σs (eligible pairs: PairState)
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |

@@ -4464,16 +4464,6 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __shared__ FoldShared sh;
     __shared__ OrderShared osh;
     __shared__ int32_t last;
-#if ICP4R_FOLD_LDS_PAD
-    // experiment: fewer resident workgroups per CU (LDS-limited), so a pair's passes re-read its
-    // records from the Infinity Cache
-    __shared__ float lds_pad[ICP4R_FOLD_LDS_PAD];
-    if (order_ncu == -12345) {  // never true: keeps the array allocated
-        lds_pad[threadIdx.x] = (float)blockIdx.x;
-        __syncthreads();
-        w.ticks[threadIdx.x] = (uint64_t)lds_pad[ICP4R_FOLD_LDS_PAD - 1 - threadIdx.x];
-    }
-#endif
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     const int nwork = fold_update_pair(a, w, tail_test, p, sh);
     if (order_ncu <= 0) return;
@@ -5248,10 +5238,9 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
     hipError_t e;
     const int qpart = kLdsWaves * qrun;  // queries per workgroup
     const dim3 grid((max_m + kLdsTargets - 1) / kLdsTargets, (max_n + qpart - 1) / qpart, npairs);
-    // one tile: the search kernel seeds, stores and writes the records itself (ICP4R_TILE_OWN=0: the
+    // one tile: the search kernel seeds, stores and writes the records itself (w.tile_own = 0: the
     // three-launch form, for A/B)
-    static const int own_env = getenv("ICP4R_TILE_OWN") ? atoi(getenv("ICP4R_TILE_OWN")) : 1;
-    const bool own = grid.x == 1 && own_env != 0;
+    const bool own = grid.x == 1 && w.tile_own != 0;
     // (w.seed_next: the previous update / fitness_prep_kernel wrote the seeds, except for the first pass)
     if (!own && (first || !w.seed_next))
         hipLaunchKernelGGL(nn_seed_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w, fitness_pass,

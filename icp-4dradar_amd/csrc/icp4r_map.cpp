@@ -94,6 +94,7 @@ extern "C" {
 int icp4r_map_create(icp4r_ctx* ctx, icp4r_map** out) {
     if (!ctx || !out) return fail(ICP4R_E_INVALID, "ctx/out is NULL");
     *out = nullptr;
+    if (ctx->device < 0) return fail(ICP4R_E_INVALID, "icp4r_map_create: a context without a device");
     icp4r_map* m = new icp4r_map();
     m->ctx = ctx;
     *out = m;

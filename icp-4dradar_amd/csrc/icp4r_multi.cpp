@@ -14,13 +14,14 @@
 
 #include "icp4r/icp4r.h"
 #include "icp4r/icp4r_multi.h"
+#include "icp4r_batch.hpp"
 #include "icp4r_host.hpp"
 
 using icp4r_host::DevBuf;
 using icp4r_host::fail;
 
 struct icp4r_comm {
-    icp4r_ctx* ctx = nullptr;  // (not touched by icp4r_comm_destroy: the context may be gone by then)
+    icp4r_ctx* ctx = nullptr;  // NULL once icp4r_destroy(ctx) ran (icp4r_host::comm_detach)
     int device = 0;
     ncclComm_t nccl = nullptr;
     int32_t rank = 0, nranks = 1;
@@ -30,8 +31,9 @@ struct icp4r_comm {
     hipEvent_t done = nullptr;
     bool done_recorded = false;
     hipStream_t last = nullptr;
-    // Test switch (ICP4R_GATHER_PADDED=1 at creation): every gather takes the padded branch, so a
-    // one-rank communicator exercises the staging path that only unequal multi-rank shards reach.
+    // Test switch (the context's plan option gather_padded at creation): every gather takes the padded
+    // branch, so a one-rank communicator exercises the staging path that only unequal multi-rank
+    // shards reach.
     bool force_padded = false;
 };
 
@@ -41,6 +43,10 @@ struct icp4r_comm {
         if (_r != ncclSuccess)                                                                             \
             return fail(ICP4R_E_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(_r), __FILE__, __LINE__); \
     } while (0)
+
+namespace icp4r_host {
+void comm_detach(icp4r_comm* c) { c->ctx = nullptr; }
+}  // namespace icp4r_host
 
 namespace {
 
@@ -118,8 +124,9 @@ int icp4r_comm_create(icp4r_comm** out, icp4r_ctx* ctx, int32_t nranks, int32_t 
     c->device = ctx->device;
     c->rank = rank;
     c->nranks = nranks;
-    const char* fp = getenv("ICP4R_GATHER_PADDED");
-    c->force_padded = fp && atoi(fp) != 0;
+    // (plan option gather_padded, copied from the context at creation: the padded all-gather branch on
+    // any communicator, so one GPU can test it)
+    c->force_padded = icp4r_pipe::opt(ctx, icp4r_pipe::kOptGatherPadded, 0) != 0;
     if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(ICP4R_E_HIP, "icp4r_comm_create: hipEventCreate failed");
@@ -131,12 +138,21 @@ int icp4r_comm_create(icp4r_comm** out, icp4r_ctx* ctx, int32_t nranks, int32_t 
         return fail(ICP4R_E_RCCL, "ncclCommInitRank (rank %d of %d, device %d): %s", rank, nranks, ctx->device,
                     ncclGetErrorString(r));
     }
+    ctx->comms.push_back(c);
     *out = c;
     return ICP4R_OK;
 }
 
 int icp4r_comm_destroy(icp4r_comm* comm) {
     if (!comm) return ICP4R_OK;
+    if (comm->ctx) {
+        auto& v = comm->ctx->comms;
+        for (size_t k = 0; k < v.size(); ++k)
+            if (v[k] == comm) {
+                v.erase(v.begin() + (long)k);
+                break;
+            }
+    }
     (void)hipSetDevice(comm->device);
     // the last gather (and with it every earlier one on its stream) done before the staging is freed
     if (comm->done_recorded) (void)hipEventSynchronize(comm->done);
@@ -174,6 +190,8 @@ int icp4r_gather_results(icp4r_comm* comm, const icp4r_result* shard_rows, int32
     if (npairs == 0) return ICP4R_OK;
     icp4r_host::Range range("icp4r_gather_results");
     HIP_TRY(hipSetDevice(comm->device));
+    if (!hip_stream && !comm->ctx)
+        return fail(ICP4R_E_INVALID, "icp4r_gather_results: the communicator's context was destroyed; pass a stream");
     hipStream_t st = hip_stream ? static_cast<hipStream_t>(hip_stream) : comm->ctx->stream;
     constexpr size_t R = sizeof(icp4r_result);
     const int32_t maxc = (npairs + comm->nranks - 1) / comm->nranks;
@@ -205,6 +223,7 @@ int icp4r_align_batch_sharded(icp4r_comm* comm, const icp4r_batch* shard, int32_
                               const icp4r_params* params, icp4r_result* shard_results, icp4r_result* gathered,
                               void* hip_stream) {
     if (!comm || !shard) return fail(ICP4R_E_INVALID, "icp4r_align_batch_sharded: NULL argument");
+    if (!comm->ctx) return fail(ICP4R_E_INVALID, "icp4r_align_batch_sharded: the communicator's context was destroyed");
     int32_t first, count;
     if (npairs_total < 0) return fail(ICP4R_E_INVALID, "npairs_total < 0");
     shard_of(npairs_total, comm->nranks, comm->rank, &first, &count);

@@ -33,6 +33,7 @@ library_path = os.environ.get("ICP4R_LIBRARY") or os.path.join(HERE, "_lib", "li
 
 OK, E_INVALID, E_EMPTY, E_TOO_FEW_CORR, E_NONFINITE, E_HIP, E_RCCL, E_NOMEM, E_TOO_LARGE = 0, -1, -2, -3, -4, -5, -6, -7, -8
 NUMERICS_PCL, NUMERICS_F64 = 0, 1
+NO_DEVICE = -1  # icp4r_create(&ctx, ICP4R_NO_DEVICE): plan queries and plan options only
 NN_AUTO, NN_BRUTE, NN_BRUTE_PACKED, NN_PRUNED = 0, 1, 2, 3
 STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH, STAGE_GICP_COV = 0, 1, 2, 3, 4
 DBL_MAX = sys.float_info.max
@@ -47,8 +48,14 @@ EXPORTED_SYMBOLS = [
     "icp4r_create", "icp4r_destroy", "icp4r_align", "icp4r_align_batch_device", "icp4r_align_batch_host",
     "icp4r_fitness", "icp4r_nearest", "icp4r_synchronize", "icp4r_kernel_time_ms", "icp4r_batch_time_ms",
     "icp4r_kernel_time_reset", "icp4r_set_kernel_timing", "icp4r_plan", "icp4r_nn_counters", "icp4r_nn_cache_hits", "icp4r_stage_time_ms",
-    "icp4r_nn_stats",
+    "icp4r_nn_stats", "icp4r_set_plan_option", "icp4r_get_plan_option", "icp4r_reset_plan_options",
 ]
+# the plan options of icp4r_set_plan_option: A/B and diagnostic switches, never a result
+PLAN_OPTIONS = (
+    "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad", "phase_ticks", "kd",
+    "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer", "groups", "search_cu_div",
+    "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded", "gicp_cov_brute",
+)
 # include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
 EGO_EXPORTED_SYMBOLS = [
     "icp4r_ego_params_default", "icp4r_radar_features", "icp4r_ego_velocity", "icp4r_ego_velocity_batch_device",
@@ -169,7 +176,10 @@ def load():
         "icp4r_kernel_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_batch_time_ms": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(i32)]),
         "icp4r_kernel_time_reset": (C.c_int, [vp]),
-        "icp4r_plan": (C.c_int, [i32, i32, i32, i32, C.POINTER(PlanInfo)]),
+        "icp4r_plan": (C.c_int, [vp, i32, i32, i32, i32, i32, C.POINTER(PlanInfo)]),
+        "icp4r_set_plan_option": (C.c_int, [vp, C.c_char_p, i32]),
+        "icp4r_get_plan_option": (C.c_int, [vp, C.c_char_p, C.POINTER(i32), C.POINTER(i32)]),
+        "icp4r_reset_plan_options": (C.c_int, [vp]),
         "icp4r_nn_counters": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "icp4r_nn_cache_hits": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
         "icp4r_stage_time_ms": (C.c_int, [vp, i32, C.POINTER(C.c_double), C.POINTER(i32)]),
@@ -234,11 +244,15 @@ def _ptr(a: np.ndarray):
 class Context:
     """One HIP device's stream and buffers (icp4r_create / icp4r_destroy)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, plan: dict | None = None):
+        """device = NO_DEVICE: a context for plan queries and plan options only (no GPU needed).
+        plan: plan options to set (icp4r_set_plan_option)."""
         self._lib = load()
         self._h = C.c_void_p()
         _check(self._lib.icp4r_create(C.byref(self._h), device), "icp4r_create")
         self.device = device
+        if plan:
+            self.set_plan(**plan)
 
     def close(self):
         if self._h:
@@ -331,6 +345,24 @@ class Context:
         between kernels; batch_time_ms is always available)."""
         _check(self._lib.icp4r_set_kernel_timing(self._h, 1 if on else 0), "icp4r_set_kernel_timing")
 
+    # -- plan options (icp4r_set_plan_option; DESIGN.md §6) -------------------------------------
+    def set_plan_option(self, name: str, value: int):
+        """Set one plan option (A/B and diagnostics: never changes a result) for this context's calls."""
+        _check(self._lib.icp4r_set_plan_option(self._h, name.encode(), int(value)), f"plan option {name}")
+
+    def set_plan(self, **options):
+        for k, v in options.items():
+            self.set_plan_option(k, v)
+
+    def get_plan_option(self, name: str) -> tuple[int, bool]:
+        """(value in effect, whether it was set)."""
+        v, is_set = C.c_int32(), C.c_int32()
+        _check(self._lib.icp4r_get_plan_option(self._h, name.encode(), C.byref(v), C.byref(is_set)), f"plan option {name}")
+        return v.value, bool(is_set.value)
+
+    def reset_plan_options(self):
+        _check(self._lib.icp4r_reset_plan_options(self._h), "icp4r_reset_plan_options")
+
     def stage_time_ms(self, stage: int) -> tuple[float, int]:
         """(average ms, launches) of a stage (STAGE_NN, STAGE_NN_TEST, STAGE_UPDATE, STAGE_BATCH)."""
         ms, k = C.c_double(), C.c_int32()
@@ -365,9 +397,12 @@ class Context:
         return self.nn_counters()[0]
 
 
-def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO) -> dict:
+def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO, numerics: int = NUMERICS_PCL,
+         ctx: "Context | None" = None) -> dict:
+    """The launch plan of a batch shape (ctx: whose plan options and CU count; None: the defaults)."""
     info = PlanInfo()
-    _check(load().icp4r_plan(npairs, max_src_n, max_tgt_n, nn_mode, C.byref(info)), "icp4r_plan")
+    _check(load().icp4r_plan(ctx.handle if ctx is not None else None, npairs, max_src_n, max_tgt_n, nn_mode, numerics,
+                             C.byref(info)), "icp4r_plan")
     return {"pruned": bool(info.pruned), "lds": bool(info.lds), "cache": bool(info.cache), "q": info.q, "splits": info.splits,
             "leaf": info.leaf, "nn_blocks": info.nn_blocks, "solo": bool(info.solo),
             "wide_update": bool(info.wide_update)}
@@ -552,3 +587,16 @@ class Comm:
                                                    C.c_void_p(shard_results_ptr), C.c_void_p(gathered_ptr),
                                                    C.c_void_p(stream) if stream else None),
                "icp4r_align_batch_sharded")
+
+
+def env_plan(environ=None) -> dict:
+    """TOOLING ONLY (A/B scripts, tests): the plan options named by ICP4R_<NAME> environment variables,
+    e.g. ICP4R_GROUPS=1 -> {"groups": 1}.  Neither the library nor Context reads the environment; a
+    tool applies this dict explicitly (Context.set_plan(**env_plan()))."""
+    environ = os.environ if environ is None else environ
+    out = {}
+    for name in PLAN_OPTIONS:
+        v = environ.get("ICP4R_" + name.upper())
+        if v not in (None, ""):
+            out[name] = int(v)
+    return out

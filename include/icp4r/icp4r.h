@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ICP4R_ABI_VERSION 4
+#define ICP4R_ABI_VERSION 5
 
 typedef enum icp4r_status {
     ICP4R_OK = 0,
@@ -135,6 +135,10 @@ const char* icp4r_last_error(void);
 void icp4r_params_default(icp4r_params* p);
 int icp4r_device_count(int* count);
 
+/* A context on one HIP device (its stream, workspace and plan options).  device = ICP4R_NO_DEVICE
+ * makes a context without a device, for icp4r_plan queries and plan options only: no HIP call, and
+ * every device call on it fails. */
+#define ICP4R_NO_DEVICE (-1)
 int icp4r_create(icp4r_ctx** out, int device);
 int icp4r_destroy(icp4r_ctx* ctx);
 
@@ -181,8 +185,7 @@ int icp4r_kernel_time_reset(icp4r_ctx* ctx);
 /* Per-kernel timing (the events behind icp4r_kernel_time_ms / icp4r_stage_time_ms for NN, NN_TEST and
  * UPDATE): off by default — each event record between two kernels costs device time (an 8k pair's
  * registration 1.89 ms without them, 2.19 ms with them; a 1024-pair batch 7.01 vs 7.31 ms).  The
- * whole-call events (icp4r_batch_time_ms) are always recorded.  The environment variable
- * ICP4R_KERNEL_EVENTS=1 turns it on for contexts created afterwards. */
+ * whole-call events (icp4r_batch_time_ms) are always recorded. */
 int icp4r_set_kernel_timing(icp4r_ctx* ctx, int32_t enable);
 
 /* Average device time of one stage of the registrations since the last reset (HIP events on the
@@ -225,6 +228,19 @@ typedef struct icp4r_nn_stats_t {
 } icp4r_nn_stats_t;
 int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out);
 
+/* Plan options (A/B experiments and diagnostics): how a registration is laid out on the device —
+ * which search and update kernels run, grid shapes, pair groups on streams, debug stamps.  No option
+ * changes a result (the parity tests assert bit-identical registrations across them), and an option
+ * never set keeps its measured-best default (DESIGN.md §6 lists every name and default).  Options
+ * belong to a context and apply to its later calls; the library reads no environment variable.
+ * An unknown name, or a value outside the option's range (e.g. "groups" above 3: a fourth pair
+ * group would share a hardware queue with the third), is ICP4R_E_INVALID.
+ * icp4r_get_plan_option: the value in effect for the context's calls (the default when never set)
+ * and *is_set (may be NULL). */
+int icp4r_set_plan_option(icp4r_ctx* ctx, const char* name, int32_t value);
+int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value, int32_t* is_set);
+int icp4r_reset_plan_options(icp4r_ctx* ctx);
+
 /* Launch geometry the batch path picks for a shape — exposed for tests and the benchmark report. */
 typedef struct icp4r_plan_info {
     int32_t pruned;     /* 1: ICP4R_NN_PRUNED kernel, 0: brute force                 */
@@ -235,18 +251,21 @@ typedef struct icp4r_plan_info {
                            work lists); used for >= 256 pairs with <= 8192 targets    */
     int32_t cache;      /* lds: cached-neighbour test (a query keeps its previous NN
                            without a search when a second-nearest bound proves it;
-                           exact); off with ICP4R_NN_CACHE=0                          */
+                           exact); off with plan option nn_cache = 0                  */
     int64_t nn_blocks;  /* workgroups of one NN launch                               */
     int32_t solo;       /* 1: a PCL-numerics registration of this shape runs whole in one
                            workgroup per pair (solo_kernel): targets <= 8192, sources <=
-                           1024 by default (ICP4R_SOLO=1: up to 16384), and a plan that
-                           does not take the batched LDS search (fewer than 256 pairs,
-                           or ICP4R_NN_LDS=0); ICP4R_SOLO=0: never                    */
+                           1024 by default (plan option solo = 1: up to 16384), and a
+                           plan that does not take the batched LDS search (fewer than
+                           256 pairs, or nn_lds = 0); solo = 0: never                 */
     int32_t wide_update; /* 1: the PCL-numerics update runs one 1024-thread workgroup per pair
                            (fold_update_wide_kernel: at most one pair per CU, no fused cache
-                           test); off with ICP4R_WIDE_UPDATE=0                          */
+                           test, PCL numerics); off with plan option wide_update = 0    */
 } icp4r_plan_info;
-int icp4r_plan(int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode, icp4r_plan_info* out);
+/* ctx: whose plan options and CU count apply (NULL: the defaults and 256 CUs); numerics:
+ * ICP4R_NUMERICS_PCL / _F64, as icp4r_params.numerics. */
+int icp4r_plan(const icp4r_ctx* ctx, int32_t npairs, int32_t max_src_n, int32_t max_tgt_n, int32_t nn_mode,
+               int32_t numerics, icp4r_plan_info* out);
 
 #ifdef __cplusplus
 }

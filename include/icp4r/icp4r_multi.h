@@ -68,8 +68,10 @@ int icp4r_comm_check(icp4r_comm* comm);
  * Asynchronous on hip_stream (NULL: the context's stream); equal shards gather in place, unequal
  * ones through a padded staging buffer and one copy per rank.  Gathers of one communicator may run
  * on different streams: a gather waits for the previous one (an event on its stream) before it
- * reuses the staging buffers.  ICP4R_GATHER_PADDED=1 at icp4r_comm_create (a test switch) sends
- * every gather through the padded branch. */
+ * reuses the staging buffers.  The context's plan option "gather_padded" = 1 at icp4r_comm_create
+ * (a test switch) sends every gather through the padded branch.  A communicator may outlive its
+ * context: after icp4r_destroy(ctx) a gather needs an explicit hip_stream (NULL is
+ * ICP4R_E_INVALID), and icp4r_align_batch_sharded is ICP4R_E_INVALID. */
 int icp4r_gather_results(icp4r_comm* comm, const icp4r_result* shard_rows, int32_t npairs, icp4r_result* gathered,
                          void* hip_stream);
 

@@ -51,3 +51,12 @@ def gpu_ctx():
     ctx = icp4r.Context(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture
+def plan(gpu_ctx):
+    """Plan options (icp4r_set_plan_option) on the session's GPU context for one test: plan(groups=1,
+    ...) sets them; every option is back at its default afterwards."""
+    gpu_ctx.reset_plan_options()
+    yield gpu_ctx.set_plan
+    gpu_ctx.reset_plan_options()

@@ -77,7 +77,7 @@ def test_params_default_matches_pcl():
     assert math.isinf(p.huber_delta)
     assert p.fitness_max_range == sys.float_info.max
     L = icp4r.load()
-    assert L.icp4r_abi_version() == 4
+    assert L.icp4r_abi_version() == 5
     assert b"gfx950" in L.icp4r_version()
 
 
@@ -89,52 +89,103 @@ def test_struct_layouts():
     assert icp4r.Result.fitness.offset == 64
 
 
-def test_plan_geometry(monkeypatch):
+def test_plan_geometry():
     import icp4r
 
-    big = icp4r.plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
-    assert big["pruned"] and big["lds"] and big["q"] == 2 and big["leaf"] == 16 and big["nn_blocks"] == 1024
-    assert big["cache"] and icp4r.plan(1024, 16384, 8192)["lds"]
-    # the batched search's query records hold 14-bit source indices: larger sources take the tiled search
-    assert not icp4r.plan(1024, 16385, 8192)["lds"] and not icp4r.plan(1024, 16385, 8192)["cache"]
-    monkeypatch.setenv("ICP4R_NN_LDS", "1")
-    assert not icp4r.plan(8, 20000, 8192)["lds"]  # ... even when forced
-    monkeypatch.delenv("ICP4R_NN_LDS")
-    assert not icp4r.plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
-    assert not icp4r.plan(1024, 8192, 65540)["lds"] and icp4r.plan(1024, 8192, 65540)["pruned"]
-    c1 = icp4r.plan(1, 2048, 2048)  # C1: the multi-launch plan, one tile x 16 query parts of 128
-    assert c1["pruned"] and not c1["lds"] and not c1["solo"] and c1["nn_blocks"] == 16
-    small = icp4r.plan(1, 1024, 2048)  # up to 1024 sources: the whole registration in one workgroup
-    assert small["pruned"] and not small["lds"] and small["solo"] and small["nn_blocks"] == 1
-    assert icp4r.plan(200, 1024, 8192)["solo"] and not icp4r.plan(200, 1025, 8192)["solo"]
-    assert not big["solo"] and not icp4r.plan(1, 2048, 8193)["solo"]
-    single = icp4r.plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 64 query parts of 128
-    assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 64
-    monkeypatch.setenv("ICP4R_TILE_RUN", "64")  # runs of 64 queries: parts of 1024
-    assert icp4r.plan(1, 8192, 8192)["nn_blocks"] == 8 and icp4r.plan(1, 8192, 65540)["nn_blocks"] == 72
-    monkeypatch.delenv("ICP4R_TILE_RUN")
-    assert icp4r.plan(64, 8192, 8192)["nn_blocks"] == 64 * 8  # a small batch already covers the CUs
-    monkeypatch.setenv("ICP4R_SOLO", "1")  # forced: up to the cached-neighbour test's 16384 sources
-    assert icp4r.plan(1, 8192, 8192)["solo"] and icp4r.plan(200, 16384, 8192)["solo"]
-    assert not icp4r.plan(200, 16385, 8192)["solo"]
-    monkeypatch.setenv("ICP4R_SOLO", "0")
-    assert not icp4r.plan(1, 2048, 2048)["solo"] and icp4r.plan(1, 2048, 2048)["nn_blocks"] == 16
-    monkeypatch.delenv("ICP4R_SOLO")
-    c5 = icp4r.plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 32 query parts
-    assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 32 * 9
-    monkeypatch.setenv("ICP4R_NN_TILE", "0")  # the streamed kernel instead
-    single = icp4r.plan(1, 8192, 8192)  # one query per lane, the target in 4 chunks
-    assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32 * 4
-    c5 = icp4r.plan(1, 8192, 65540)  # 513 superblocks in 9 chunks of <= 64
-    assert c5["pruned"] and not c5["lds"] and c5["nn_blocks"] == 32 * 9
-    monkeypatch.delenv("ICP4R_NN_TILE")
-    brute = icp4r.plan(1024, 8192, 8192, icp4r.NN_BRUTE)
-    assert not brute["pruned"] and brute["q"] == 4 and brute["splits"] == 1
-    bsingle = icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)
-    assert bsingle["splits"] > 1 and bsingle["nn_blocks"] >= 512
-    tiny = icp4r.plan(1, 10, 7)  # small target: brute force
-    assert not tiny["pruned"] and tiny["q"] == 1 and tiny["splits"] == 1
-    assert icp4r.plan(1, 10, 7, icp4r.NN_PRUNED)["pruned"]
+    ctx = icp4r.Context(icp4r.NO_DEVICE)  # plan options without a GPU
+    plan = lambda *a, **k: icp4r.plan(*a, ctx=ctx, **k)  # noqa: E731
+    try:
+        big = plan(1024, 8192, 8192)  # C3: pruned search, targets in LDS, one workgroup per pair
+        assert big["pruned"] and big["lds"] and big["q"] == 2 and big["leaf"] == 16 and big["nn_blocks"] == 1024
+        assert big["cache"] and plan(1024, 16384, 8192)["lds"]
+        # the batched search's query records hold 14-bit source indices: larger sources take the tiled search
+        assert not plan(1024, 16385, 8192)["lds"] and not plan(1024, 16385, 8192)["cache"]
+        ctx.set_plan_option("nn_lds", 1)
+        assert not plan(8, 20000, 8192)["lds"]  # ... even when forced
+        ctx.reset_plan_options()
+        assert not plan(1024, 8192, 8193)["lds"]  # target set larger than LDS: streamed kernel
+        assert not plan(1024, 8192, 65540)["lds"] and plan(1024, 8192, 65540)["pruned"]
+        c1 = plan(1, 2048, 2048)  # C1: the multi-launch plan, one tile x 16 query parts of 128
+        assert c1["pruned"] and not c1["lds"] and not c1["solo"] and c1["nn_blocks"] == 16
+        small = plan(1, 1024, 2048)  # up to 1024 sources: the whole registration in one workgroup
+        assert small["pruned"] and not small["lds"] and small["solo"] and small["nn_blocks"] == 1
+        assert plan(200, 1024, 8192)["solo"] and not plan(200, 1025, 8192)["solo"]
+        assert not big["solo"] and not plan(1, 2048, 8193)["solo"]
+        single = plan(1, 8192, 8192)  # C2: the multi-launch plan, one target tile x 64 query parts of 128
+        assert single["pruned"] and not single["lds"] and not single["solo"] and single["nn_blocks"] == 64
+        ctx.set_plan_option("tile_run", 64)  # runs of 64 queries: parts of 1024
+        assert plan(1, 8192, 8192)["nn_blocks"] == 8 and plan(1, 8192, 65540)["nn_blocks"] == 72
+        ctx.reset_plan_options()
+        assert plan(64, 8192, 8192)["nn_blocks"] == 64 * 8  # a small batch already covers the CUs
+        ctx.set_plan_option("solo", 1)  # forced: up to the cached-neighbour test's 16384 sources
+        assert plan(1, 8192, 8192)["solo"] and plan(200, 16384, 8192)["solo"]
+        assert not plan(200, 16385, 8192)["solo"]
+        ctx.set_plan_option("solo", 0)
+        assert not plan(1, 2048, 2048)["solo"] and plan(1, 2048, 2048)["nn_blocks"] == 16
+        ctx.reset_plan_options()
+        c5 = plan(1, 8192, 65540)  # C5: 9 target tiles of <= 8192 x 32 query parts
+        assert c5["pruned"] and not c5["lds"] and not c5["solo"] and c5["nn_blocks"] == 32 * 9
+        ctx.set_plan_option("nn_tile", 0)  # the streamed kernel instead
+        single = plan(1, 8192, 8192)  # one query per lane, the target in 4 chunks
+        assert single["pruned"] and not single["lds"] and single["q"] == 1 and single["nn_blocks"] == 32 * 4
+        c5 = plan(1, 8192, 65540)  # 513 superblocks in 9 chunks of <= 64
+        assert c5["pruned"] and not c5["lds"] and c5["nn_blocks"] == 32 * 9
+        ctx.reset_plan_options()
+        brute = plan(1024, 8192, 8192, icp4r.NN_BRUTE)
+        assert not brute["pruned"] and brute["q"] == 4 and brute["splits"] == 1
+        bsingle = plan(1, 8192, 8192, icp4r.NN_BRUTE)
+        assert bsingle["splits"] > 1 and bsingle["nn_blocks"] >= 512
+        tiny = plan(1, 10, 7)  # small target: brute force
+        assert not tiny["pruned"] and tiny["q"] == 1 and tiny["splits"] == 1
+        assert plan(1, 10, 7, icp4r.NN_PRUNED)["pruned"]
+        # the wide update: PCL numerics only, at most one pair per CU, not with the fused cache test
+        assert plan(1, 8192, 8192)["wide_update"] and plan(200, 8192, 8192)["wide_update"]
+        assert not plan(1, 8192, 8192, numerics=icp4r.NUMERICS_F64)["wide_update"]
+        assert not plan(1024, 8192, 8192)["wide_update"]
+        ctx.set_plan_option("wide_update", 0)
+        assert not plan(1, 8192, 8192)["wide_update"]
+        # without a context: the defaults
+        assert icp4r.plan(1, 8192, 8192) == icp4r.plan(1, 8192, 8192, ctx=icp4r.Context(icp4r.NO_DEVICE))
+    finally:
+        ctx.close()
+
+
+def test_plan_options_api():
+    """icp4r_set_plan_option / get / reset: every documented name is known, unknown
+    names and a group count that would share a hardware queue are refused, reset restores the
+    defaults, and a context without a device holds options but fails every device call."""
+    import numpy as np
+
+    import icp4r
+
+    ctx = icp4r.Context(icp4r.NO_DEVICE)
+    try:
+        for name in icp4r.PLAN_OPTIONS:
+            v, is_set = ctx.get_plan_option(name)
+            assert not is_set, name
+        assert ctx.get_plan_option("groups") == (2, False) and ctx.get_plan_option("leaf") == (16, False)
+        ctx.set_plan(groups=1, nn_cache=0)
+        assert ctx.get_plan_option("groups") == (1, True) and ctx.get_plan_option("nn_cache") == (0, True)
+        for bad in (("groups", 4), ("groups", 0), ("no_such_option", 1), ("xpad", -1)):
+            with pytest.raises(icp4r.ICP4RError):
+                ctx.set_plan_option(*bad)
+        ctx.reset_plan_options()
+        assert ctx.get_plan_option("groups") == (2, False)
+        with pytest.raises(icp4r.ICP4RError):
+            ctx.align(np.zeros((8, 4), np.float32), np.zeros((8, 4), np.float32))
+    finally:
+        ctx.close()
+    assert icp4r.env_plan({"ICP4R_GROUPS": "1", "ICP4R_NN_CACHE": "0", "ICP4R_OTHER": "3"}) == {"groups": 1, "nn_cache": 0}
+
+
+def test_library_reads_no_environment():
+    """Plan choices come from icp4r_set_plan_option only: the shipped library imports no getenv
+    (deployment behaviour cannot depend on the process environment)."""
+    import icp4r
+
+    out = subprocess.run(["nm", "-D", "--undefined-only", icp4r.library_path], capture_output=True, text=True).stdout
+    assert "getenv" not in out, [l for l in out.splitlines() if "getenv" in l]
+    assert out.strip(), "nm printed nothing"
 
 
 def test_fails_loudly_without_library(tmp_path, monkeypatch):

@@ -124,7 +124,7 @@ def test_gpu_covariances_match_oracle(gpu_ctx, oracle_mod, reg):
 
 
 @pytest.mark.gpu
-def test_gpu_pruned_knn_equals_brute_force(gpu_ctx, oracle_mod, monkeypatch):
+def test_gpu_pruned_knn_equals_brute_force(gpu_ctx, oracle_mod, plan):
     """The Morton-pruned k-NN (clouds >= 512 points) returns exactly the brute-force neighbour sets:
     covariances bit-identical, including clouds with duplicated points (distance ties)."""
     gicp = _gicp()
@@ -133,9 +133,9 @@ def test_gpu_pruned_knn_equals_brute_force(gpu_ctx, oracle_mod, monkeypatch):
     for cloud in (src, dup, _grid_plane(40)):
         for k in (1, 5, 20, 32):
             pruned = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
-            monkeypatch.setenv("ICP4R_GICP_COV_BRUTE", "1")
+            plan(gicp_cov_brute=1)
             brute = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
-            monkeypatch.delenv("ICP4R_GICP_COV_BRUTE")
+            plan(gicp_cov_brute=0)
             np.testing.assert_array_equal(pruned, brute)
     want = oracle_mod.gicp_covariances(dup, 5, 3)
     np.testing.assert_allclose(gicp.covariances(dup, 5, 3, ctx=gpu_ctx), want, rtol=1e-9, atol=1e-12)

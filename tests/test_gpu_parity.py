@@ -142,9 +142,16 @@ def test_icp_random_pairs_pcl_defaults(gpu_ctx, oracle_mod, i):
     (8192, 8192, {"eigen_l1_bytes": -1}),                    # unblocked: one chain of |C|
     (8192, 8192, {"eigen_l1_bytes": 49152, "eigen_gebp_mr": 16}),  # other host facts
 ])
-def test_sigma_panels_vs_oracle(gpu_ctx, oracle_mod, n, m, kw):
+@pytest.mark.parametrize("wide", [1, 0])
+def test_sigma_panels_vs_oracle(gpu_ctx, oracle_mod, n, m, kw, wide, plan):
+    """Both single-pair updates on the multi-launch plan (solo = 0): fold_update_wide_kernel (the
+    panels side by side) and, with plan option wide_update = 0, fold_update_kernel's sequential pass B
+    over correspondence records (test_sigma_panels_batch_and_solo covers solo_kernel)."""
     import icp4r
 
+    plan(wide_update=wide, solo=0)
+    pl = icp4r.plan(1, n, m, ctx=gpu_ctx)
+    assert pl["wide_update"] == bool(wide) and not pl["solo"]
     src, tgt = _pair(700 + n % 97, n, m)
     r, out = gpu_ctx.align(src, tgt, icp4r.default_params(**kw), want_aligned=True)
     o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True, **kw)
@@ -157,13 +164,13 @@ def test_sigma_panels_vs_oracle(gpu_ctx, oracle_mod, n, m, kw):
     assert (out == o["aligned"]).all()
 
 
-@pytest.mark.parametrize("solo", ["0", "1"])
-def test_sigma_panels_batch_and_solo(gpu_ctx, oracle_mod, solo, monkeypatch):
+@pytest.mark.parametrize("solo,wide", [("0", 1), ("0", 0), ("1", 1)])
+def test_sigma_panels_batch_and_solo(gpu_ctx, oracle_mod, solo, wide, plan):
     """Panels in the one-workgroup registration (solo_kernel, forced up to 16k sources) and in a
-    batch of ragged pairs, against the oracle pair by pair."""
+    batch of ragged pairs (either update kernel), against the oracle pair by pair."""
     import icp4r
 
-    monkeypatch.setenv("ICP4R_SOLO", solo)
+    plan(solo=int(solo), wide_update=wide)
     shapes = [(1024, 1024), (2048, 1500), (700, 2048), (5000, 4000), (681, 681)]
     pairs = [_pair(800 + k, n, m) for k, (n, m) in enumerate(shapes)]
     p = icp4r.default_params(max_iterations=12)
@@ -233,8 +240,8 @@ def test_target_split_equals_unsplit(gpu_ctx):
     import icp4r
 
     s, t = _pair(300, 8192)
-    assert icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE)["splits"] > 1
-    assert icp4r.plan(64, 8192, 8192, icp4r.NN_BRUTE)["splits"] == 1
+    assert icp4r.plan(1, 8192, 8192, icp4r.NN_BRUTE, ctx=gpu_ctx)["splits"] > 1
+    assert icp4r.plan(64, 8192, 8192, icp4r.NN_BRUTE, ctx=gpu_ctx)["splits"] == 1
     p = icp4r.default_params(max_iterations=20, nn_mode=icp4r.NN_BRUTE)
     r, _ = gpu_ctx.align(s, t, p)
     res = gpu_ctx.align_batch_host(*_batch([(s, t)] * 64), params=p)
@@ -245,7 +252,7 @@ def test_target_split_equals_unsplit(gpu_ctx):
 @pytest.mark.parametrize("lds,cache,tile,solo", [("0", "1", "1", "1"), ("0", "1", "1", "0"), ("0", "1", "0", "0"),
                                                 ("1", "0", "1", "1"), ("1", "1", "1", "1")])
 @pytest.mark.parametrize("case", ["c2", "ragged", "far_guess", "lattice", "map", "dup_map", "big_src", "huge_src"])
-def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, monkeypatch):
+def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, plan):
     """Pruned (the whole registration per workgroup, LDS target tiles x query parts, the scalar-cache
     stream, or with the target set in LDS and per-query work lists, with or without the
     cached-neighbour test), brute-force and packed searches produce bit-identical registrations (T,
@@ -255,10 +262,10 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, monkeypatch):
     (their own index) with ones ordered by the target's tree."""
     import icp4r
 
-    monkeypatch.setenv("ICP4R_NN_LDS", lds)  # 1: force nn_lds_kernel whenever the targets fit
-    monkeypatch.setenv("ICP4R_NN_CACHE", cache)
-    monkeypatch.setenv("ICP4R_NN_TILE", tile)  # 0: the scalar-cache stream for the unbatched plan
-    monkeypatch.setenv("ICP4R_SOLO", solo)  # 0: the multi-launch unbatched plan (solo_kernel off)
+    plan(nn_lds=int(lds))  # 1: force nn_lds_kernel whenever the targets fit
+    plan(nn_cache=int(cache))
+    plan(nn_tile=int(tile))  # 0: the scalar-cache stream for the unbatched plan
+    plan(solo=int(solo))  # 0: the multi-launch unbatched plan (solo_kernel off)
     guess = None
     if case == "c2":
         pairs = [_pair(310, 8192)]
@@ -289,7 +296,7 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, monkeypatch):
     elif case == "huge_src":  # sources past the batched search's 14-bit query records (tiled search)
         shapes = [(20000, 8000), (16385, 4096), (16384, 8192), (700, 300)]
         pairs = [_pair(360 + k, n, m) for k, (n, m) in enumerate(shapes)]
-        assert not icp4r.plan(len(pairs), 20000, 8192)["lds"]
+        assert not icp4r.plan(len(pairs), 20000, 8192, ctx=gpu_ctx)["lds"]
     else:
         sp, tp = _pair(340, 3000, 6000)
         pairs = [(sp, np.concatenate([tp, tp]))]
@@ -308,7 +315,7 @@ def test_nn_modes_identical(gpu_ctx, case, lds, cache, tile, solo, monkeypatch):
 
 
 @pytest.mark.parametrize("numerics,huber", [(0, float("inf")), (1, float("inf")), (0, 0.5), (1, 0.5)])
-def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatch):
+def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, plan):
     """The batched LDS search with the cached-neighbour test: bit-identical to the same search
     without it (every numerics / weighting), to the oracle (PCL numerics), and it resolves most
     queries of the late iterations without a search."""
@@ -317,14 +324,14 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
     npairs, n = 256, 8192
     pairs = [_pair(700 + k, n) for k in range(npairs)]
     args = _batch(pairs)
-    assert icp4r.plan(npairs, n, n)["lds"] and icp4r.plan(npairs, n, n)["cache"]
+    assert icp4r.plan(npairs, n, n, ctx=gpu_ctx)["lds"] and icp4r.plan(npairs, n, n, ctx=gpu_ctx)["cache"]
     p = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
                              numerics=numerics, huber_delta=huber)
-    monkeypatch.setenv("ICP4R_NN_CACHE", "0")
+    plan(nn_cache=0)
     gpu_ctx.reset_timers()
     plain = gpu_ctx.align_batch_host(*args, params=p)
     ev_plain, _ = gpu_ctx.nn_counters()
-    monkeypatch.setenv("ICP4R_NN_CACHE", "1")
+    plan(nn_cache=1)
     gpu_ctx.reset_timers()
     cached = gpu_ctx.align_batch_host(*args, params=p)
     ev_cached, _ = gpu_ctx.nn_counters()
@@ -341,10 +348,10 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, monkeypatc
             assert (cached[k]["T"].reshape(4, 4).T == o["T"]).all() and cached[k]["fitness"] == o["fitness"]
 
 
-def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
-    """nn_tile_kernel's queries per wave run (ICP4R_TILE_RUN 64 / 32 / 16 / 8: 1024 / 512 / 256 / 128 queries per
+def test_tile_run_lengths_identical(gpu_ctx, plan):
+    """nn_tile_kernel's queries per wave run (plan option tile_run 64 / 32 / 16 / 8: 1024 / 512 / 256 / 128 queries per
     workgroup, the single-pair plans' default picks the length whose grid covers the CUs), and the
-    update's transform deferred into the one-tile search or not (ICP4R_TILE_DEFER): bit-identical
+    update's transform deferred into the one-tile search or not (tile_defer): bit-identical
     registrations, one target tile (C2's and C1's shapes) and several (a scan-to-map target), fixed
     iterations and PCL's defaults, aligned clouds included."""
     import icp4r
@@ -354,11 +361,11 @@ def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
                    icp4r.default_params()):
         for s, t in cases:
             out = {}
-            # (ICP4R_TILE_DEFER=0: the update transforms the cloud itself instead of the next search)
+            # (tile_defer = 0: the update transforms the cloud itself instead of the next search)
             for run, defer in (("64", "1"), ("32", "1"), ("16", "1"), ("8", "1"), ("16", "0")):
-                monkeypatch.setenv("ICP4R_TILE_RUN", run)
-                monkeypatch.setenv("ICP4R_TILE_DEFER", defer)
-                pl = icp4r.plan(1, len(s), len(t))
+                plan(tile_run=int(run))
+                plan(tile_defer=int(defer))
+                pl = icp4r.plan(1, len(s), len(t), ctx=gpu_ctx)
                 assert pl["pruned"] and not pl["lds"] and not pl["solo"]
                 r, al = gpu_ctx.align(s, t, params, want_aligned=True)
                 out[run + defer] = (bytes(r), al.tobytes())
@@ -366,7 +373,7 @@ def test_tile_run_lengths_identical(gpu_ctx, monkeypatch):
 
 
 @pytest.mark.parametrize("early", [False, True])
-def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
+def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, plan):
     """The cached-neighbour test run in the tail of fold_update_kernel (default) instead of its own
     nn_cache_test_kernel launch: bit-identical batches, with fixed iterations and with PCL's early
     stops live (pairs converging at different iterations, so some skip the fused tail), over ragged
@@ -376,15 +383,15 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
     shapes = [(8192, 8192)] * 200 + [(8000, 8100), (4096, 8192), (2048, 600), (1000, 1200), (37, 4000)] * 12
     pairs = [_pair(1300 + k, n, m) for k, (n, m) in enumerate(shapes)]
     args = _batch(pairs)
-    assert icp4r.plan(len(pairs), 8192, 8192)["lds"] and icp4r.plan(len(pairs), 8192, 8192)["cache"]
+    assert icp4r.plan(len(pairs), 8192, 8192, ctx=gpu_ctx)["lds"] and icp4r.plan(len(pairs), 8192, 8192, ctx=gpu_ctx)["cache"]
     kw = {} if early else dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     p = icp4r.default_params(max_iterations=20, **kw)
     out = {}
-    # (ICP4R_FUSE_ORDER=1, the default: the update's last workgroup also builds the next search's
+    # (fuse_order = 1, the default: the update's last workgroup also builds the next search's
     # work list from the words the other workgroups publish; 0: nn_order_kernel does)
     for fuse, order in (("0", "1"), ("1", "0"), ("1", "1")):
-        monkeypatch.setenv("ICP4R_FUSE_TEST", fuse)
-        monkeypatch.setenv("ICP4R_FUSE_ORDER", order)
+        plan(fuse_test=int(fuse))
+        plan(fuse_order=int(order))
         gpu_ctx.reset_timers()
         out[fuse + order] = gpu_ctx.align_batch_host(*args, params=p)
         st = gpu_ctx.nn_stats()
@@ -401,9 +408,33 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, monkeypatch):
         assert out["1"][k]["iterations"] == o["iterations"]
 
 
+@pytest.mark.parametrize("cache", [0, 1])
+def test_batched_update_panels_with_rejections(gpu_ctx, oracle_mod, cache, plan):
+    """fold_update_kernel, the batched plan's update (more pairs than CUs), with rejected
+    correspondences: the sigma panels then start at ranked positions counted in accepted
+    correspondences (fold_bounds).  cache = 0 takes the correspondence records (no cached-neighbour
+    test, nothing fused); cache = 1 reads X and nn_t.  Sampled pairs bit-equal to the oracle, and
+    every one of them really rejected some correspondences."""
+    import icp4r
+
+    plan(nn_cache=cache)
+    shapes = [(2048, 2048)] * 290 + [(3000, 2500), (1400, 3000)] * 5
+    pairs = [_pair(2500 + k, n, m) for k, (n, m) in enumerate(shapes)]
+    pl = icp4r.plan(len(pairs), 3000, 3000, ctx=gpu_ctx)
+    assert pl["lds"] and pl["cache"] == bool(cache) and not pl["wide_update"]
+    kw = dict(max_iterations=10, max_correspondence_distance=0.45)
+    res = gpu_ctx.align_batch_host(*_batch(pairs), params=icp4r.default_params(**kw))
+    for k in (0, 7, 145, 289, 290, 291, 299):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, **kw)
+        assert 0 < o["n_correspondences"] < len(pairs[k][0]), k
+        assert res[k]["n_correspondences"] == o["n_correspondences"], k
+        assert res[k]["iterations"] == o["iterations"], k
+        assert (res[k]["T"].reshape(4, 4).T == o["T"]).all() and res[k]["fitness"] == o["fitness"], k
+
+
 @pytest.mark.parametrize("kw", [{}, {"max_correspondence_distance": 1.0}, {"huber_delta": 0.5}])
-def test_sums_tail_identical(gpu_ctx, oracle_mod, kw, monkeypatch):
-    """The fused tail folding the next pass A's source centroid sums (ICP4R_SUMS_TAIL, eligible
+def test_sums_tail_identical(gpu_ctx, oracle_mod, kw, plan):
+    """The fused tail folding the next pass A's source centroid sums (plan option sums_tail, eligible
     registrations: every correspondence kept, unweighted, no MSE criterion; the other two
     parametrisations are ineligible and must take the normal pass A): bit-identical batches either
     way, and the oracle on sampled pairs."""
@@ -412,12 +443,12 @@ def test_sums_tail_identical(gpu_ctx, oracle_mod, kw, monkeypatch):
     shapes = [(2048, 2048)] * 240 + [(3000, 2500), (700, 2048), (2048, 900)] * 8
     pairs = [_pair(1700 + k, n, m) for k, (n, m) in enumerate(shapes)]
     args = _batch(pairs)
-    assert icp4r.plan(len(pairs), 3000, 2500)["lds"]
+    assert icp4r.plan(len(pairs), 3000, 2500, ctx=gpu_ctx)["lds"]
     fixed = dict(max_iterations=15, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, **kw)
     p = icp4r.default_params(**fixed)
     out = {}
     for on in ("0", "1"):
-        monkeypatch.setenv("ICP4R_SUMS_TAIL", on)
+        plan(sums_tail=int(on))
         out[on] = gpu_ctx.align_batch_host(*args, params=p)
     assert out["1"].tobytes() == out["0"].tobytes()
     for k in (0, 239, 240, 242):
@@ -426,9 +457,9 @@ def test_sums_tail_identical(gpu_ctx, oracle_mod, kw, monkeypatch):
 
 
 @pytest.mark.parametrize("npairs", [1, 300])
-def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
+def test_source_order_identical(gpu_ctx, npairs, plan):
     """Sources ordered by descending their target's kd tree (src_order_kernel; the batched plan's default) or by their
-    own kd tree (ICP4R_SRC_ORDER=0): the order and the first-pass seeds change, the registrations do
+    own kd tree (plan option src_order = 0): the order and the first-pass seeds change, the registrations do
     not — bit-identical on the single-pair pruned kernel and the batched LDS search, ragged shapes,
     a lattice (ties) and targets over 8192 points (their sources keep the own-tree path)."""
     import icp4r
@@ -447,7 +478,7 @@ def test_source_order_identical(gpu_ctx, npairs, monkeypatch):
     p = icp4r.default_params(max_iterations=15)
     out = {}
     for so in ("0", "1"):
-        monkeypatch.setenv("ICP4R_SRC_ORDER", so)
+        plan(src_order=int(so))
         out[so] = gpu_ctx.align_batch_host(*args, params=p)
     assert out["0"].tobytes() == out["1"].tobytes()
     assert (out["1"]["status"] == 0).all()
@@ -552,12 +583,12 @@ def test_pcl_facade_callsite(oracle_mod, golden, exe_name):
 
 
 @pytest.mark.parametrize("solo", ["1", "0"])
-def test_kernel_timing_api(gpu_ctx, solo, monkeypatch):
+def test_kernel_timing_api(gpu_ctx, solo, plan):
     """The NN kernel timer counts one launch per NN pass (5 iterations + the fitness pass) on the
     multi-launch plan, and the one solo_kernel launch of the whole registration on the solo plan."""
     import icp4r
 
-    monkeypatch.setenv("ICP4R_SOLO", solo)
+    plan(solo=int(solo))
     s, t = _pair(700, 2048)
     p = icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1)
     gpu_ctx.reset_timers()  # per-kernel timing off (the default): only the whole call is timed
@@ -621,7 +652,7 @@ def test_kd_index_degenerate_clouds(gpu_ctx, shape, m):
     assert (gi == bi).all()
 
 
-def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, monkeypatch):
+def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, plan):
     """BASELINE.json configs[2] at its own size, exactly as bench.py runs it: 1024 pairs of 8192/8192
     points (pair i seeded 1000 + i), 20 fixed iterations + the fitness pass, device-resident, the
     default plan (two pair groups on two streams, cached-neighbour test fused into the update).
@@ -645,8 +676,8 @@ def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, monkeypatch):
                         tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,
                         max_src_n=n, max_tgt_n=n)
     params = icp4r.default_params(max_iterations=iters, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
-    plan = icp4r.plan(P, n, n)
-    assert plan["lds"] and plan["cache"]
+    pl = icp4r.plan(P, n, n, ctx=gpu_ctx)
+    assert pl["lds"] and pl["cache"]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def run():
@@ -655,12 +686,10 @@ def test_c3_full_size_bench_workload(gpu_ctx, oracle_mod, monkeypatch):
         torch.cuda.synchronize(dev)
         return np.frombuffer(out.cpu().numpy().tobytes(), dtype=icp4r.RESULT_DTYPE)
 
-    for k in ("ICP4R_GROUPS", "ICP4R_NN_CACHE", "ICP4R_FUSE_TEST", "ICP4R_NN_LDS"):
-        monkeypatch.delenv(k, raising=False)
+    gpu_ctx.reset_plan_options()
     default = run()
     assert (default["status"] == 0).all() and (default["iterations"] == iters).all()
-    monkeypatch.setenv("ICP4R_GROUPS", "1")
-    monkeypatch.setenv("ICP4R_NN_CACHE", "0")
+    plan(groups=1, nn_cache=0)
     plain = run()
     assert default.tobytes() == plain.tobytes()
     picks = [0, 1, 100, 255, 384, 510, 511, 512, 513, 640, 777, 900, 1000, 1021, 1022, 1023]
@@ -685,8 +714,8 @@ def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
     mp = synth.make_map_pair(0)
     src, tgt = mp.src_xyzi(), mp.tgt_xyzi()
     assert (len(src), len(tgt)) == (8192, 65540)
-    plan = icp4r.plan(1, len(src), len(tgt))
-    assert plan["pruned"] and not plan["lds"]
+    pl = icp4r.plan(1, len(src), len(tgt), ctx=gpu_ctx)
+    assert pl["pruned"] and not pl["lds"]
     kw = dict(mse_threshold_absolute=-1.0, transformation_epsilon=-1.0) if fixed else {}
     r, al = gpu_ctx.align(src, tgt, icp4r.default_params(max_iterations=20, **kw), want_aligned=True)
     o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=20, aligned=True, **kw)
@@ -701,10 +730,10 @@ def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
 
 
 @pytest.mark.parametrize("npairs", [1, 5, 40])
-def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypatch):
+def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, plan):
     """Targets too large for the in-LDS kd build (the C5 submap class): their Morton sort on one
     workgroup per 8192-point chunk (index_mo_hist_kernel / index_mo_scatter_kernel, the default for
-    few pairs) or on one workgroup per target (ICP4R_MORTON_MWG=0) — the order changes, the
+    few pairs) or on one workgroup per target (plan option morton_mwg = 0) — the order changes, the
     registrations do not: bit-identical, ragged targets (8193 .. 40000 points, a partial last chunk,
     a lattice with ties, a small target in the same batch), and bit-equal to the oracle."""
     import icp4r
@@ -724,7 +753,7 @@ def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, monkeypat
     p = icp4r.default_params(max_iterations=12)
     out = {}
     for mwg in ("0", "1"):
-        monkeypatch.setenv("ICP4R_MORTON_MWG", mwg)
+        plan(morton_mwg=int(mwg))
         out[mwg] = gpu_ctx.align_batch_host(*args, params=p)
     assert out["0"].tobytes() == out["1"].tobytes()
     assert (out["1"]["status"] == 0).all()

@@ -105,9 +105,9 @@ def test_rccl_single_rank_sharded_batch(gpu_ctx):
         comm.close()
 
 
-def test_rccl_gather_padded_branch(gpu_ctx, monkeypatch):
+def test_rccl_gather_padded_branch(gpu_ctx, plan):
     """icp4r_gather_results' unequal-shard branch (padded send / recv staging, one copy per rank),
-    forced on a one-rank communicator by the ICP4R_GATHER_PADDED test switch: the rows of a batch
+    forced on a one-rank communicator by the gather_padded plan option (a test switch): the rows of a batch
     whose size no rank count divides evenly (7 pairs) land byte for byte in global order, also when
     consecutive gathers run on different streams (the staging is reused behind an event)."""
     import torch
@@ -122,7 +122,7 @@ def test_rccl_gather_padded_branch(gpu_ctx, monkeypatch):
     ref_h = gpu_ctx.align_batch_host(*args, params=params)
     dev = torch.device("cuda", 0)
     rows = torch.from_numpy(np.frombuffer(ref_h.tobytes(), dtype=np.uint8).reshape(P, 96).copy()).to(dev)
-    monkeypatch.setenv("ICP4R_GATHER_PADDED", "1")
+    plan(gather_padded=1)
     comm = icp4r.Comm(gpu_ctx, 1, 0, icp4r.Comm.unique_id())
     s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     try:

@@ -28,7 +28,7 @@ from icp4r import synth  # noqa: E402
 
 
 def run(name, src, tgt, params, oparams, reps=5):
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     ctx.set_kernel_timing(True)  # (this tool reports per-kernel times)
     r, _ = ctx.align(src, tgt, params)  # warm-up
     ctx.reset_timers()

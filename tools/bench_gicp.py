@@ -89,7 +89,7 @@ def main():
     b.src, b.tgt = ts["src"].data_ptr(), ts["tgt"].data_ptr()
     b.src_off, b.src_n, b.tgt_off, b.tgt_n = ts["so"].data_ptr(), ts["sn"].data_ptr(), ts["to"].data_ptr(), ts["tn"].data_ptr()
     b.npairs, b.max_src_n, b.max_tgt_n = len(pairs), int(sn.max()), int(tn.max())
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     ctx.set_kernel_timing(True)  # (this tool reports per-kernel times)
     k = a.k or k
     p = gicp.default_params(k_correspondences=k)

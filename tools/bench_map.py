@@ -49,7 +49,7 @@ def main():
     a = ap.parse_args()
     import torch
 
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     tree = KD_TREE(0.3, 0.6, 0.5, ctx=ctx)
     base = [synth.make_pair(7000 + i, 6554).src_xyzi() for i in range(64)]
     t0 = time.perf_counter()

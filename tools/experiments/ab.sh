@@ -9,16 +9,11 @@ R=$1; shift
 mkdir -p gpurun_out
 for r in $(seq 1 "$R"); do
     for lib in "$@"; do
-        out=$(ICP4R_LIBRARY="$lib" timeout -k 10 120 python3 bench.py --no-cpu --no-upload --no-c5 --check 2 --steps 20 \
+        out=$(ICP4R_LIBRARY="$lib" timeout -k 10 120 python3 bench.py --plan-from-env --no-cpu --no-upload --configs= --check 2 --steps 20 \
               2> gpurun_out/ab_err.log | grep '^{')
         rc=$?
         if [ $rc -ne 0 ]; then echo "ab: bench failed on $lib (rc=$rc)"; tail -5 gpurun_out/ab_err.log; exit 2; fi
         echo "$out" >> gpurun_out/ab.jsonl
-        python3 - "$lib" "$out" <<'EOF'
-import json, sys
-r = json.loads(sys.argv[2])
-print(f"{sys.argv[1]:40s} value {r['value']:9.0f}  search {r['roofline']['avg_launch_ms']*1e3:6.1f} us  "
-      f"update {r['update_kernel']['avg_launch_ms']*1e3:6.1f} us  batch {r['batch_device_ms']:6.3f} ms  parity {r['parity_ok']}", flush=True)
-EOF
+        python3 tools/experiments/benchline.py "$lib" "$out"
     done
 done

@@ -33,7 +33,7 @@ def main():
     tgt = np.concatenate([p.tgt_xyzi() for p in pairs])
     cnt = np.full(P, n, np.int32)
     off = np.arange(P, dtype=np.int64) * n
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
 
     prev_h = prev_e = 0
     for k in range(1, a.iters + 2):

@@ -9,7 +9,7 @@ R=$1; CFG=$2; shift 2
 for r in $(seq 1 "$R"); do
   for setting in "$@"; do
     envs=(); [ "$setting" != "-" ] && read -r -a envs <<< "$setting"
-    env "${envs[@]}" timeout -k 10 150 python3 bench.py --no-c3 --no-cpu --check 1 --configs "$CFG" > gpurun_out/config_ab.json 2> gpurun_out/config_ab_err.log || { echo "bench failed: $setting"; tail -20 gpurun_out/config_ab_err.log; exit 2; }
+    env "${envs[@]}" timeout -k 10 150 python3 bench.py --plan-from-env --no-c3 --no-cpu --check 1 --configs "$CFG" > gpurun_out/config_ab.json 2> gpurun_out/config_ab_err.log || { echo "bench failed: $setting"; tail -20 gpurun_out/config_ab_err.log; exit 2; }
     python3 - "$setting" <<'PY'
 import json, sys
 r = json.loads([l for l in open("gpurun_out/config_ab.json") if l.startswith("{")][-1])

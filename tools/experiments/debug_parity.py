@@ -14,7 +14,7 @@ def ulps(a, b):
 
 g = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
 src, tgt = load_case_clouds(g["cases"][0])
-ctx = icp4r.Context(0)
+ctx = icp4r.Context(0, plan=icp4r.env_plan())
 for it in (1, 2, 3, 5, 10):
     r, out = ctx.align(src, tgt, icp4r.default_params(max_iterations=it), want_aligned=True)
     o = oracle.align(src, tgt, numerics=oracle.NUM_F32, max_iterations=it, trace=True, aligned=True)

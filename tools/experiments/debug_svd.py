@@ -9,7 +9,7 @@ rng = np.random.default_rng(0)
 k = 2000
 S = rng.normal(0, 100, (k, 9)).astype(np.float32)
 S[:1000] = (np.eye(3).ravel()[None, :] * 500 + rng.normal(0, 1, (1000, 9))).astype(np.float32)
-ctx = icp4r.Context(0)
+ctx = icp4r.Context(0, plan=icp4r.env_plan())
 Rg = np.zeros((k, 9), np.float32)
 rc = L.icp4r__test_rot_f32(ctx.handle, C.c_void_p(S.ctypes.data), C.c_void_p(Rg.ctypes.data), k)
 assert rc == 0, rc

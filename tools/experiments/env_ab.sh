@@ -9,16 +9,10 @@ mkdir -p gpurun_out
 for r in $(seq 1 "$R"); do
     for setting in "$@"; do
         envs=(); [ "$setting" != "-" ] && read -r -a envs <<< "$setting"
-        out=$(env "${envs[@]}" timeout -k 10 120 python3 bench.py --no-cpu --no-upload --no-c5 --check 2 --steps 20 \
+        out=$(env "${envs[@]}" timeout -k 10 120 python3 bench.py --plan-from-env --no-cpu --no-upload --configs= --check 2 --steps 20 \
               2> gpurun_out/env_ab_err.log | grep '^{')
         rc=$?
         if [ $rc -ne 0 ]; then echo "env_ab: bench failed on '$setting' (rc=$rc)"; tail -5 gpurun_out/env_ab_err.log; exit 2; fi
-        python3 - "$setting" "$out" <<'PY'
-import json, sys
-r = json.loads(sys.argv[2])
-print(f"{sys.argv[1]:36s} value {r['value']:9.0f}  search {r['roofline']['avg_launch_ms']*1e3:6.1f} us  "
-      f"update {r['update_kernel']['avg_launch_ms']*1e3:6.1f} us  batch {r['batch_device_ms']:6.3f} ms  "
-      f"hit {r['update_kernel'].get('cache_hit_rate') or 0:.4f}  parity {r['parity_ok']}", flush=True)
-PY
+        python3 tools/experiments/benchline.py "$setting" "$out"
     done
 done

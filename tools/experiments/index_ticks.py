@@ -37,7 +37,7 @@ def main():
         tgt = np.concatenate([p.tgt_xyzi() for p in pairs])
         cnt = np.full(P, a.points, np.int32)
         off = np.arange(P, dtype=np.int64) * a.points
-        ctx = icp4r.Context(0)
+        ctx = icp4r.Context(0, plan=icp4r.env_plan())
         p = icp4r.default_params(max_iterations=1, compute_fitness=0)
         for _ in range(2):
             ctx.align_batch_host(src, off, cnt, tgt, off, cnt, params=p)

@@ -34,7 +34,7 @@ def main():
     tgt = np.concatenate([p.tgt_xyzi() for p in pairs])
     cnt = np.full(P, n, np.int32)
     off = np.arange(P, dtype=np.int64) * n
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
     for k in range(1, a.iters + 1):

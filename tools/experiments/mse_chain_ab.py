@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
 import icp4r  # noqa: E402
 from icp4r import synth  # noqa: E402
 
-ctx = icp4r.Context(0)
+ctx = icp4r.Context(0, plan=icp4r.env_plan())
 for name, n in (("C1", 2048), ("C2", 8192)):
     p = synth.make_pair(0 if name == "C1" else 1, n)
     s, t = p.src_xyzi(), p.tgt_xyzi()

@@ -44,7 +44,7 @@ def main():
     tgt = np.concatenate([p.tgt_xyzi() for p in pairs])
     cnt = np.full(P, n, np.int32)
     off = np.arange(P, dtype=np.int64) * n
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     ctx.set_kernel_timing(True)
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]

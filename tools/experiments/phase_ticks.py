@@ -33,7 +33,7 @@ def ticks(ctx) -> list[float]:
 
 
 def main():
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     p = icp4r.default_params(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
                              eigen_l1_bytes=int(os.environ.get("EIGEN_L1", "0")))
     for n in (2048, 8192):

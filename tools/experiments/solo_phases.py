@@ -29,7 +29,7 @@ def main():
     os.environ.setdefault("ICP4R_SOLO", "1")  # (C2's 8192 sources are past the default solo size)
     for name, pair, params in (("C1", synth.make_pair(0, 2048), icp4r.default_params()),
                                ("C2", synth.make_pair(1, 8192), icp4r.default_params(**fixed))):
-        ctx = icp4r.Context(0)
+        ctx = icp4r.Context(0, plan=icp4r.env_plan())
         ctx.set_kernel_timing(True)
         s, t = pair.src_xyzi(), pair.tgt_xyzi()
         ctx.align(s, t, params)  # warm-up (allocates the tick slots)

@@ -25,7 +25,7 @@ def main():
     import icp4r
     from icp4r import synth
 
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     settings = {"pcl_defaults": icp4r.default_params(),
                 "fixed20": icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0,
                                                 transformation_epsilon=-1.0)}

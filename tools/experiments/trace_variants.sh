@@ -11,6 +11,6 @@ for spec in "$@"; do
     name=${spec%%:*}
     envs=${spec#*:}
     env $envs timeout -k 10 240 rocprofv3 --kernel-trace -d "gpurun_out/tv_$name" -o run --output-format csv -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu --check 0 --no-upload --configs= > "gpurun_out/tv_$name.log" 2>&1
+        python3 bench.py --plan-from-env --steps 2 --warmup 1 --no-cpu --check 0 --no-upload --configs= > "gpurun_out/tv_$name.log" 2>&1
     echo "trace_variants: $name done"
 done

@@ -40,7 +40,7 @@ def main():
     off = torch.arange(P, dtype=torch.int64, device=dev) * n
     cnt = torch.full((P,), n, dtype=torch.int32, device=dev)
     res = torch.zeros((P, 96), dtype=torch.uint8, device=dev)
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
                         tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), npairs=P, max_src_n=n, max_tgt_n=n)
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -44,7 +44,7 @@ def main():
     off = torch.arange(P, dtype=torch.int64, device=dev) * n
     cnt = torch.full((P,), n, dtype=torch.int32, device=dev)
     results = torch.zeros((P, 96), dtype=torch.uint8, device=dev)
-    ctx = icp4r.Context(0)
+    ctx = icp4r.Context(0, plan=icp4r.env_plan())
     params = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
     batch = icp4r.Batch(src=src.data_ptr(), tgt=tgt.data_ptr(), src_off=off.data_ptr(), src_n=cnt.data_ptr(),
                         tgt_off=off.data_ptr(), tgt_n=cnt.data_ptr(), guess=None, aligned=None, npairs=P,

@@ -21,7 +21,7 @@ run() {  # run <config> <dir-suffix> <rocprof args...>
         args="--no-c3 --no-cpu --check 0 --configs $cfg"
     fi
     ICP4R_GROUPS=1 timeout -k 10 300 rocprofv3 "$@" -d "gpurun_out/prof_${cfg}_$d" -o run --output-format csv -- \
-        python3 bench.py $args > "gpurun_out/prof_${cfg}_$d.log" 2>&1
+        python3 bench.py --plan-from-env $args > "gpurun_out/prof_${cfg}_$d.log" 2>&1
 }
 for cfg in ${CONFIGS//,/ }; do
     run "$cfg" stats --kernel-trace --stats
