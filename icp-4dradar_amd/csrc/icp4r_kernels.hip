@@ -3033,31 +3033,54 @@ __device__ __forceinline__ TAcc fold_tail(const float* f, int len, TAcc acc) {
     return acc;
 }
 
+// acc + x.x + x.y + x.z + x.w in that order, each IEEE add as v_add_f32 does it, with acc kept in one
+// register (the tied operand): the allocator had used a consumed group register as the running sum,
+// then copied the next group into place with 16 v_mov per round.
+__device__ __forceinline__ float chain_add4(float acc, const float4& x) {
+    asm("v_add_f32 %0, %1, %0\n\t"
+        "v_add_f32 %0, %2, %0\n\t"
+        "v_add_f32 %0, %3, %0\n\t"
+        "v_add_f32 %0, %4, %0"
+        : "+v"(acc)
+        : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w));
+    return acc;
+}
+
 // A panel chain's step over one chunk row (len <= T floats, T a multiple of 8; 16-B aligned): groups
-// of 16 floats, the next group's four ds_read_b128 issued before this group's 16 dependent adds (as
-// long as the LDS round trip), the rest through fold_tail — half fold_seq's registers: the panel fold
-// lanes share their waves' allocation with the fillers.
+// of 16 floats in two register sets that trade roles (the next group's four ds_read_b128 issued before
+// this group's 16 dependent adds, as long as the LDS round trip; no register copies: one set carried
+// into the next round had cost 16 v_mov and a full lgkmcnt wait per 16 adds, ~15 cycles per add
+// against ~7), the rest through fold_tail — half fold_seq's registers: the panel fold lanes share
+// their waves' allocation with the fillers.
 __device__ __forceinline__ float fold_row(const float* f, int len, float acc) {
     int k = 0;
-    if (len >= 16) {
-        float4 a[4];
+    if (len >= 32) {
+        float4 a[4], b[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
-        for (; k + 16 <= len; k += 16) {
-            const int nx = (k + 32 <= len) ? k + 16 : k;  // the next group, or a harmless re-read
-            float4 b[4];
+        for (; k + 32 <= len; k += 32) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + nx + 4 * u);
+            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + k + 16 + 4 * u);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                acc = acc + a[u].x;
-                acc = acc + a[u].y;
-                acc = acc + a[u].z;
-                acc = acc + a[u].w;
+                acc = chain_add4(acc, a[u]);
             }
+            const int nx = (k + 48 <= len) ? k + 32 : k;  // the next group, or a harmless re-read
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = b[u];
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + nx + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = chain_add4(acc, b[u]);
+            }
+        }
+        if (k + 16 <= len) {  // a holds f[k, k + 16)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = chain_add4(acc, a[u]);
+            }
+            k += 16;
         }
     }
     return k < len ? fold_tail<float>(f + k, len - k, acc) : acc;
@@ -3753,6 +3776,7 @@ struct FoldIn {
     const float4* X;
     const float4* NT;
     int n;
+    uint64_t* tk = nullptr;  // debug (phase ticks, pair 0, thread 0): pass B's sub-phase stamps
 };
 
 // A running exact sum of non-negative doubles that are widened floats: S in units of 2^E (E = the
@@ -3788,6 +3812,12 @@ __device__ __forceinline__ void wave_exact_total(uint64_t& S, int& E) {  // ever
     S = t;
     E = e;
 }
+
+constexpr int kSliceGroup = 14;  // panels folded together (9 x 14 = 126 chains: two fold waves)
+#ifndef ICP4R_FILL_BATCH
+#define ICP4R_FILL_BATCH 2
+#endif
+constexpr int kFillBatch = ICP4R_FILL_BATCH;  // a filler's correspondences in flight per round
 
 // Pass A of the PCL-numerics update by a workgroup of WG threads over LDS chunks of CH points
 // (buf: two chunks of 9 rows of ROW floats): wave 0 lanes 0..6 fold Σs, Σd (Eigen 3.3
@@ -3976,11 +4006,6 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
 //    strided ≡ 4 mod 8 floats so the fold lanes' ds_read_b128 hit distinct banks): the chain per
 //    panel is kc long instead of |C|.
 // Leaves the finished sigma in s.sigmaf.
-constexpr int kSliceGroup = 14;  // panels folded together (9 x 14 = 126 chains: two fold waves)
-#ifndef ICP4R_FILL_BATCH
-#define ICP4R_FILL_BATCH 2
-#endif
-constexpr int kFillBatch = ICP4R_FILL_BATCH;  // a filler's correspondences in flight per round
 
 // Panel starts of panels [s0, s0 + G] (point indices) when some correspondences are rejected: the
 // panel of rank r starts at the point holding the (s·kc)-th accepted correspondence.  A scan over
@@ -4043,6 +4068,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
         }
     };
     const int n = f.n;
+    if (f.tk) f.tk[19] = __builtin_amdgcn_s_memrealtime();
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const float ms[3] = {s.mean[0], s.mean[1], s.mean[2]};
     const float md[3] = {s.mean[3], s.mean[4], s.mean[5]};
@@ -4268,14 +4294,12 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
     float sig = 0.0f;               // wave 0 lanes 0..8: sigma(a, b), the panels added in order
     if (tid == 0) s.bnd[0] = 0;
     __syncthreads();
+    if (f.tk) f.tk[18] = __builtin_amdgcn_s_memrealtime();
     for (int s0 = 0; s0 < S; s0 += kSliceGroup) {
         const int G = min(kSliceGroup, S - s0);
         const int R = 9 * G;                                      // fold chains of the group
-        const int stride = (((CAP / R) - 4) & ~7) + 4;            // row stride, ≡ 4 mod 8 floats
-        const int T = stride - 4;                                 // steps per chunk (a multiple of 8)
         const int FW = (R + 63) / 64;                             // fold waves (1 or 2)
         const int nF = WG - 64 * FW;                              // fillers
-        const float invT = 1.0f / (float)T;
         if (rejected) {
             auto accepted = [&](int i) {
                 float4 r0, r1;
@@ -4291,6 +4315,11 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
         };
         int maxlen = 0;
         for (int sl = 0; sl < G; ++sl) maxlen = max(maxlen, (s0 + sl + 1 >= S ? n : start(sl + 1)) - start(sl));
+        // chunks of T steps per panel row, double-buffered (one chunk over both buffers, for the
+        // 2k clouds' 4 panels, measured slower: its staging takes two round trips and hides nothing)
+        const int stride = (((CAP / R) - 4) & ~7) + 4;           // row stride, ≡ 4 mod 8 floats
+        const int T = stride - 4;                                 // steps per chunk (a multiple of 8)
+        const float invT = 1.0f / (float)T;
         const int nch = (maxlen + T - 1) / T;
         // the fillers' slots of chunk c: slot q = (panel sl, step t), q = sl * T + t
         const int per = (G * T + nF - 1) / nF;
@@ -4327,17 +4356,21 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
         const int L = tid;
         const int my_sl = L / 9;
         const int my_len = (wv < FW && L < R) ? ((s0 + my_sl + 1 >= S ? n : start(my_sl + 1)) - start(my_sl)) : 0;
+        if (f.tk && s0 == 0) f.tk[0] = __builtin_amdgcn_s_memrealtime();
         if (wv >= FW && nch > 0) fill(0);
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
+            if (f.tk && s0 == 0 && c < 2) f.tk[c == 0 ? 1 : 16] = __builtin_amdgcn_s_memrealtime();
             if (wv < FW) {
                 const int len = min(T, my_len - c * T);
                 if (L < R && len > 0) acc = fold_row(bufs(c) + L * stride, len, acc);
+                if (f.tk && s0 == 0 && c < 2) f.tk[15 + 2 * c] = __builtin_amdgcn_s_memrealtime();
             } else if (c + 1 < nch) {
                 fill(c + 1);
             }
         }
         __syncthreads();  // every chunk folded: the buffer of chunk nch (unused) takes the chains
+        if (f.tk && s0 == 0) f.tk[2] = __builtin_amdgcn_s_memrealtime();
         float* cs = bufs(nch);
         if (wv < FW && L < R) cs[L] = acc;
         __syncthreads();
@@ -4348,6 +4381,7 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
     }
     if (wave == 0 && lane < 9) s.sigmaf[lane] = sig;
     __syncthreads();
+    if (f.tk) f.tk[3] = __builtin_amdgcn_s_memrealtime();
 }
 
 // The update of pair p; returns the pair's work in the next pass (its misses in the fused test; 0
@@ -4511,11 +4545,29 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
     const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
     const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
     if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
-    const FoldIn fin{C, Xp, NT, n};
+    const FoldIn fin{C, Xp, NT, n, ticks ? w.ticks + 12 : nullptr};
     fold_pass_a<kWideWG, kWideChunkP, kWideRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
     if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
     fold_pass_b<kWideWG, kWideChunkP, kWideRow, true>(kp, fin, sh.buf, sh.s);
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
+#ifdef ICP4R_SOLVE_PROBE
+    // debug: the rotation of this sigma twice, back to back (ticks[5], [6]: durations) — a cold
+    // instruction cache shows as a first run much slower than the second
+    if (ticks) {
+        for (int rep = 0; rep < 2; ++rep) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            float z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            float sg[9], R[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sg[k] = sh.s.sigmaf[k] + z;
+            umeyama_rotation_f32_reg(sg, R);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) asm volatile("" ::"v"(R[k]));
+            w.ticks[5 + rep] = __builtin_amdgcn_s_memrealtime() - t0;
+        }
+    }
+#endif
     if (tid == 0) solve_pair<kNumericsPCL>(sh.s, st, kp);
     __syncthreads();
     if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
