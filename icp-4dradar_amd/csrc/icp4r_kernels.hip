@@ -3859,7 +3859,8 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     constexpr int kPerA = (CH + (WG - 128) - 1) / (WG - 128);
     // fill: load_a issues the loads of chunk c's records (clamped: at most kPerA per filler),
     // store_a turns them into the chain rows of LDS buffer c & 1.  (Loading two chunks ahead in two
-    // register sets was measured: no faster — pass A at 1024 pairs is not waiting on these loads.)
+    // register sets, here and in pass B, was measured slower: C3 update 176 -> 189 us per launch at two
+    // pair groups — the batched update is bound by its bytes, not by these loads' latency.)
     auto load_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {
         const int base = c * CH, len = min(CH, n - base), nf = WG - fill0;
 #pragma unroll
