@@ -19,9 +19,10 @@ against the oracle) are the TIMED run's, copied before any diagnostic rerun.
 
 Beside the headline: ``incl_upload`` (the same steps with each batch's H2D upload from pinned host
 memory inside the timed region, overlapped with the previous batch on a copy stream), ``gather``
-(the all-gather timed alone), ``roofline`` (the dominant kernel, the batched search, from the
-library's HIP events on its launch stream; ``traffic`` from the committed PMC passes of the same
-library build, matched by sha256), ``c1`` / ``c2`` / ``c5`` (BASELINE.json's single-pair configs:
+(the all-gather timed alone), ``roofline`` (the kernel with the larger share of the single-group
+step, the batched update since round 4, with the batched search beside it as ``nn_kernel``: SURVEY
+§8(d)'s algorithmic bytes over the library's HIP events on the launch stream; ``traffic`` from the
+committed PMC passes of the same library build, matched by sha256), ``c1`` / ``c2`` / ``c5`` (BASELINE.json's single-pair configs:
 2k/2k PCL defaults, 8k/8k 20 iterations, and the 8k-scan-vs-65k-map registration, one pair per call,
 each with its own roofline, oracle check and single-core CPU baseline) and ``cpu_baseline`` (the
 oracle — the C restatement of the reference CPU path — on one pinned core, with median / p90 per
