@@ -23,6 +23,10 @@
 #include "icp4r_host.hpp"
 #include "icp4r_internal.hpp"
 
+#ifndef ICP4R_FOLD_KEYS
+#define ICP4R_FOLD_KEYS 1  // multi-tile wide updates form their records in pass A (0: corr_kernel)
+#endif
+
 using namespace icp4r;
 
 namespace icp4r_host {
@@ -583,6 +587,10 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
     // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)
     const bool wide = pcl && !fuse && npairs <= ctx->ncu && opt(ctx, kOptWideUpdate, 1) != 0;
+    // ... which, on the multi-tile plan (the scan-to-map target), forms the correspondence records in
+    // its pass A instead of corr_kernel after every search (ICP4R_FOLD_KEYS=0 build: corr_kernel)
+    if (ICP4R_FOLD_KEYS && wide && pl.tile && !pl.lds && w.corr && (pl.chunks > 1 || !w.tile_own))
+        for (int g = 0; g < groups; ++g) wg[g].fold_keys = 1;
     char pass_name[48];
     for (int it = 0; it < iters; ++it) {
         snprintf(pass_name, sizeof(pass_name), "icp4r ICP pass %d", it + 1);

@@ -154,6 +154,9 @@ struct WorkArgs {
                           // (plan option tile_own = 0: the three-launch form, for A/B)
     int32_t defer_xform;  // 1: the update leaves X_i := T_inc X_i to the next pass's test kernel
     int32_t sums_tail;    // 1: the fused tail also folds the next pass A's Σs (eligible pairs: PairState)
+    int32_t fold_keys;    // 1 (multi-tile single pairs, wide update): no corr_kernel after the search — the
+                          // update's pass A forms the correspondence records from X and the merged keys'
+                          // targets and writes them for pass B
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |
                         // the query's sorted position << 14 (nt_pack)
     float4* sq;         // [npairs * x_stride] the pass's miss list in the order the test found them: a

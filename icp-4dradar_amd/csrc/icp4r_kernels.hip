@@ -3777,6 +3777,11 @@ struct FoldIn {
     const float4* NT;
     int n;
     uint64_t* tk = nullptr;  // debug (phase ticks, pair 0, thread 0): pass B's sub-phase stamps
+    // key mode (WorkArgs::fold_keys, pass A only; C, NT null): the NN of X_i is TG[key_idx(K[i])], and
+    // pass A writes the record pair corr_kernel would have written to Cw (pass B then reads them)
+    const NNKey* K = nullptr;
+    const float4* TG = nullptr;
+    float4* Cw = nullptr;
 };
 
 // A running exact sum of non-negative doubles that are widened floats: S in units of 2^E (E = the
@@ -3863,6 +3868,18 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
     // pair groups — the batched update is bound by its bytes, not by these loads' latency.)
     auto load_a = [&](int c, float4 (&r)[kPerA][2]) __attribute__((always_inline)) {
         const int base = c * CH, len = min(CH, n - base), nf = WG - fill0;
+        if (f.K) {  // key mode: X and the keys in flight together, then the targets they name
+            uint32_t ti[kPerA];
+#pragma unroll
+            for (int e = 0; e < kPerA; ++e) {
+                const int i = base + min(tid - fill0 + e * nf, len - 1);
+                r[e][0] = f.X[i];
+                ti[e] = (uint32_t)key_idx(f.K[i]);
+            }
+#pragma unroll
+            for (int e = 0; e < kPerA; ++e) r[e][1] = f.TG[ti[e]];
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < kPerA; ++e) {
             const int i = base + min(tid - fill0 + e * nf, len - 1);
@@ -3888,6 +3905,10 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
             }
             rec_fix(r[e][0], r[e][1]);
             const float d2 = r[e][1].w;
+            if (f.Cw) {  // corr_kernel's record pair: {s.xyz, w}, {d.xyz, d²}
+                f.Cw[2 * (base + o)] = r[e][0];
+                f.Cw[2 * (base + o) + 1] = r[e][1];
+            }
             const float sv[6] = {r[e][0].x, r[e][0].y, r[e][0].z, r[e][1].x, r[e][1].y, r[e][1].z};
             float v[6], wt = 0.0f, dd = 0.0f;
 #pragma unroll
@@ -4547,7 +4568,16 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
     const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
     if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
     const FoldIn fin{C, Xp, NT, n, ticks ? w.ticks + 12 : nullptr};
-    fold_pass_a<kWideWG, kWideChunkP, kWideRow>(kp, fin, sh.buf, sh.res, sh.cnt, sh.s);
+    // fold_keys: pass A reads X and the merged keys' targets and writes the records pass B reads
+    // (corr_kernel's work, without its launch)
+    FoldIn fa = fin;
+    if (w.fold_keys && C) {
+        fa.C = nullptr;
+        fa.K = w.nn_key + (int64_t)p * xs;
+        fa.TG = a.tgt + a.tgt_off[p];
+        fa.Cw = const_cast<float4*>(C);
+    }
+    fold_pass_a<kWideWG, kWideChunkP, kWideRow>(kp, fa, sh.buf, sh.res, sh.cnt, sh.s);
     if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
     fold_pass_b<kWideWG, kWideChunkP, kWideRow, true>(kp, fin, sh.buf, sh.s);
     if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
@@ -5301,7 +5331,7 @@ hipError_t launch_nn_tile(const PairArgs& a, const WorkArgs& w, int npairs, int 
     if (tile_start && (e = hipEventRecord(tile_start, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(nn_tile_kernel, grid, dim3(kLdsWG), 0, st, a, w, fitness_pass, own ? first : -1, qrun);
     if (tile_stop && (e = hipEventRecord(tile_stop, st)) != hipSuccess) return e;
-    if (!own && w.corr != nullptr && !fitness_pass)  // records from the merged keys
+    if (!own && w.corr != nullptr && !fitness_pass && !w.fold_keys)  // records from the merged keys
         hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
     return hipGetLastError();
 }
