@@ -23,10 +23,6 @@
 #include "icp4r_host.hpp"
 #include "icp4r_internal.hpp"
 
-#ifndef ICP4R_FOLD_KEYS
-#define ICP4R_FOLD_KEYS 1  // multi-tile wide updates form their records in pass A (0: corr_kernel)
-#endif
-
 using namespace icp4r;
 
 namespace icp4r_host {
@@ -108,7 +104,7 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad",
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
-    "gicp_cov_brute"};
+    "gicp_cov_brute", "fold_keys"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
     return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
@@ -588,8 +584,8 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)
     const bool wide = pcl && !fuse && npairs <= ctx->ncu && opt(ctx, kOptWideUpdate, 1) != 0;
     // ... which, on the multi-tile plan (the scan-to-map target), forms the correspondence records in
-    // its pass A instead of corr_kernel after every search (ICP4R_FOLD_KEYS=0 build: corr_kernel)
-    if (ICP4R_FOLD_KEYS && wide && pl.tile && !pl.lds && w.corr && (pl.chunks > 1 || !w.tile_own))
+    // its pass A instead of corr_kernel after every search (plan option fold_keys = 0: corr_kernel)
+    if (wide && pl.tile && !pl.lds && w.corr && (pl.chunks > 1 || !w.tile_own) && opt(ctx, kOptFoldKeys, 1) != 0)
         for (int g = 0; g < groups; ++g) wg[g].fold_keys = 1;
     char pass_name[48];
     for (int it = 0; it < iters; ++it) {
@@ -1097,7 +1093,7 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
         static const int32_t dflt[kNumPlanOpts] = {
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
-            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0};
+            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

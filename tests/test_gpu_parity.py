@@ -729,6 +729,33 @@ def test_c5_full_size_scan_to_map(gpu_ctx, oracle_mod, fixed):
     assert (al[:, :3].view(np.uint32) == o["aligned"][:, :3].view(np.uint32)).all()
 
 
+@pytest.mark.parametrize("huber", [False, True])
+def test_fold_keys_identical(gpu_ctx, oracle_mod, huber, plan):
+    """The multi-tile single pair (targets over one 8192-point tile: the scan-to-map call) with the
+    wide update forming the correspondence records in its pass A from X and the merged keys (plan
+    option fold_keys = 1, the default) or corr_kernel writing them after every search (fold_keys = 0):
+    bit-identical registrations (T, fitness, iterations, correspondences, the aligned cloud), PCL's
+    early stops live, unweighted and Huber-weighted, and bit-equal to the oracle."""
+    import icp4r
+
+    src, tgt = _pair(2300, 4096, 30001)
+    pl = icp4r.plan(1, len(src), len(tgt), ctx=gpu_ctx)
+    assert pl["pruned"] and not pl["lds"] and pl["wide_update"]
+    kw = dict(huber_delta=0.5) if huber else {}
+    p = icp4r.default_params(max_iterations=12, **kw)
+    out = {}
+    for fk in (0, 1):
+        plan(fold_keys=fk)
+        r, al = gpu_ctx.align(src, tgt, p, want_aligned=True)
+        out[fk] = (r.matrix().copy(), r.fitness, r.iterations, r.n_correspondences, r.status, al.copy())
+    a, b = out[0], out[1]
+    assert (a[0] == b[0]).all() and a[1:5] == b[1:5]
+    assert (a[5].view(np.uint32) == b[5].view(np.uint32)).all()
+    assert b[4] == 0
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, max_iterations=12, **kw)
+    assert (b[0] == o["T"]).all() and b[2] == o["iterations"] and b[1] == o["fitness"]
+
+
 @pytest.mark.parametrize("npairs", [1, 5, 40])
 def test_morton_multi_workgroup_identical(gpu_ctx, oracle_mod, npairs, plan):
     """Targets too large for the in-LDS kd build (the C5 submap class): their Morton sort on one
