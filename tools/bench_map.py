@@ -109,9 +109,14 @@ def main():
         t2 = time.perf_counter()
         tree.add_scan(scan, R, t)
         tree.sector_search_device(center, RADAR_RADIUS, heading, d_out.data_ptr(), d_cnt.data_ptr())
+        # the submap's size sizes the registration's plan (its tiles, index and workspace strides): read
+        # back once per frame, as the node's host loop would; sizing the plan for the whole map (the
+        # sector search's worst case) had launched ~1,200 mostly empty target tiles per NN pass
+        ctx.synchronize()  # (the search runs on the context's stream)
+        m_sub = int(d_cnt.item())
         batch = icp4r.Batch(src=src.data_ptr(), tgt=d_out.data_ptr(), src_off=zero.data_ptr(), src_n=sn.data_ptr(),
                             tgt_off=zero.data_ptr(), tgt_n=d_cnt.data_ptr(), npairs=1, max_src_n=len(scan),
-                            max_tgt_n=tree.size())
+                            max_tgt_n=m_sub)
         ctx.align_batch_device(batch, p, res.data_ptr(), None)
         ctx.synchronize()
         walls.append(time.perf_counter() - t2)
