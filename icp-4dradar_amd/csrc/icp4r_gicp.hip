@@ -314,9 +314,44 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
             }
             visit(sb, true);
         }
-    } else {  // large clouds (the scan-to-map submap): outward walk over every superblock
-        int up = sb0, dn = sb0 - 1;
-        for (int it = 0; it < nsb; ++it) visit((up < nsb && (dn < 0 || !(it & 1))) ? up++ : dn--, true);
+    } else {  // large clouds (the scan-to-map submap): the superblocks 64 at a time, groups outward from
+              // the own one — one lane-parallel coarse test per group with the bound reached so far, then
+              // only its survivors, in outward order (a scalar walk over every superblock had cost a box
+              // load and a test per superblock per wave: 512 of them per wave on the 65k map)
+        visit(sb0, false);
+        const v4f* sbv = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+        const int ng = (nsb + 63) / 64, g0 = sb0 / 64;
+        for (int d = 0; g0 - d >= 0 || g0 + d < ng; ++d) {
+            for (int side = 0; side < 2; ++side) {
+                const int g = side == 0 ? g0 + d : g0 - d;
+                if (g < 0 || g >= ng || (d == 0 && side == 1)) continue;
+                const int sl = min(g * 64 + lane, nsb - 1);
+                const uint64_t cm = __ballot(g * 64 + lane < nsb && g * 64 + lane != sb0 && maybe(sbv[2 * sl], sbv[2 * sl + 1]));
+                if (g > g0) {  // ascending from the group's start
+                    for (uint64_t m = cm; m; m &= m - 1) visit(g * 64 + __builtin_ctzll(m), true);
+                } else if (g < g0) {  // descending from its end
+                    for (uint64_t m = cm; m;) {
+                        const int b = 63 - __builtin_clzll(m);
+                        m &= ~(1ull << b);
+                        visit(g * 64 + b, true);
+                    }
+                } else {  // the own group: outward from sb0
+                    const int r0 = sb0 - g * 64;
+                    uint64_t um = r0 < 63 ? (cm >> (r0 + 1)) << (r0 + 1) : 0ull, dm = cm & ~um;
+                    for (bool upnext = true; um | dm; upnext = !upnext) {
+                        int b;
+                        if (um && (upnext || !dm)) {
+                            b = __builtin_ctzll(um);
+                            um &= um - 1;
+                        } else {
+                            b = 63 - __builtin_clzll(dm);
+                            dm &= ~(1ull << b);
+                        }
+                        visit(g * 64 + b, true);
+                    }
+                }
+            }
+        }
     }
     if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, 64));
     if (base + lane >= n) return;
