@@ -7,8 +7,10 @@
 //   covariances x 2                source and target (calculate_covariances): k-NN over each cloud's
 //                                  Morton index (pruned plans; the target's stays for the NN passes)
 //                                  or brute force
-//   repeat                         NN pass (exact 1-NN of X in the target) + gicp_iter_kernel
-//                                  (Mahalanobis, H / g, LM trials, x0 update, X := float(x0) src);
+//   repeat                         NN pass (exact 1-NN of X in the target) + the iteration's three
+//                                  kernels over slices of the source (Mahalanobis and H / g, the last
+//                                  slice solving the LM trials; the trials' errors, the last slice
+//                                  deciding x0; X := float(x0) src);
 //                                  every 4 iterations the host reads how many pairs still iterate
 //   fitness_prep + NN + finish     getFitnessScore and the results, as the ICP path
 //
@@ -82,7 +84,7 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     // and the batched search, which stages t_stride targets, only runs when those fit its LDS
     const int idx_both = max_n > max_m ? max_n : max_m;
     Plan pl = make_plan(ctx, npairs, mn, max_m, ICP4R_NN_AUTO, idx_both <= kLdsMaxTargets);
-    pl.cache = false;  // gicp_iter_kernel moves X without maintaining the cached-neighbour bounds
+    pl.cache = false;  // the iteration kernels move X without maintaining the cached-neighbour bounds
     WorkArgs w;
     int rc;
     const int idx_m = pl.pruned ? idx_both : max_m;
@@ -94,11 +96,19 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     HIP_TRY(ctx->gicp_cov_tgt.ensure((size_t)npairs * ts * 6 * sizeof(double)));
     HIP_TRY(ctx->gicp_mah.ensure((size_t)npairs * xs * 6 * sizeof(double)));
     HIP_TRY(ctx->gicp_active.ensure(sizeof(int32_t)));
+    const size_t lin_b = (size_t)npairs * kGicpMaxSlices * kGicpSys * sizeof(double);
+    const size_t err_b = (size_t)npairs * kGicpMaxSlices * kGicpSpec * sizeof(double);
+    const size_t cand_b = (size_t)npairs * sizeof(GicpCand);
+    HIP_TRY(ctx->gicp_part.ensure(lin_b + err_b + cand_b + (size_t)npairs * sizeof(int32_t)));
     GicpArgs g;
     g.gs = static_cast<GicpState*>(ctx->gicp_gs.p);
     g.cov_src = static_cast<const double*>(ctx->gicp_cov_src.p);
     g.cov_tgt = static_cast<const double*>(ctx->gicp_cov_tgt.p);
     g.mah = static_cast<double*>(ctx->gicp_mah.p);
+    g.part_lin = static_cast<double*>(ctx->gicp_part.p);
+    g.part_err = g.part_lin + lin_b / sizeof(double);
+    g.cand = reinterpret_cast<GicpCand*>(g.part_err + err_b / sizeof(double));
+    g.cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(g.cand) + cand_b);
     g.t_stride = ts;
     const float thr = (float)fmin(gp.max_correspondence_distance, (double)FLT_MAX);
     g.max_d2 = (double)(thr * thr);  // corr_dist_threshold_ * corr_dist_threshold_ (float)
@@ -107,12 +117,20 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     g.lm_init = gp.lm_init_lambda_factor;
     g.lm_max_iterations = gp.lm_max_iterations;
     g.max_iterations = gp.max_iterations;
+    // (plan option gicp_spec: trials per speculative pass; fewer only for the test that the one-by-one
+    // trials decide identically)
+    const int spec = opt(ctx, kOptGicpSpec, kGicpSpec);
+    g.spec = spec < 0 ? 0 : spec > kGicpSpec ? kGicpSpec : spec;
+    // (plan option gicp_grid: how many workgroups share the slices; the sums do not depend on it)
+    const int grid = opt(ctx, kOptGicpGrid, kGicpGrid);
+    g.grid = grid < 1 ? 1 : grid;
 
     EventPair* be;
     if ((rc = next_event(ctx->batch_events, ctx->batch_used, &be))) return rc;
     HIP_TRY(hipEventRecord(be->start, st));
     HIP_TRY(launch_init(a, w, npairs, st));
     HIP_TRY(launch_gicp_init(a.guess, g.gs, npairs, st));
+    HIP_TRY(hipMemsetAsync(g.cnt, 0, (size_t)npairs * sizeof(int32_t), st));
     // per-stage events only with icp4r_set_kernel_timing (each record between kernels costs device time)
     const bool kev = ctx->kernel_timing;
     EventPair* ce = nullptr;
@@ -139,7 +157,7 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
             if ((rc = next_event(ctx->upd_events, ctx->upd_used, &ue))) return rc;
             HIP_TRY(hipEventRecord(ue->start, st));
         }
-        HIP_TRY(launch_gicp_iter(a, w, g, npairs, it, st));
+        HIP_TRY(launch_gicp_iter(a, w, g, npairs, mn, it, st));
         if (kev) HIP_TRY(hipEventRecord(ue->stop, st));
         if ((it + 1) % kActiveCheck == 0 && it + 1 < gp.max_iterations) {
             int32_t h = 0;

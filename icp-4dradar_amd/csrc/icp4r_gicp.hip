@@ -360,9 +360,19 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
 }
 
 // ---- per-iteration update
-constexpr int kGicpWG = 1024;
-constexpr int kGicpWaves = kGicpWG / 64;
-constexpr int kGicpSys = 21 + 6 + 1 + 1;  // H (upper triangle), g, y, |valid|
+constexpr int kGicpSliceWG = 256;  // threads per slice workgroup; a slice is a multiple of it
+constexpr int kGicpSliceWaves = kGicpSliceWG / 64;
+
+// points per slice and slices of an n-point source: at least one slice (an empty source still
+// decides), at most kGicpMaxSlices, a slice a multiple of kGicpSliceWG points
+__host__ __device__ __forceinline__ int gicp_slice_pts(int n) {
+    const int m = (n + kGicpSliceWG * kGicpMaxSlices - 1) / (kGicpSliceWG * kGicpMaxSlices);
+    return kGicpSliceWG * (m > 1 ? m : 1);
+}
+__host__ __device__ __forceinline__ int gicp_slices(int n) {
+    const int s = (n + gicp_slice_pts(n) - 1) / gicp_slice_pts(n);
+    return s > 1 ? s : 1;
+}
 
 __device__ __forceinline__ void sym_unpack(const double* s, double* m) {
     m[0] = s[0]; m[1] = s[1]; m[2] = s[2];
@@ -392,30 +402,31 @@ __device__ void gicp_so3_exp(const double* w, double* R) {
     R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
 }
 
-// (A) x = b, A symmetric positive definite 6x6 (row-major), LDLᵀ without pivoting
-__device__ void gicp_ldlt6(const double* A, const double* b, double* x) {
-    double L[36], D[6], y[6];
-    for (int t = 0; t < 36; ++t) L[t] = 0.0;
+// (A) x = b, A symmetric positive definite 6x6 (row-major), LDLᵀ without pivoting; L overwrites A's
+// strict lower triangle (each A[i][j], i > j, is read once, just before L[i][j] replaces it: the same
+// operations in the same order as with a separate L, in a third of the registers — the separate 6x6
+// arrays beside the LM state had spilled the iteration kernel to scratch)
+__device__ void gicp_ldlt6(double (&A)[36], const double (&b)[6], double (&x)[6]) {
+    double D[6], y[6];
     for (int j = 0; j < 6; ++j) {
         double s = A[6 * j + j];
-        for (int k = 0; k < j; ++k) s -= L[6 * j + k] * L[6 * j + k] * D[k];
+        for (int k = 0; k < j; ++k) s -= A[6 * j + k] * A[6 * j + k] * D[k];
         D[j] = s;
-        L[6 * j + j] = 1.0;
         for (int i = j + 1; i < 6; ++i) {
             double t = A[6 * i + j];
-            for (int k = 0; k < j; ++k) t -= L[6 * i + k] * L[6 * j + k] * D[k];
-            L[6 * i + j] = D[j] != 0.0 ? t / D[j] : t;  // Eigen: a zero pivot leaves its column undivided
+            for (int k = 0; k < j; ++k) t -= A[6 * i + k] * A[6 * j + k] * D[k];
+            A[6 * i + j] = D[j] != 0.0 ? t / D[j] : t;  // Eigen: a zero pivot leaves its column undivided
         }
     }
     for (int i = 0; i < 6; ++i) {
         double s = b[i];
-        for (int k = 0; k < i; ++k) s -= L[6 * i + k] * y[k];
+        for (int k = 0; k < i; ++k) s -= A[6 * i + k] * y[k];
         y[i] = s;
     }
     for (int i = 0; i < 6; ++i) y[i] = fabs(D[i]) > DBL_MIN ? y[i] / D[i] : 0.0;  // Eigen's LDLT::solve
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int k = i + 1; k < 6; ++k) s -= L[6 * k + i] * x[k];
+        for (int k = i + 1; k < 6; ++k) s -= A[6 * k + i] * x[k];
         x[i] = s;
     }
 }
@@ -428,217 +439,423 @@ __device__ __forceinline__ bool gicp_converged(const double* R, const double* t,
     return m < 1.0;
 }
 
-struct GicpShared {
-    double red[kGicpWaves * kGicpSys];
-    double sys[kGicpSys];
-    double R[9], t[3];    // the transform the error pass evaluates
-    double dR[9], dt[3];  // the trial delta
-    int32_t stop;
-};
-
-// Σ eᵀMe (and with `lin` the system) over this thread's valid correspondences at transform (R, t).
+// the error eᵀMe of correspondence (a, b) at transform (R, t), and with LIN its terms of H = Σ JᵀMJ and
+// g = Σ JᵀMe (J = [skew(Ta), -I]) and the count, into acc (fast_gicp's linearize / compute_error)
 template <bool LIN>
-__device__ __forceinline__ void gicp_accumulate(const float4* src, const float4* tgt, const NNKey* key, const double* mah,
-                                                int n, double max_d2, const double* R, const double* t,
-                                                double (&acc)[kGicpSys]) {
-    for (int i = threadIdx.x; i < n; i += kGicpWG) {
-        const NNKey kk = key[i];
-        if (!((double)key_d2(kk) < max_d2)) continue;
-        const float4 sa = src[i], sb = tgt[key_idx(kk)];
-        const double a[3] = {sa.x, sa.y, sa.z};
-        double ta[3];
-        for (int r = 0; r < 3; ++r) ta[r] = R[3 * r] * a[0] + R[3 * r + 1] * a[1] + R[3 * r + 2] * a[2] + t[r];
-        const double e[3] = {(double)sb.x - ta[0], (double)sb.y - ta[1], (double)sb.z - ta[2]};
-        double M[9];
-        sym_unpack(mah + (int64_t)i * 6, M);
-        double Me[3];
-        for (int r = 0; r < 3; ++r) Me[r] = M[3 * r] * e[0] + M[3 * r + 1] * e[1] + M[3 * r + 2] * e[2];
-        acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
-        if (!LIN) continue;
-        acc[28] += 1.0;
-        // J = [skew(ta), -I]; H = JᵀMJ, g = JᵀMe
-        const double J[18] = {0.0, -ta[2], ta[1], -1.0, 0.0, 0.0,
-                              ta[2], 0.0, -ta[0], 0.0, -1.0, 0.0,
-                              -ta[1], ta[0], 0.0, 0.0, 0.0, -1.0};
-        double MJ[18];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 6; ++c) MJ[6 * r + c] = M[3 * r] * J[c] + M[3 * r + 1] * J[6 + c] + M[3 * r + 2] * J[12 + c];
-        int u = 0;
-        for (int r = 0; r < 6; ++r) {
-            for (int c = r; c < 6; ++c) acc[u++] += J[r] * MJ[c] + J[6 + r] * MJ[6 + c] + J[12 + r] * MJ[12 + c];
-            acc[21 + r] += J[r] * Me[0] + J[6 + r] * Me[1] + J[12 + r] * Me[2];
+__device__ __forceinline__ void gicp_point(const float4 sa, const float4 sb, const double (&M)[9], const double* R,
+                                           const double* t, double* acc) {
+    const double a[3] = {sa.x, sa.y, sa.z};
+    double ta[3];
+    for (int r = 0; r < 3; ++r) ta[r] = R[3 * r] * a[0] + R[3 * r + 1] * a[1] + R[3 * r + 2] * a[2] + t[r];
+    const double e[3] = {(double)sb.x - ta[0], (double)sb.y - ta[1], (double)sb.z - ta[2]};
+    double Me[3];
+    for (int r = 0; r < 3; ++r) Me[r] = M[3 * r] * e[0] + M[3 * r + 1] * e[1] + M[3 * r + 2] * e[2];
+    if (!LIN) {
+        acc[0] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+        return;
+    }
+    acc[27] += e[0] * Me[0] + e[1] * Me[1] + e[2] * Me[2];
+    acc[28] += 1.0;
+    // J = [skew(Ta), -I] (row k: J[k][0..2] = skew, J[k][3 + k] = -1). The terms with a zero or -1
+    // factor of J are left out or reduced to a negation: the same values as the generic JᵀMJ / JᵀMe
+    // sums (x + (+-0) = x), in half the operations.
+    auto js = [&](int k, int c) -> double {  // skew(Ta)[k][c], k != c
+        return k == 0 ? (c == 1 ? -ta[2] : ta[1]) : k == 1 ? (c == 0 ? ta[2] : -ta[0]) : (c == 0 ? -ta[1] : ta[0]);
+    };
+    double MS[9];  // M skew(Ta)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const int k0 = c == 0 ? 1 : 0, k1 = c == 2 ? 1 : 2;
+            MS[3 * r + c] = M[3 * r + k0] * js(k0, c) + M[3 * r + k1] * js(k1, c);
         }
+    int u = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int k0 = r == 0 ? 1 : 0, k1 = r == 2 ? 1 : 2;  // the rows k != r of column r of J
+#pragma unroll
+        for (int c = r; c < 3; ++c) acc[u++] += js(k0, r) * MS[3 * k0 + c] + js(k1, r) * MS[3 * k1 + c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[u++] += js(k0, r) * -M[3 * k0 + c] + js(k1, r) * -M[3 * k1 + c];
+        acc[21 + r] += js(k0, r) * Me[k0] + js(k1, r) * Me[k1];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = r; c < 3; ++c) acc[u++] += M[3 * r + c];
+        acc[24 + r] += -Me[r];
     }
 }
 
-__device__ __forceinline__ void gicp_block_sum(double (&v)[kGicpSys], GicpShared& sh) {
+// Σ over the workgroup of each v[k] in a fixed order (butterfly per wave, then the waves in order);
+// the sum of v[k] is returned to thread k < NV. red: kGicpSliceWaves * NV doubles of LDS.
+template <int NV>
+__device__ __forceinline__ double gicp_slice_sum(double (&v)[NV], double* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < kGicpSys; ++k) {
+    for (int k = 0; k < NV; ++k) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
     }
     if (lane == 0)
-        for (int k = 0; k < kGicpSys; ++k) sh.red[wave * kGicpSys + k] = v[k];
+        for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
     __syncthreads();
-    if (threadIdx.x < kGicpSys) {
-        double t = 0.0;
-        for (int w = 0; w < kGicpWaves; ++w) t += sh.red[w * kGicpSys + threadIdx.x];
-        sh.sys[threadIdx.x] = t;
-    }
-    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x < NV)
+        for (int q = 0; q < kGicpSliceWaves; ++q) r += red[q * NV + threadIdx.x];
+    __syncthreads();  // red is free again
+    return r;
 }
 
-__global__ __launch_bounds__(kGicpWG) void gicp_iter_kernel(PairArgs a, WorkArgs w, GicpArgs g, int it) {
-    __shared__ GicpShared sh;
-    const int p = blockIdx.x;
-    PairState& st = w.state[p];
-    if (st.phase != kPhaseActive) return;
-    GicpState& gs = g.gs[p];
-    const int n = a.src_n[p];
-    const float4* src = a.src + a.src_off[p];
-    const float4* tgt = a.tgt + a.tgt_off[p];
-    const NNKey* key = w.nn_key + (int64_t)p * w.x_stride;
-    double* mah = g.mah + (int64_t)p * w.x_stride * 6;
+// The same for the 29 sums of the linearisation, as a transposing reduction: at each step a lane keeps
+// half of its values and adds its partner's copy of that half (one shuffle per kept value), so the 32
+// padded values take 16 + 8 + 4 + 2 + 1 + 1 shuffles instead of 29 x 6; lanes 2k and 2k + 1 end with
+// the wave's sum of value k (another fixed order than the butterfly's). In place in v.
+__device__ __forceinline__ double gicp_slice_sum_sys(double (&v)[kGicpSys], double* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    {
+        const bool hi = lane & 32;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const double lo_v = v[k], hi_v = k + 16 < kGicpSys ? v[k + 16] : 0.0;
+            v[k] = (hi ? hi_v : lo_v) + __shfl_xor(hi ? lo_v : hi_v, 32, 64);
+        }
+    }
+#pragma unroll
+    for (int h = 8, o = 16; h >= 1; h >>= 1, o >>= 1) {
+        const bool hi = lane & o;
+#pragma unroll
+        for (int k = 0; k < h; ++k) {
+            const double a = v[k], b = v[k + h];
+            v[k] = (hi ? b : a) + __shfl_xor(hi ? a : b, o, 64);
+        }
+    }
+    const double r1 = v[0] + __shfl_xor(v[0], 1, 64);
+    const int k = lane >> 1;  // the value this lane pair holds
+    if (!(lane & 1) && k < kGicpSys) red[wave * kGicpSys + k] = r1;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x < kGicpSys)
+        for (int q = 0; q < kGicpSliceWaves; ++q) r += red[q * kGicpSys + threadIdx.x];
+    __syncthreads();
+    return r;
+}
+
+// the LM trial of damping lambda from the system sys at x0 = (R0, t0): delta from (H + λI) d = -g,
+// the trial transform delta * x0 (fast_gicp LsqRegistration::step_lm)
+__device__ void gicp_make_trial(const double* sys, double lambda, const double* R0, const double* t0, GicpTrial& o) {
+    double A[36], nb[6];
+    int u = 0;
+    for (int r = 0; r < 6; ++r)
+        for (int c = r; c < 6; ++c) A[6 * r + c] = A[6 * c + r] = sys[u++];
+    for (int k = 0; k < 6; ++k) A[7 * k] += lambda;
+    for (int k = 0; k < 6; ++k) nb[k] = -sys[21 + k];
+    double d[6];
+    gicp_ldlt6(A, nb, d);
+    for (int k = 0; k < 6; ++k) o.d[k] = d[k];
+    gicp_so3_exp(d, o.dR);
+    o.dt[0] = d[3];
+    o.dt[1] = d[4];
+    o.dt[2] = d[5];
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) o.R[3 * r + c] = o.dR[3 * r] * R0[c] + o.dR[3 * r + 1] * R0[3 + c] + o.dR[3 * r + 2] * R0[6 + c];
+        o.t[r] = o.dR[3 * r] * t0[0] + o.dR[3 * r + 1] * t0[1] + o.dR[3 * r + 2] * t0[2] + o.dt[r];
+    }
+    o.lambda = lambda;
+}
+
+struct GicpPairView {
+    int n, ps, ns;  // points, points per slice, slices
+    const float4 *src, *tgt;
+    const NNKey* key;
+    double* mah;
+};
+
+__device__ __forceinline__ GicpPairView gicp_view(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int p) {
+    GicpPairView v;
+    v.n = a.src_n[p];
+    v.ps = gicp_slice_pts(v.n);
+    v.ns = gicp_slices(v.n);
+    v.src = a.src + a.src_off[p];
+    v.tgt = a.tgt + a.tgt_off[p];
+    v.key = w.nn_key + (int64_t)p * w.x_stride;
+    v.mah = g.mah + (int64_t)p * w.x_stride * 6;
+    return v;
+}
+
+// Workgroup j of a pair takes its slices j, j + W, j + 2W, ... (W workgroups per pair, fewer for many pairs:
+// the slicing, and so every sum, depends on n only; W only spreads the slices over the chip).
+// The per-slice sums of one pair reach the workgroup that finishes last (the counter form of the
+// hand-off in cdna_hip_programming.md §6 Guideline 16, with write-through sum stores, gicp_publish,
+// in place of a release fence in every workgroup): every workgroup waits for its stores and draws a
+// ticket; the one drawing nw - 1 acquires, resets the counter for the next launch and returns true
+// (in all its threads).
+// This block's pair and its index j < W among the pair's workgroups: the W workgroups of a pair on one
+// XCD, as blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one), so a pair's
+// gathered target data is fetched into one L2, not eight (a speed choice only: nothing depends on it)
+__device__ __forceinline__ bool gicp_block(int npairs, int W, int& p, int& j) {
+    const int b = blockIdx.x, x = b & 7, r = b >> 3;
+    p = (r / W) * 8 + x;
+    j = r % W;
+    return p < npairs;
+}
+
+__device__ __forceinline__ void gicp_publish(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool gicp_last_slice(int32_t* cnt, int nw, int32_t* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == nw - 1;
+        if (last) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
+// (1) update_correspondences + linearize over one slice: M_i = (C_B + R C_A Rᵀ)⁻¹ of every valid
+// correspondence (kept for the trials) and the slice's sums of H, g, y, |valid| at x0. The last slice
+// sums the slices in order and solves the first LM trials (step_lm's (H + λI) d = -g, λ, 2λ, 8λ, ...).
+__global__ __launch_bounds__(kGicpSliceWG) void gicp_lin_kernel(PairArgs a, WorkArgs w, GicpArgs g, int npairs, int W) {
+    __shared__ double red[kGicpSliceWaves * kGicpSys];
+    __shared__ int32_t last;
+    int p, j;
+    if (!gicp_block(npairs, W, p, j)) return;
+    if (w.state[p].phase != kPhaseActive) return;
+    const GicpPairView v = gicp_view(a, w, g, p);
+    if (j >= v.ns) return;
+    const int nw = min(W, v.ns);
     const double* cs = g.cov_src + (int64_t)p * w.x_stride * 6;
     const double* ct = g.cov_tgt + (int64_t)p * g.t_stride * 6;
+    const GicpState& gs = g.gs[p];
     double R[9], t[3];
     for (int k = 0; k < 9; ++k) R[k] = gs.R[k];
     for (int k = 0; k < 3; ++k) t[k] = gs.t[k];
-    // update_correspondences: Mahalanobis of every valid correspondence
-    for (int i = threadIdx.x; i < n; i += kGicpWG) {
-        const NNKey kk = key[i];
-        if (!((double)key_d2(kk) < g.max_d2)) continue;
-        double CA[9], CB[9], RC[9], RCR[9], Mi[9];
-        sym_unpack(cs + (int64_t)i * 6, CA);
-        sym_unpack(ct + (int64_t)key_idx(kk) * 6, CB);
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) RC[3 * r + c] = R[3 * r] * CA[c] + R[3 * r + 1] * CA[3 + c] + R[3 * r + 2] * CA[6 + c];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c)
-                RCR[3 * r + c] = CB[3 * r + c] + (RC[3 * r] * R[3 * c] + RC[3 * r + 1] * R[3 * c + 1] + RC[3 * r + 2] * R[3 * c + 2]);
-        gicp_inv3(RCR, Mi);
-        double* o = mah + (int64_t)i * 6;
-        o[0] = Mi[0];
-        o[1] = Mi[1];
-        o[2] = Mi[2];
-        o[3] = Mi[4];
-        o[4] = Mi[5];
-        o[5] = Mi[8];
-    }
-    __syncthreads();  // workgroup-scope visibility of the Mahalanobis array
-    double acc[kGicpSys];
-    for (int k = 0; k < kGicpSys; ++k) acc[k] = 0.0;
-    gicp_accumulate<true>(src, tgt, key, mah, n, g.max_d2, R, t, acc);
-    gicp_block_sum(acc, sh);
-    // step_lm
-    double H[36], gv[6], y0 = 0.0, lambda = 0.0, nu = 2.0;
-    if (threadIdx.x == 0) {
-        int u = 0;
-        for (int r = 0; r < 6; ++r)
-            for (int c = r; c < 6; ++c) H[6 * r + c] = H[6 * c + r] = sh.sys[u++];
-        for (int r = 0; r < 6; ++r) gv[r] = sh.sys[21 + r];
-        y0 = sh.sys[27];
-        lambda = gs.lambda;
-        if (lambda < 0.0) {
-            double mx = 0.0;
-            for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(H[7 * k]));
-            lambda = g.lm_init * mx;
-        }
-        st.ncorr = (int)sh.sys[28];
-    }
-    int outcome = 0;  // 1 accepted, 2 converged on a rejected step, 0 failed
-    double d[6];
-    for (int trial = 0; trial < g.lm_max_iterations; ++trial) {
-        if (threadIdx.x == 0) {
-            double A[36], nb[6];
-            for (int k = 0; k < 36; ++k) A[k] = H[k];
-            for (int k = 0; k < 6; ++k) A[7 * k] += lambda;
-            for (int k = 0; k < 6; ++k) nb[k] = -gv[k];
-            gicp_ldlt6(A, nb, d);
-            gicp_so3_exp(d, sh.dR);
-            sh.dt[0] = d[3];
-            sh.dt[1] = d[4];
-            sh.dt[2] = d[5];
-            // xi = delta * x0
-            for (int r = 0; r < 3; ++r) {
-                for (int c = 0; c < 3; ++c)
-                    sh.R[3 * r + c] = sh.dR[3 * r] * R[c] + sh.dR[3 * r + 1] * R[3 + c] + sh.dR[3 * r + 2] * R[6 + c];
-                sh.t[r] = sh.dR[3 * r] * t[0] + sh.dR[3 * r + 1] * t[1] + sh.dR[3 * r + 2] * t[2] + sh.dt[r];
-            }
-        }
-        __syncthreads();
-        double ri[9], ti[3];
-        for (int k = 0; k < 9; ++k) ri[k] = sh.R[k];
-        for (int k = 0; k < 3; ++k) ti[k] = sh.t[k];
+    double* part = g.part_lin + (int64_t)p * kGicpMaxSlices * kGicpSys;
+    for (int q = j; q < v.ns; q += W) {
+        double acc[kGicpSys];
         for (int k = 0; k < kGicpSys; ++k) acc[k] = 0.0;
-        gicp_accumulate<false>(src, tgt, key, mah, n, g.max_d2, ri, ti, acc);
-        gicp_block_sum(acc, sh);
-        if (threadIdx.x == 0) {
-            const double yi = sh.sys[27];
-            double den = 0.0;
-            for (int k = 0; k < 6; ++k) den += d[k] * (lambda * d[k] - gv[k]);
-            const double rho = (y0 - yi) / den;
-            sh.stop = 0;
-            if (rho < 0) {
-                if (gicp_converged(sh.dR, sh.dt, g.rot_eps, g.trans_eps)) {
-                    sh.stop = 2;
-                } else {
-                    lambda = nu * lambda;
-                    nu = 2 * nu;
-                }
-            } else {
-                for (int k = 0; k < 9; ++k) R[k] = sh.R[k];
-                for (int k = 0; k < 3; ++k) t[k] = sh.t[k];
-                lambda = lambda * fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
-                sh.stop = 1;
-            }
+        const int hi = min(v.n, (q + 1) * v.ps);
+        for (int i = q * v.ps + threadIdx.x; i < hi; i += kGicpSliceWG) {
+            const NNKey kk = v.key[i];
+            if (!((double)key_d2(kk) < g.max_d2)) continue;
+            const int j = key_idx(kk);
+            double CA[9], CB[9], RC[9], RCR[9], Mi[9];
+            sym_unpack(cs + (int64_t)i * 6, CA);
+            sym_unpack(ct + (int64_t)j * 6, CB);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) RC[3 * r + c] = R[3 * r] * CA[c] + R[3 * r + 1] * CA[3 + c] + R[3 * r + 2] * CA[6 + c];
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    RCR[3 * r + c] = CB[3 * r + c] + (RC[3 * r] * R[3 * c] + RC[3 * r + 1] * R[3 * c + 1] + RC[3 * r + 2] * R[3 * c + 2]);
+            gicp_inv3(RCR, Mi);
+            const double m6[6] = {Mi[0], Mi[1], Mi[2], Mi[4], Mi[5], Mi[8]};
+            double* o = v.mah + (int64_t)i * 6;
+            for (int k = 0; k < 6; ++k) o[k] = m6[k];
+            double M[9];
+            sym_unpack(m6, M);
+            gicp_point<true>(v.src[i], v.tgt[j], M, R, t, acc);
         }
-        __syncthreads();
-        outcome = sh.stop;
-        __syncthreads();  // every thread read sh.stop before the next trial rewrites it
-        if (outcome) break;
+        const double r = gicp_slice_sum_sys(acc, red);
+        if (threadIdx.x < kGicpSys) gicp_publish(part + q * kGicpSys + threadIdx.x, r);
     }
-    if (threadIdx.x == 0) {
-        st.iterations = it;  // nr_iterations_ = i
-        gs.lambda = lambda;
-        for (int k = 0; k < 9; ++k) gs.R[k] = R[k];
-        for (int k = 0; k < 3; ++k) gs.t[k] = t[k];
-        // final_transformation_ = x0.cast<float>() (column-major)
-        for (int r = 0; r < 3; ++r) {
-            for (int c = 0; c < 3; ++c) st.final_T[4 * c + r] = (float)R[3 * r + c];
-            st.final_T[12 + r] = (float)t[r];
-            st.final_T[4 * r + 3] = 0.0f;
-        }
-        st.final_T[15] = 1.0f;
-        if (!outcome) {
-            st.phase = kPhaseFailed;  // step_lm returned false: "lm not converged!!", break
-        } else if (gicp_converged(sh.dR, sh.dt, g.rot_eps, g.trans_eps)) {
-            st.phase = kPhaseConverged;
-            st.conv_state = 2;
-        } else if (it + 1 >= g.max_iterations) {
-            st.conv_state = 1;
-        }
-        for (int k = 0; k < 9; ++k) sh.R[k] = R[k];
-        for (int k = 0; k < 3; ++k) sh.t[k] = t[k];
+    if (!gicp_last_slice(g.cnt + p, nw, &last)) return;
+    double* sys = red;  // (free again)
+    if (threadIdx.x < kGicpSys) {
+        double t = 0.0;
+        for (int q = 0; q < v.ns; ++q) t += part[q * kGicpSys + threadIdx.x];
+        sys[threadIdx.x] = t;
     }
     __syncthreads();
+    GicpCand& gc = g.cand[p];
+    const int nt = min(g.spec, g.lm_max_iterations);
+    if (threadIdx.x < nt) {
+        const int k = threadIdx.x;
+        double lambda = gs.lambda, nu = 2.0;
+        if (lambda < 0.0) {
+            double mx = 0.0;
+            const int diag[6] = {0, 6, 11, 15, 18, 20};  // (r, r) in the packed upper triangle
+            for (int q = 0; q < 6; ++q) mx = fmax(mx, fabs(sys[diag[q]]));
+            lambda = g.lm_init * mx;
+        }
+        for (int q = 0; q < k; ++q) {
+            lambda = nu * lambda;
+            nu = 2 * nu;
+        }
+        GicpTrial tr;
+        gicp_make_trial(sys, lambda, R, t, tr);
+        gc.c[k] = tr;
+    }
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + kGicpSys) gc.sys[threadIdx.x - 64] = sys[threadIdx.x - 64];
+    if (threadIdx.x >= 128 && threadIdx.x < 140) {
+        const int q = threadIdx.x - 128;
+        if (q < 9) gc.R0[q] = R[q];
+        else gc.t0[q - 9] = t[q - 9];
+    }
+}
+
+// (2) the trials' errors over one slice. The last slice sums them in order and decides (accept, converge
+// on a rejected step, or raise λ); in the rare case every speculative trial was rejected it runs the
+// further trials one by one over all slices, each summed slice by slice exactly as above; then it
+// writes x0, λ and the pair's state.
+__global__ __launch_bounds__(kGicpSliceWG) void gicp_trial_kernel(PairArgs a, WorkArgs w, GicpArgs g, int npairs, int W, int it) {
+    __shared__ double red[kGicpSliceWaves * kGicpSpec];
+    __shared__ double pose[kGicpSpec][12];
+    __shared__ double err[kGicpSpec];
+    __shared__ double x0[12];   // the transform after this iteration
+    __shared__ GicpTrial cur;   // the last trial decided on
+    __shared__ double lam, nuv;
+    __shared__ int32_t stop;    // 1 accepted, 2 converged on a rejected step, 0 none yet
+    __shared__ int32_t last;
+    int p, j;
+    if (!gicp_block(npairs, W, p, j)) return;
+    PairState& st = w.state[p];
     if (st.phase != kPhaseActive) return;
-    // X := trans.cast<float>() * src for the next NN pass (float, Eigen's order)
+    const GicpPairView v = gicp_view(a, w, g, p);
+    const int ns = v.ns;
+    if (j >= ns) return;
+    const int nw = min(W, ns);
+    const int nt = min(g.spec, g.lm_max_iterations);
+    const GicpCand& gc = g.cand[p];
+    if (threadIdx.x < nt * 12) {
+        const int k = threadIdx.x / 12, q = threadIdx.x % 12;
+        pose[k][q] = q < 9 ? gc.c[k].R[q] : gc.c[k].t[q - 9];
+    }
+    __syncthreads();
+    {
+        double* part = g.part_err + (int64_t)p * kGicpMaxSlices * kGicpSpec;
+        for (int q = j; q < ns; q += W) {
+            double acc[kGicpSpec];
+            for (int k = 0; k < kGicpSpec; ++k) acc[k] = 0.0;
+            const int hi = min(v.n, (q + 1) * v.ps);
+            for (int i = q * v.ps + threadIdx.x; i < hi; i += kGicpSliceWG) {
+                const NNKey kk = v.key[i];
+                if (!((double)key_d2(kk) < g.max_d2)) continue;
+                const float4 sa = v.src[i], sb = v.tgt[key_idx(kk)];
+                double M[9];
+                sym_unpack(v.mah + (int64_t)i * 6, M);
+                for (int k = 0; k < nt; ++k) gicp_point<false>(sa, sb, M, pose[k], pose[k] + 9, acc + k);
+            }
+            const double r = gicp_slice_sum(acc, red);
+            if (threadIdx.x < kGicpSpec) gicp_publish(part + q * kGicpSpec + threadIdx.x, r);
+        }
+        if (!gicp_last_slice(g.cnt + p, nw, &last)) return;
+        if (threadIdx.x < nt) {
+            double t = 0.0;
+            for (int q = 0; q < ns; ++q) t += part[q * kGicpSpec + threadIdx.x];
+            err[threadIdx.x] = t;
+        }
+    }
+    __syncthreads();
+    const double y0 = gc.sys[27];
+    // rho = (y0 - yi) / dᵀ(λd - g)
+    auto decide = [&](double yi) {
+        const double lambda = cur.lambda;
+        double den = 0.0;
+        for (int k = 0; k < 6; ++k) den += cur.d[k] * (lambda * cur.d[k] - gc.sys[21 + k]);
+        const double rho = (y0 - yi) / den;
+        if (rho < 0) {
+            if (gicp_converged(cur.dR, cur.dt, g.rot_eps, g.trans_eps)) {
+                stop = 2;
+            } else {
+                lam = nuv * lambda;
+                nuv = 2 * nuv;
+            }
+        } else {
+            for (int k = 0; k < 9; ++k) x0[k] = cur.R[k];
+            for (int k = 0; k < 3; ++k) x0[9 + k] = cur.t[k];
+            lam = lambda * fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
+            stop = 1;
+        }
+    };
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 9; ++k) x0[k] = gc.R0[k];
+        for (int k = 0; k < 3; ++k) x0[9 + k] = gc.t0[k];
+        stop = 0;
+        nuv = 2.0;
+        lam = nt > 0 ? gc.c[0].lambda : 0.0;
+        for (int k = 0; k < nt && !stop; ++k) {
+            cur = gc.c[k];
+            decide(err[k]);
+        }
+    }
+    __syncthreads();
+    for (int k = nt; k < g.lm_max_iterations; ++k) {
+        if (stop) break;
+        __syncthreads();  // every thread read stop
+        if (threadIdx.x == 0) gicp_make_trial(gc.sys, lam, gc.R0, gc.t0, cur);
+        __syncthreads();
+        double tot = 0.0;
+        for (int q = 0; q < ns; ++q) {
+            double e[1] = {0.0};
+            const int hi = min(v.n, (q + 1) * v.ps);
+            for (int i = q * v.ps + threadIdx.x; i < hi; i += kGicpSliceWG) {
+                const NNKey kk = v.key[i];
+                if (!((double)key_d2(kk) < g.max_d2)) continue;
+                double M[9];
+                sym_unpack(v.mah + (int64_t)i * 6, M);
+                gicp_point<false>(v.src[i], v.tgt[key_idx(kk)], M, cur.R, cur.t, e);
+            }
+            tot += gicp_slice_sum(e, red);
+        }
+        if (threadIdx.x == 0) decide(tot);
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    GicpState& gs = g.gs[p];
+    st.ncorr = (int)gc.sys[28];
+    st.iterations = it;  // nr_iterations_ = i
+    gs.lambda = lam;
+    for (int k = 0; k < 9; ++k) gs.R[k] = x0[k];
+    for (int k = 0; k < 3; ++k) gs.t[k] = x0[9 + k];
+    // final_transformation_ = x0.cast<float>() (column-major)
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) st.final_T[4 * c + r] = (float)x0[3 * r + c];
+        st.final_T[12 + r] = (float)x0[9 + r];
+        st.final_T[4 * r + 3] = 0.0f;
+    }
+    st.final_T[15] = 1.0f;
+    if (!stop) {
+        st.phase = kPhaseFailed;  // step_lm returned false: "lm not converged!!", break
+    } else if (gicp_converged(cur.dR, cur.dt, g.rot_eps, g.trans_eps)) {
+        st.phase = kPhaseConverged;
+        st.conv_state = 2;
+    } else if (it + 1 >= g.max_iterations) {
+        st.conv_state = 1;
+    }
+}
+
+// (3) X := trans.cast<float>() * src over one slice for the next NN pass (float, Eigen's order), for the
+// pairs still iterating
+__global__ __launch_bounds__(kGicpSliceWG) void gicp_move_kernel(PairArgs a, WorkArgs w, GicpArgs g, int npairs, int W) {
+    int p, j;
+    if (!gicp_block(npairs, W, p, j)) return;
+    if (w.state[p].phase != kPhaseActive) return;
+    const GicpPairView v = gicp_view(a, w, g, p);
+    const GicpState& gs = g.gs[p];
     float Rf[9], tf[3];
-    for (int k = 0; k < 9; ++k) Rf[k] = (float)sh.R[k];
-    for (int k = 0; k < 3; ++k) tf[k] = (float)sh.t[k];
+    for (int k = 0; k < 9; ++k) Rf[k] = (float)gs.R[k];
+    for (int k = 0; k < 3; ++k) tf[k] = (float)gs.t[k];
     float4* X = w.X + (int64_t)p * w.x_stride;
-    for (int i = threadIdx.x; i < n; i += kGicpWG) {
-        const float4 s = src[i];
+    for (int i = j * kGicpSliceWG + threadIdx.x; i < v.n; i += W * kGicpSliceWG) {
+        const float4 sp = v.src[i];
         float o[3];
         for (int r = 0; r < 3; ++r) {
-            float v = Rf[3 * r] * s.x;
-            v = v + Rf[3 * r + 1] * s.y;
-            v = v + Rf[3 * r + 2] * s.z;
-            o[r] = v + tf[r];
+            float x = Rf[3 * r] * sp.x;
+            x = x + Rf[3 * r + 1] * sp.y;
+            x = x + Rf[3 * r + 2] * sp.z;
+            o[r] = x + tf[r];
         }
-        X[i] = make_float4(o[0], o[1], o[2], s.w);
+        X[i] = make_float4(o[0], o[1], o[2], sp.w);
     }
 }
 
@@ -718,9 +935,17 @@ hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const in
     return hipGetLastError();
 }
 
-hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int it,
+hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st) {
-    hipLaunchKernelGGL(gicp_iter_kernel, dim3(npairs), dim3(kGicpWG), 0, st, a, w, g, it);
+    if (npairs <= 0) return hipSuccess;
+    // about g.grid workgroups in all (a single pair: one per slice)
+    const int ns = gicp_slices(max_n);
+    const int per = g.grid / npairs;
+    const int W = per < 1 ? 1 : per > ns ? ns : per;
+    const dim3 grid((unsigned)W * ((npairs + 7) / 8 * 8)), block(kGicpSliceWG);
+    hipLaunchKernelGGL(gicp_lin_kernel, grid, block, 0, st, a, w, g, npairs, W);
+    hipLaunchKernelGGL(gicp_trial_kernel, grid, block, 0, st, a, w, g, npairs, W, it);
+    hipLaunchKernelGGL(gicp_move_kernel, grid, block, 0, st, a, w, g, npairs, W);
     return hipGetLastError();
 }
 

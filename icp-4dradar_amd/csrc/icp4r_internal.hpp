@@ -262,8 +262,31 @@ struct GicpState {
     double R[9], t[3];  // x0 (row-major rotation, translation)
     double lambda;      // lm_lambda_ (< 0: not yet initialised)
 };
+// One iteration runs as three kernels over slices of each pair's source points (gicp_slices(n), a
+// function of n only, so a pair's sums do not depend on the batch around it): the linearisation (its
+// last slice solves the first kGicpSpec Levenberg-Marquardt trials), the trials' errors (its last
+// slice decides), and the move of X.
+constexpr int kGicpSys = 21 + 6 + 1 + 1;  // H (upper triangle), g, y, |valid|
+constexpr int kGicpSpec = 2;             // LM trials evaluated per pass (the rest, rarely needed, one by one)
+constexpr int kGicpMaxSlices = 64;
+constexpr int kGicpGrid = 2048;          // workgroups per iteration kernel, about (a pair: at most its slices)
+struct GicpTrial {
+    double R[9], t[3];    // the trial transform delta * x0
+    double dR[9], dt[3];  // delta
+    double d[6];          // the LDLT step
+    double lambda;
+};
+struct GicpCand {  // written by the linearisation's last slice, read by the trial kernel
+    GicpTrial c[kGicpSpec];
+    double sys[kGicpSys];  // H, g, y0, |valid| at x0
+    double R0[9], t0[3];   // x0
+};
 struct GicpArgs {
     GicpState* gs;        // [npairs]
+    GicpCand* cand;       // [npairs]
+    double* part_lin;     // [npairs][kGicpMaxSlices][kGicpSys] per-slice linearisation sums
+    double* part_err;     // [npairs][kGicpMaxSlices][kGicpSpec] per-slice trial errors
+    int32_t* cnt;         // [npairs] slices arrived (zero between launches)
     const double* cov_src;  // [npairs * x_stride * 6] regularised source covariances (upper triangle)
     const double* cov_tgt;  // [npairs * t_stride * 6]
     double* mah;          // [npairs * x_stride * 6] Mahalanobis of the current correspondences
@@ -271,6 +294,8 @@ struct GicpArgs {
     double max_d2;        // corr_dist_threshold_² (float) as double
     double rot_eps, trans_eps, lm_init;
     int32_t lm_max_iterations, max_iterations;
+    int32_t spec;         // LM trials evaluated speculatively, 0..kGicpSpec (plan option gicp_spec)
+    int32_t grid;         // workgroups per iteration kernel, about (plan option gicp_grid)
 };
 hipError_t launch_gicp_init(const float* guess, GicpState* gs, int npairs, hipStream_t st);
 hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, int npairs, int max_n,
@@ -279,7 +304,7 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
 hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
                                int npairs, int max_n, int64_t stride, int k, int reg, double* cov, hipStream_t st);
 hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s);
-hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int it,
+hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st);
 
 }  // namespace icp4r

@@ -209,6 +209,41 @@ def test_gpu_small_clouds_fewer_points_than_k(gpu_ctx, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_gpu_lm_trials_speculative_equals_one_by_one(gpu_ctx, oracle_mod, plan):
+    """The iteration evaluates its first LM trials together (plan option gicp_spec, default 2) and any
+    further trial one by one, each summed slice by slice in the same order: every gicp_spec gives
+    bit-identical results, and so does every spread of the slices over workgroups (gicp_grid). Cases: far initial poses (rejected trials), lm_max_iterations = 1 and 0,
+    and a source of 17k points (512-point slices)."""
+    gicp = _gicp()
+    cases = []
+    for seed in (0, 3):
+        src, tgt, _ = _scene(seed, 2000)
+        c, s_ = np.cos(0.6), np.sin(0.6)
+        guess = np.eye(4, dtype=np.float32)
+        guess[:2, :2] = [[c, -s_], [s_, c]]
+        guess[:3, 3] = [0.8, -0.5, 0.3]
+        for lm in (10, 1, 0):
+            cases.append((src, tgt, guess, gicp.default_params(k_correspondences=5, lm_max_iterations=lm)))
+    src, tgt, _ = _scene(9, 17000)
+    cases.append((src, tgt, None, gicp.default_params(k_correspondences=5)))
+    for src, tgt, guess, p in cases:
+        runs = []
+        for spec, grid in ((0, 2048), (1, 3), (2, 1), (2, 2048)):
+            plan(gicp_spec=spec, gicp_grid=grid)
+            r, aligned = gicp.align(src, tgt, p, guess=guess, want_aligned=True, ctx=gpu_ctx)
+            runs.append((r.matrix(), r.iterations, r.converged, r.fitness, r.status, aligned))
+        plan(gicp_spec=2, gicp_grid=2048)
+        for other in runs[:3]:
+            np.testing.assert_array_equal(other[0], runs[3][0])
+            assert other[1:5] == runs[3][1:5]
+            np.testing.assert_array_equal(other[5], runs[3][5])
+    o = oracle_mod.gicp_align(src, tgt, k=5)
+    r = runs[3]
+    assert r[1] == o["iterations"] and bool(r[2]) == o["converged"]
+    assert max(pose_err(r[0], o["T"])) < 1e-5
+
+
+@pytest.mark.gpu
 def test_gpu_batch_device_equals_single(gpu_ctx):
     import torch
 
