@@ -52,21 +52,33 @@ int check_params(const icp4r_gicp_params* p) {
 // k-NN covariances of the clouds (cloud, off, cnt) of npairs pairs: pruned over a Morton index of each
 // cloud (index_kernel with the cloud as its target; w's index buffers must fit max_n points) when
 // the plan prunes, brute force otherwise (ICP4R_GICP_COV_BRUTE=1 forces brute force).
+// is_tgt: the cloud is the pairs' target, whose boxes init_kernel found (w.tbb): its index is the one
+// the NN passes search, on the plan's strides (the multi-workgroup Morton sort where the plan has it).
+// Otherwise (the source) the index is built on strides of the cloud's own size (the in-LDS kd build
+// for up to 8192 points, not a Morton sort refined chunk by chunk on the target's strides).
 int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, const float4* cloud, const int64_t* off,
              const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st,
-             bool brute) {
+             bool brute, bool is_tgt) {
     if (pl.pruned && !brute) {
         PairArgs ai = a;
         ai.tgt = cloud;
         ai.tgt_off = off;
         ai.tgt_n = cnt;
-        // (w.tbb holds init_kernel's target boxes, not this cloud's: the index finds its own)
         WorkArgs wi = w;
-        wi.tbb = nullptr;
-        wi.mo_hist = nullptr;
-        wi.mo_rep = nullptr;
+        if (!is_tgt) {
+            wi.tbb = nullptr;  // (init_kernel's target boxes: the index finds the cloud's own)
+            wi.mo_hist = nullptr;
+            wi.mo_rep = nullptr;
+            const int64_t span = (int64_t)w.leaf * kSuper;
+            const int64_t ts = ((max_n > 0 ? max_n : 1) + span - 1) / span * span;
+            if (ts < w.t_stride) {
+                wi.t_stride = ts;
+                wi.b_stride = ts / w.leaf;
+                wi.sb_stride = wi.b_stride / kSuper;
+            }
+        }
         HIP_TRY(launch_index(ai, wi, npairs, st));
-        HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, w, npairs, max_n, stride, k, reg, out, st));
+        HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, wi, npairs, max_n, stride, k, reg, out, st));
     } else {
         HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, st));
     }
@@ -142,10 +154,10 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     if (kev) HIP_TRY(hipEventRecord(ce->start, st));
     // source covariances first: the target's index (built last) stays for the NN passes
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
-                       st, cov_brute)))
+                       st, cov_brute, false)))
         return rc;
     if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
-                       st, cov_brute)))
+                       st, cov_brute, true)))
         return rc;
     if (pl.pruned && cov_brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
@@ -335,7 +347,8 @@ int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_
     if ((rc = icp4r_pipe::setup_work(ctx, pl, 1, n, n, false, st, w))) return rc;
     HIP_TRY(hipMemsetAsync(w.state, 0, sizeof(PairState), st));  // phase = active: index_kernel runs
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, 1, n, n, k, regularization,
-                       static_cast<double*>(ctx->gicp_cov_src.p), st, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0) != 0)))
+                       static_cast<double*>(ctx->gicp_cov_src.p), st, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0) != 0,
+                       false)))
         return rc;
     std::vector<double> h6((size_t)n * 6);
     HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));
