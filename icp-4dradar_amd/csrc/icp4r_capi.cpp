@@ -104,7 +104,7 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad",
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
-    "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid"};
+    "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
     return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
@@ -1093,7 +1093,7 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
         static const int32_t dflt[kNumPlanOpts] = {
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
-            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid};
+            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid, 0 /*gicp_knn_lanes: auto*/};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

@@ -58,7 +58,7 @@ int check_params(const icp4r_gicp_params* p) {
 // for up to 8192 points, not a Morton sort refined chunk by chunk on the target's strides).
 int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, const float4* cloud, const int64_t* off,
              const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st,
-             bool brute, bool is_tgt) {
+             bool brute, bool is_tgt, int lanes) {
     if (pl.pruned && !brute) {
         PairArgs ai = a;
         ai.tgt = cloud;
@@ -78,7 +78,7 @@ int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, c
             }
         }
         HIP_TRY(launch_index(ai, wi, npairs, st));
-        HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, wi, npairs, max_n, stride, k, reg, out, st));
+        HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, wi, npairs, max_n, stride, k, reg, out, lanes, st));
     } else {
         HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, st));
     }
@@ -151,13 +151,14 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     double* ct = static_cast<double*>(ctx->gicp_cov_tgt.p);
     // (plan option gicp_cov_brute: brute-force k-NN covariances, for A/B and the equality test)
     const bool cov_brute = opt(ctx, kOptGicpCovBrute, 0) != 0;
+    const int knn_lanes = opt(ctx, kOptGicpKnnLanes, 0);
     if (kev) HIP_TRY(hipEventRecord(ce->start, st));
     // source covariances first: the target's index (built last) stays for the NN passes
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
-                       st, cov_brute, false)))
+                       st, cov_brute, false, knn_lanes)))
         return rc;
     if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
-                       st, cov_brute, true)))
+                       st, cov_brute, true, knn_lanes)))
         return rc;
     if (pl.pruned && cov_brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
@@ -348,7 +349,7 @@ int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_
     HIP_TRY(hipMemsetAsync(w.state, 0, sizeof(PairState), st));  // phase = active: index_kernel runs
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, 1, n, n, k, regularization,
                        static_cast<double*>(ctx->gicp_cov_src.p), st, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0) != 0,
-                       false)))
+                       false, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpKnnLanes, 0))))
         return rc;
     std::vector<double> h6((size_t)n * 6);
     HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));

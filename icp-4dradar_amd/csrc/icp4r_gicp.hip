@@ -215,10 +215,14 @@ __global__ __launch_bounds__(kCovWG) void gicp_cov_kernel(const float4* __restri
 }
 
 // Pruned exact k-NN over the cloud's own Morton index (index_kernel of the ICP core, built with the
-// cloud as target: tsort / tbox / sbox).  One query per lane, the queries of a wave Morton-contiguous
-// (sorted position = query); the wave walks superblocks outward from its own and skips a
-// (super)block whose box lower bound exceeds every lane's current K-th best d² (kLbShrink margin).
+// cloud as target: tsort / tbox / sbox).  L lanes per query, each taking every L-th point of a block
+// into a top-K list of its own; the 64 / L queries of a wave are Morton-contiguous (sorted position =
+// query); the wave walks superblocks outward from its own and skips a (super)block whose box lower
+// bound exceeds every query's bound (the least K-th best d² of its L lanes, kLbShrink margin: the
+// K-th best of the union is no larger). At the end the L lists of a query merge (shuffles + inserts).
 // Keys are (d², index): the K smallest are exactly the brute-force set, ties to the lowest index.
+// (L = 1 had one wave walk ~25 blocks of 16 points one after another for 64 queries, ~400 distance
+// evaluations per query on the bench clouds: latency-bound, a wave per SIMD on a single 8k cloud.)
 __device__ __forceinline__ float box_lb(const v4f lo, const v4f hi, float x, float y, float z) {
     const float gx = fmaxf(fmaxf(lo.x - x, x - hi.x), 0.0f);
     const float gy = fmaxf(fmaxf(lo.y - y, y - hi.y), 0.0f);
@@ -237,22 +241,24 @@ __device__ __forceinline__ float wave_min(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
 }
 
-template <int K>
+template <int K, int L>
 __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __restrict__ cloud,
                                                               const int64_t* __restrict__ off,
                                                               const int32_t* __restrict__ cnt, WorkArgs w,
                                                               int64_t stride, int k, int reg,
                                                               double* __restrict__ cov_out) {
-    constexpr int B = 16;
+    constexpr int B = 16, Q = 64 / L;
+    static_assert(L == 1 || L == 2 || L == 4 || L == 8, "lanes per query");
     const int chunks = gridDim.x;
     const int g = xcd_remap(blockIdx.x + chunks * blockIdx.y, chunks * gridDim.y);
     const int p = g / chunks, ch = g - p * chunks;
     const int n = uload(cnt + p);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int base = ch * kCovWG + wave * 64;
+    const int base = ch * (kCovWG / L) + wave * Q;
     if (base >= n) return;
+    const int qi = lane / L, sub = lane % L;
     const float4* tsg = w.tsort + (int64_t)p * w.t_stride;
-    const float4 qv = tsg[min(base + lane, n - 1)];
+    const float4 qv = tsg[min(base + qi, n - 1)];
     const float x = qv.x, y = qv.y, z = qv.z;
     // empty slots hold (+inf, ~0): a real d² bound for the pruning tests (all-ones bits would be a NaN
     // d² that no box bound passes) that every finite key beats
@@ -262,8 +268,15 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
     float qlo[3] = {wave_min(x), wave_min(y), wave_min(z)};
     float qhi[3] = {wave_max(x), wave_max(y), wave_max(z)};
     float qmax = INFINITY;
+    float gb = INFINITY;  // this query's bound: the least K-th best of its L lanes
+    auto group_bound = [&]() {
+        float b = __uint_as_float((uint32_t)(best[K - 1] >> 32));
+#pragma unroll
+        for (int o = 1; o < L; o <<= 1) b = fminf(b, __shfl_xor(b, o, 64));
+        return b;
+    };
     const int nb = (n + B - 1) / B, nsb = (nb + kSuper - 1) / kSuper;
-    const int sb0 = base / (B * kSuper);
+    const int sb0 = base / (B * kSuper);  // (Q divides B * kSuper: the wave's queries share it)
     const cv4f_ptr ts = as_const(tsg);
     const cv4f_ptr tb = as_const(w.tbox + (int64_t)p * 2 * w.b_stride);
     const cv4f_ptr sbx = as_const(w.sbox + (int64_t)p * 2 * w.sb_stride);
@@ -273,9 +286,7 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
         const float gz = fmaxf(fmaxf(lo.z - qhi[2], qlo[2] - hi.z), 0.0f);
         return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx)) * kLbShrink <= qmax;
     };
-    auto needed = [&](const v4f lo, const v4f hi) {
-        return __any(box_lb(lo, hi, x, y, z) * kLbShrink <= __uint_as_float((uint32_t)(best[K - 1] >> 32)));
-    };
+    auto needed = [&](const v4f lo, const v4f hi) { return __any(box_lb(lo, hi, x, y, z) * kLbShrink <= gb); };
     unsigned long long swept = 0;
     auto visit = [&](int sb, bool test) {  // sweep superblock sb's needed blocks, then refresh the bound
         const v4f slo = sbx[2 * sb], shi = sbx[2 * sb + 1];
@@ -285,13 +296,14 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
             if (!maybe(blo, bhi) || !needed(blo, bhi)) continue;
             const cv4f_ptr blk = ts + (int64_t)b * B;
 #pragma unroll
-            for (int t = 0; t < B; ++t) {
-                const v4f v = blk[t];
+            for (int t = 0; t < B / L; ++t) {
+                const v4f v = blk[sub + L * t];
                 knn_insert<K>(best, make_key(l2_simple(x, y, z, v.x, v.y, v.z), __float_as_uint(v.w)));
             }
             ++swept;
+            gb = group_bound();
         }
-        qmax = wave_max(__uint_as_float((uint32_t)(best[K - 1] >> 32)));
+        qmax = wave_max(gb);
     };
     if (nsb <= 64) {
         // the wave's own superblock first (a finite K-th bound for every lane), then one lane-parallel
@@ -353,8 +365,20 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
             }
         }
     }
-    if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, 64));
-    if (base + lane >= n) return;
+    if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, Q));
+    // the L lists of a query into one: each lane takes in its partners' keys (all L lanes end alike)
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) {
+        uint64_t other[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            const uint32_t lo = __shfl_xor((uint32_t)best[s], o, 64), hi = __shfl_xor((uint32_t)(best[s] >> 32), o, 64);
+            other[s] = (uint64_t)hi << 32 | lo;
+        }
+#pragma unroll
+        for (int s = 0; s < K; ++s) knn_insert<K>(best, other[s]);
+    }
+    if (sub != 0 || base + qi >= n) return;
     const uint32_t oi = __float_as_uint(qv.w);
     gicp_cov_from_knn<K>(best, min(k, n), k, reg, cloud + off[p], n, cov_out + ((int64_t)p * stride + oi) * 6);
 }
@@ -914,24 +938,43 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
 }
 
 hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
-                               int npairs, int max_n, int64_t stride, int k, int reg, double* cov, hipStream_t st) {
+                               int npairs, int max_n, int64_t stride, int k, int reg, double* cov, int lanes,
+                               hipStream_t st) {
     if (npairs <= 0 || max_n <= 0) return hipSuccess;
     if (w.leaf != 16) return hipErrorInvalidValue;
-    const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
+    if (lanes == 0) {  // auto: more lanes per query only where the grid leaves the chip short of waves
+        // (a single 8k scan: 128 waves at one lane per query; the map call's two clouds 1.42 -> 1.29 ms at
+        // 8 lanes, while a 256-pair batch, 32k waves, ran 1.57 -> 4.57 ms of covariances at 8)
+        const int64_t waves1 = (int64_t)npairs * ((max_n + 63) / 64);
+        lanes = 1;
+        while (lanes < 8 && waves1 * lanes * 2 <= kGicpKnnWaves) lanes *= 2;
+    }
+    if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8) return hipErrorInvalidValue;
+    const int qpw = kCovWG / lanes;  // queries per workgroup
+    const dim3 grid((max_n + qpw - 1) / qpw, npairs), block(kCovWG);
     // the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default
     // 20 have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
-    if (k <= 5)
-        hipLaunchKernelGGL(gicp_knn_cov_kernel<5>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
-    else if (k <= 8)
-        hipLaunchKernelGGL(gicp_knn_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
-    else if (k <= 16)
-        hipLaunchKernelGGL(gicp_knn_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
-    else if (k <= 20)
-        hipLaunchKernelGGL(gicp_knn_cov_kernel<20>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
-    else if (k <= 32)
-        hipLaunchKernelGGL(gicp_knn_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov);
-    else
+#define ICP4R_KNN_COV(KK)                                                                                              \
+    switch (lanes) {                                                                                                   \
+        case 1: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 1>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
+        case 2: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 2>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
+        case 4: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 4>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
+        default: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 8>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
+    }
+    if (k <= 5) {
+        ICP4R_KNN_COV(5)
+    } else if (k <= 8) {
+        ICP4R_KNN_COV(8)
+    } else if (k <= 16) {
+        ICP4R_KNN_COV(16)
+    } else if (k <= 20) {
+        ICP4R_KNN_COV(20)
+    } else if (k <= 32) {
+        ICP4R_KNN_COV(32)
+    } else {
         return hipErrorInvalidValue;
+    }
+#undef ICP4R_KNN_COV
     return hipGetLastError();
 }
 

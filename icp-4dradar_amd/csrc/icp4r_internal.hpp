@@ -269,7 +269,9 @@ struct GicpState {
 constexpr int kGicpSys = 21 + 6 + 1 + 1;  // H (upper triangle), g, y, |valid|
 constexpr int kGicpSpec = 2;             // LM trials evaluated per pass (the rest, rarely needed, one by one)
 constexpr int kGicpMaxSlices = 64;
-constexpr int kGicpGrid = 2048;          // workgroups per iteration kernel, about (a pair: at most its slices)
+constexpr int kGicpGrid = 2048;
+constexpr int kGicpKnnWaves = 16384;     // k-NN covariance walk: lanes per query up to 8 while the
+                                         // grid stays within this many waves (0 lanes: this rule)          // workgroups per iteration kernel, about (a pair: at most its slices)
 struct GicpTrial {
     double R[9], t[3];    // the trial transform delta * x0
     double dR[9], dt[3];  // delta
@@ -302,7 +304,8 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
                            int64_t stride, int k, int reg, double* cov, hipStream_t st);
 // k-NN covariances over a Morton index of the cloud itself (w.tsort / tbox / sbox, leaf 16)
 hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
-                               int npairs, int max_n, int64_t stride, int k, int reg, double* cov, hipStream_t st);
+                               int npairs, int max_n, int64_t stride, int k, int reg, double* cov, int lanes,
+                               hipStream_t st);
 hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s);
 hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st);

@@ -126,17 +126,20 @@ def test_gpu_covariances_match_oracle(gpu_ctx, oracle_mod, reg):
 @pytest.mark.gpu
 def test_gpu_pruned_knn_equals_brute_force(gpu_ctx, oracle_mod, plan):
     """The Morton-pruned k-NN (clouds >= 512 points) returns exactly the brute-force neighbour sets:
-    covariances bit-identical, including clouds with duplicated points (distance ties)."""
+    covariances bit-identical, including clouds with duplicated points (distance ties), for every
+    number of lanes per query."""
     gicp = _gicp()
     src, tgt, _ = _scene(8, 6000)
     dup = np.concatenate([tgt[:1500], tgt[:1500], tgt[700:1400]])  # every point at least twice
     for cloud in (src, dup, _grid_plane(40)):
         for k in (1, 5, 20, 32):
-            pruned = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
             plan(gicp_cov_brute=1)
             brute = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
             plan(gicp_cov_brute=0)
-            np.testing.assert_array_equal(pruned, brute)
+            for lanes in (1, 2, 4, 8):  # lanes per query of the walk (plan option gicp_knn_lanes)
+                plan(gicp_knn_lanes=lanes)
+                np.testing.assert_array_equal(gicp.covariances(cloud, k, 3, ctx=gpu_ctx), brute, err_msg=f"k={k} L={lanes}")
+            plan(gicp_knn_lanes=0)
     want = oracle_mod.gicp_covariances(dup, 5, 3)
     np.testing.assert_allclose(gicp.covariances(dup, 5, 3, ctx=gpu_ctx), want, rtol=1e-9, atol=1e-12)
 
