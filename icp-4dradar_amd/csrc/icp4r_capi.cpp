@@ -1093,7 +1093,8 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
         static const int32_t dflt[kNumPlanOpts] = {
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
-            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid, 0 /*gicp_knn_lanes: auto*/};
+            0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid,
+            0 /*gicp_knn_lanes: auto*/};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

@@ -49,9 +49,16 @@ int check_params(const icp4r_gicp_params* p) {
     return ICP4R_OK;
 }
 
-// k-NN covariances of the clouds (cloud, off, cnt) of npairs pairs: pruned over a Morton index of each
-// cloud (index_kernel with the cloud as its target; w's index buffers must fit max_n points) when
-// the plan prunes, brute force otherwise (ICP4R_GICP_COV_BRUTE=1 forces brute force).
+// Brute force or pruned k-NN for the covariances: brute force where the plan does not prune, or with
+// plan option gicp_cov_brute = 1 (A/B and the equality test). (Brute force by default for small
+// grids measured slower even for a single 8k scan: the map call 1.27 -> 1.36 ms with its source by
+// brute force, an 8k pair at k = 20 0.96 -> 2.07 ms — every candidate ran the insertion chain in
+// some lane of the wave.)
+bool cov_brute(int opt_val, const icp4r_pipe::Plan& pl) { return !pl.pruned || opt_val == 1; }
+
+// k-NN covariances of the clouds (cloud, off, cnt) of npairs pairs: brute force, or pruned over an
+// index of each cloud (index_kernel with the cloud as its target; w's index buffers must fit max_n
+// points).
 // is_tgt: the cloud is the pairs' target, whose boxes init_kernel found (w.tbb): its index is the one
 // the NN passes search, on the plan's strides (the multi-workgroup Morton sort where the plan has it).
 // Otherwise (the source) the index is built on strides of the cloud's own size (the in-LDS kd build
@@ -59,7 +66,7 @@ int check_params(const icp4r_gicp_params* p) {
 int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, const float4* cloud, const int64_t* off,
              const int32_t* cnt, int npairs, int max_n, int64_t stride, int k, int reg, double* out, hipStream_t st,
              bool brute, bool is_tgt, int lanes) {
-    if (pl.pruned && !brute) {
+    if (!brute) {
         PairArgs ai = a;
         ai.tgt = cloud;
         ai.tgt_off = off;
@@ -80,7 +87,7 @@ int cov_pass(const icp4r_pipe::Plan& pl, const PairArgs& a, const WorkArgs& w, c
         HIP_TRY(launch_index(ai, wi, npairs, st));
         HIP_TRY(launch_gicp_knn_cov(cloud, off, cnt, wi, npairs, max_n, stride, k, reg, out, lanes, st));
     } else {
-        HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, st));
+        HIP_TRY(launch_gicp_cov(cloud, off, cnt, npairs, max_n, stride, k, reg, out, lanes, st));
     }
     return ICP4R_OK;
 }
@@ -149,18 +156,17 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     if (kev && (rc = next_event(ctx->gicp_events, ctx->gicp_used, &ce))) return rc;
     double* cs = static_cast<double*>(ctx->gicp_cov_src.p);
     double* ct = static_cast<double*>(ctx->gicp_cov_tgt.p);
-    // (plan option gicp_cov_brute: brute-force k-NN covariances, for A/B and the equality test)
-    const bool cov_brute = opt(ctx, kOptGicpCovBrute, 0) != 0;
+    const bool brute = cov_brute(opt(ctx, kOptGicpCovBrute, 0), pl);
     const int knn_lanes = opt(ctx, kOptGicpKnnLanes, 0);
     if (kev) HIP_TRY(hipEventRecord(ce->start, st));
     // source covariances first: the target's index (built last) stays for the NN passes
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
-                       st, cov_brute, false, knn_lanes)))
+                       st, brute, false, knn_lanes)))
         return rc;
     if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
-                       st, cov_brute, true, knn_lanes)))
+                       st, brute, true, knn_lanes)))
         return rc;
-    if (pl.pruned && cov_brute) HIP_TRY(launch_index(a, w, npairs, st));
+    if (pl.pruned && brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
     for (int it = 0; it < gp.max_iterations; ++it) {
@@ -348,8 +354,9 @@ int icp4r_gicp_covariances(icp4r_ctx* ctx, const float* cloud, int32_t n, int32_
     if ((rc = icp4r_pipe::setup_work(ctx, pl, 1, n, n, false, st, w))) return rc;
     HIP_TRY(hipMemsetAsync(w.state, 0, sizeof(PairState), st));  // phase = active: index_kernel runs
     if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, 1, n, n, k, regularization,
-                       static_cast<double*>(ctx->gicp_cov_src.p), st, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0) != 0,
-                       false, icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpKnnLanes, 0))))
+                       static_cast<double*>(ctx->gicp_cov_src.p), st,
+                       cov_brute(icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpCovBrute, 0), pl), false,
+                       icp4r_pipe::opt(ctx, icp4r_pipe::kOptGicpKnnLanes, 0))))
         return rc;
     std::vector<double> h6((size_t)n * 6);
     HIP_TRY(hipMemcpyAsync(h6.data(), ctx->gicp_cov_src.p, h6.size() * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -185,15 +185,36 @@ __device__ __forceinline__ void knn_insert(uint64_t (&best)[K], uint64_t key) {
 constexpr int kCovWG = 256;
 constexpr int kCovTile = 1024;
 
-template <int K>
+// the L lists of a query (lanes lane ^ o, o < L) into one: each lane takes in its partners' keys, so all
+// L lanes end with the K smallest of their union
+template <int K, int L>
+__device__ __forceinline__ void knn_merge_lanes(uint64_t (&best)[K]) {
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) {
+        uint64_t other[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            const uint32_t lo = __shfl_xor((uint32_t)best[s], o, 64), hi = __shfl_xor((uint32_t)(best[s] >> 32), o, 64);
+            other[s] = (uint64_t)hi << 32 | lo;
+        }
+#pragma unroll
+        for (int s = 0; s < K; ++s) knn_insert<K>(best, other[s]);
+    }
+}
+
+// Brute-force exact k-NN (every point of the cloud through LDS tiles), L lanes per query each taking
+// every L-th point of a tile: plans that do not prune, and the reference the pruned walk is tested
+// against (slower than index + pruned walk even for one 8k scan, §6d).
+template <int K, int L>
 __global__ __launch_bounds__(kCovWG) void gicp_cov_kernel(const float4* __restrict__ cloud, const int64_t* __restrict__ off,
                                                           const int32_t* __restrict__ cnt, int64_t stride, int k, int reg,
                                                           double* __restrict__ cov_out) {
     __shared__ float4 tile[kCovTile];
+    constexpr int QW = kCovWG / L;  // queries per workgroup
     const int p = blockIdx.y;
     const int n = cnt[p];
-    const int i = blockIdx.x * kCovWG + threadIdx.x;
-    if (blockIdx.x * kCovWG >= n) return;
+    const int i = blockIdx.x * QW + threadIdx.x / L, sub = threadIdx.x % L;
+    if (blockIdx.x * QW >= n) return;
     const float4* c = cloud + off[p];
     const float4 q = c[min(i, n - 1)];
     uint64_t best[K];
@@ -204,13 +225,14 @@ __global__ __launch_bounds__(kCovWG) void gicp_cov_kernel(const float4* __restri
         __syncthreads();
         for (int t = threadIdx.x; t < len; t += kCovWG) tile[t] = c[j0 + t];
         __syncthreads();
-        for (int t = 0; t < len; ++t) {
+        for (int t = sub; t < len; t += L) {
             const float4 v = tile[t];
             const float d2 = l2_simple(q.x, q.y, q.z, v.x, v.y, v.z);
             knn_insert<K>(best, make_key(d2, (uint32_t)(j0 + t)));
         }
     }
-    if (i >= n) return;
+    knn_merge_lanes<K, L>(best);
+    if (sub != 0 || i >= n) return;
     gicp_cov_from_knn<K>(best, min(k, n), k, reg, c, n, cov_out + ((int64_t)p * stride + i) * 6);
 }
 
@@ -366,18 +388,7 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
         }
     }
     if (lane == 0 && w.evals) count_add(w.evals, 0, swept * B * (unsigned long long)min(n - base, Q));
-    // the L lists of a query into one: each lane takes in its partners' keys (all L lanes end alike)
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) {
-        uint64_t other[K];
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-            const uint32_t lo = __shfl_xor((uint32_t)best[s], o, 64), hi = __shfl_xor((uint32_t)(best[s] >> 32), o, 64);
-            other[s] = (uint64_t)hi << 32 | lo;
-        }
-#pragma unroll
-        for (int s = 0; s < K; ++s) knn_insert<K>(best, other[s]);
-    }
+    knn_merge_lanes<K, L>(best);
     if (sub != 0 || base + qi >= n) return;
     const uint32_t oi = __float_as_uint(qv.w);
     gicp_cov_from_knn<K>(best, min(k, n), k, reg, cloud + off[p], n, cov_out + ((int64_t)p * stride + oi) * 6);
@@ -916,24 +927,47 @@ hipError_t launch_gicp_init(const float* guess, GicpState* gs, int npairs, hipSt
     return hipGetLastError();
 }
 
+// lanes per query: up to 8 while the grid stays within kGicpKnnWaves waves (0: this rule)
+static int knn_lanes(int lanes, int npairs, int max_n) {
+    if (lanes != 0) return lanes;
+    const int64_t waves1 = (int64_t)npairs * ((max_n + 63) / 64);
+    lanes = 1;
+    while (lanes < 8 && waves1 * lanes * 2 <= kGicpKnnWaves) lanes *= 2;
+    return lanes;
+}
+
+#define ICP4R_COV_LANES(KERNEL, KK, ...)                                                                  \
+    switch (lanes) {                                                                                     \
+        case 1: hipLaunchKernelGGL((KERNEL<KK, 1>), grid, block, 0, st, __VA_ARGS__); break;             \
+        case 2: hipLaunchKernelGGL((KERNEL<KK, 2>), grid, block, 0, st, __VA_ARGS__); break;             \
+        case 4: hipLaunchKernelGGL((KERNEL<KK, 4>), grid, block, 0, st, __VA_ARGS__); break;             \
+        default: hipLaunchKernelGGL((KERNEL<KK, 8>), grid, block, 0, st, __VA_ARGS__); break;            \
+    }
+// the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default 20
+// have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
+#define ICP4R_COV_K(KERNEL, ...)                 \
+    if (k <= 5) {                                \
+        ICP4R_COV_LANES(KERNEL, 5, __VA_ARGS__)  \
+    } else if (k <= 8) {                         \
+        ICP4R_COV_LANES(KERNEL, 8, __VA_ARGS__)  \
+    } else if (k <= 16) {                        \
+        ICP4R_COV_LANES(KERNEL, 16, __VA_ARGS__) \
+    } else if (k <= 20) {                        \
+        ICP4R_COV_LANES(KERNEL, 20, __VA_ARGS__) \
+    } else if (k <= 32) {                        \
+        ICP4R_COV_LANES(KERNEL, 32, __VA_ARGS__) \
+    } else {                                     \
+        return hipErrorInvalidValue;             \
+    }
+
 hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, int npairs, int max_n,
-                           int64_t stride, int k, int reg, double* cov, hipStream_t st) {
+                           int64_t stride, int k, int reg, double* cov, int lanes, hipStream_t st) {
     if (npairs <= 0 || max_n <= 0) return hipSuccess;
-    const dim3 grid((max_n + kCovWG - 1) / kCovWG, npairs), block(kCovWG);
-    // the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default
-    // 20 have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
-    if (k <= 5)
-        hipLaunchKernelGGL(gicp_cov_kernel<5>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
-    else if (k <= 8)
-        hipLaunchKernelGGL(gicp_cov_kernel<8>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
-    else if (k <= 16)
-        hipLaunchKernelGGL(gicp_cov_kernel<16>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
-    else if (k <= 20)
-        hipLaunchKernelGGL(gicp_cov_kernel<20>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
-    else if (k <= 32)
-        hipLaunchKernelGGL(gicp_cov_kernel<32>, grid, block, 0, st, cloud, off, cnt, stride, k, reg, cov);
-    else
-        return hipErrorInvalidValue;
+    lanes = knn_lanes(lanes, npairs, max_n);
+    if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8) return hipErrorInvalidValue;
+    const int qpw = kCovWG / lanes;
+    const dim3 grid((max_n + qpw - 1) / qpw, npairs), block(kCovWG);
+    ICP4R_COV_K(gicp_cov_kernel, cloud, off, cnt, stride, k, reg, cov)
     return hipGetLastError();
 }
 
@@ -942,41 +976,17 @@ hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const in
                                hipStream_t st) {
     if (npairs <= 0 || max_n <= 0) return hipSuccess;
     if (w.leaf != 16) return hipErrorInvalidValue;
-    if (lanes == 0) {  // auto: more lanes per query only where the grid leaves the chip short of waves
-        // (a single 8k scan: 128 waves at one lane per query; the map call's two clouds 1.42 -> 1.29 ms at
-        // 8 lanes, while a 256-pair batch, 32k waves, ran 1.57 -> 4.57 ms of covariances at 8)
-        const int64_t waves1 = (int64_t)npairs * ((max_n + 63) / 64);
-        lanes = 1;
-        while (lanes < 8 && waves1 * lanes * 2 <= kGicpKnnWaves) lanes *= 2;
-    }
+    // (a single 8k scan: 128 waves at one lane per query; the map call's two clouds 1.42 -> 1.29 ms at 8
+    // lanes, while a 256-pair batch, 32k waves, ran 1.57 -> 4.57 ms of covariances at 8)
+    lanes = knn_lanes(lanes, npairs, max_n);
     if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8) return hipErrorInvalidValue;
     const int qpw = kCovWG / lanes;  // queries per workgroup
     const dim3 grid((max_n + qpw - 1) / qpw, npairs), block(kCovWG);
-    // the list length K is the next instantiated size >= k: the node's k = 5 and fast_gicp's default
-    // 20 have their own (a longer list costs insertion work and loosens the K-th-best pruning bound)
-#define ICP4R_KNN_COV(KK)                                                                                              \
-    switch (lanes) {                                                                                                   \
-        case 1: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 1>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
-        case 2: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 2>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
-        case 4: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 4>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
-        default: hipLaunchKernelGGL((gicp_knn_cov_kernel<KK, 8>), grid, block, 0, st, cloud, off, cnt, w, stride, k, reg, cov); break; \
-    }
-    if (k <= 5) {
-        ICP4R_KNN_COV(5)
-    } else if (k <= 8) {
-        ICP4R_KNN_COV(8)
-    } else if (k <= 16) {
-        ICP4R_KNN_COV(16)
-    } else if (k <= 20) {
-        ICP4R_KNN_COV(20)
-    } else if (k <= 32) {
-        ICP4R_KNN_COV(32)
-    } else {
-        return hipErrorInvalidValue;
-    }
-#undef ICP4R_KNN_COV
+    ICP4R_COV_K(gicp_knn_cov_kernel, cloud, off, cnt, w, stride, k, reg, cov)
     return hipGetLastError();
 }
+#undef ICP4R_COV_K
+#undef ICP4R_COV_LANES
 
 hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st) {

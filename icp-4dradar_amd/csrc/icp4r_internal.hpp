@@ -301,7 +301,7 @@ struct GicpArgs {
 };
 hipError_t launch_gicp_init(const float* guess, GicpState* gs, int npairs, hipStream_t st);
 hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, int npairs, int max_n,
-                           int64_t stride, int k, int reg, double* cov, hipStream_t st);
+                           int64_t stride, int k, int reg, double* cov, int lanes, hipStream_t st);
 // k-NN covariances over a Morton index of the cloud itself (w.tsort / tbox / sbox, leaf 16)
 hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
                                int npairs, int max_n, int64_t stride, int k, int reg, double* cov, int lanes,

@@ -133,13 +133,14 @@ def test_gpu_pruned_knn_equals_brute_force(gpu_ctx, oracle_mod, plan):
     dup = np.concatenate([tgt[:1500], tgt[:1500], tgt[700:1400]])  # every point at least twice
     for cloud in (src, dup, _grid_plane(40)):
         for k in (1, 5, 20, 32):
-            plan(gicp_cov_brute=1)
+            plan(gicp_cov_brute=1, gicp_knn_lanes=1)
             brute = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
-            plan(gicp_cov_brute=0)
-            for lanes in (1, 2, 4, 8):  # lanes per query of the walk (plan option gicp_knn_lanes)
-                plan(gicp_knn_lanes=lanes)
-                np.testing.assert_array_equal(gicp.covariances(cloud, k, 3, ctx=gpu_ctx), brute, err_msg=f"k={k} L={lanes}")
-            plan(gicp_knn_lanes=0)
+            for mode in (1, 0):  # brute force, pruned (plan option gicp_cov_brute)
+                for lanes in (1, 2, 4, 8):  # lanes per query (plan option gicp_knn_lanes)
+                    plan(gicp_cov_brute=mode, gicp_knn_lanes=lanes)
+                    got = gicp.covariances(cloud, k, 3, ctx=gpu_ctx)
+                    np.testing.assert_array_equal(got, brute, err_msg=f"k={k} brute={mode} L={lanes}")
+            plan(gicp_cov_brute=0, gicp_knn_lanes=0)
     want = oracle_mod.gicp_covariances(dup, 5, 3)
     np.testing.assert_allclose(gicp.covariances(dup, 5, 3, ctx=gpu_ctx), want, rtol=1e-9, atol=1e-12)
 
