@@ -772,6 +772,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
             (void)hipEventDestroy(ev.start);
             (void)hipEventDestroy(ev.stop);
         }
+    if (ctx->gicp_hflag) (void)hipHostFree(ctx->gicp_hflag);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return ICP4R_OK;

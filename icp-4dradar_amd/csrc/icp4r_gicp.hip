@@ -905,8 +905,9 @@ __global__ void gicp_init_kernel(const float* guess, GicpState* gs, int npairs) 
     s.lambda = -1.0;
 }
 
-// number of pairs still iterating -> *out (the host's early exit between runs of iterations)
-__global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out) {
+// number of pairs still iterating -> *out, and (host_out) with a system-scope store into pinned host
+// memory the host polls (the host's early exit between runs of iterations)
+__global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out, int32_t* host_out) {
     __shared__ int32_t tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
@@ -914,11 +915,14 @@ __global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out
     for (int p = threadIdx.x; p < npairs; p += blockDim.x) c += st[p].phase == kPhaseActive;
     if (c) atomicAdd(&tot, c);
     __syncthreads();
-    if (threadIdx.x == 0) *out = tot;
+    if (threadIdx.x == 0) {
+        *out = tot;
+        if (host_out) __hip_atomic_store(host_out, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(gicp_active_kernel, dim3(1), dim3(1024), 0, s, st, npairs, out);
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int32_t* host_out, hipStream_t s) {
+    hipLaunchKernelGGL(gicp_active_kernel, dim3(1), dim3(1024), 0, s, st, npairs, out, host_out);
     return hipGetLastError();
 }
 

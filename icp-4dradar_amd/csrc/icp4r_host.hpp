@@ -113,6 +113,7 @@ struct icp4r_ctx {
     icp4r_host::DevBuf ego_rec, ego_off, ego_cnt, ego_feat, ego_pd, ego_scores, ego_res, ego_mask, ego_xyzi;
     // generalized ICP (icp4r_gicp.cpp): per-pair LM state, covariances, Mahalanobis, active count
     icp4r_host::DevBuf gicp_gs, gicp_cov_src, gicp_cov_tgt, gicp_mah, gicp_active, gicp_part;
+    int32_t* gicp_hflag = nullptr;  // pinned host slots the active-pair checks write (hipHostMalloc)
     std::vector<icp4r_host::EventPair> gicp_events;  // covariance launches (the iterations time as UPDATE)
     size_t gicp_used = 0;
 };

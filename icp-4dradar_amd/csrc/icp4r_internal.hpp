@@ -306,7 +306,8 @@ hipError_t launch_gicp_cov(const float4* cloud, const int64_t* off, const int32_
 hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const int32_t* cnt, const WorkArgs& w,
                                int npairs, int max_n, int64_t stride, int k, int reg, double* cov, int lanes,
                                hipStream_t st);
-hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, hipStream_t s);
+// the number of pairs still iterating into *out and, if host_out, into pinned host memory
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int32_t* host_out, hipStream_t s);
 hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st);
 

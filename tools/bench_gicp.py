@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="override k_correspondences")
     ap.add_argument("--reg", type=int, default=-1, help="override the regularization (icp4r_gicp_regularization)")
     ap.add_argument("--max-iterations", type=int, default=-1)
+    ap.add_argument("--no-stages", action="store_true",
+                    help="no per-stage events (each costs device time between kernels): the call's time alone")
     a = ap.parse_args()
     import torch
 
@@ -90,7 +92,7 @@ def main():
     b.src_off, b.src_n, b.tgt_off, b.tgt_n = ts["so"].data_ptr(), ts["sn"].data_ptr(), ts["to"].data_ptr(), ts["tn"].data_ptr()
     b.npairs, b.max_src_n, b.max_tgt_n = len(pairs), int(sn.max()), int(tn.max())
     ctx = icp4r.Context(0, plan=icp4r.env_plan())
-    ctx.set_kernel_timing(True)  # (this tool reports per-kernel times)
+    ctx.set_kernel_timing(not a.no_stages)  # (per-stage times, unless --no-stages)
     k = a.k or k
     p = gicp.default_params(k_correspondences=k)
     if a.reg >= 0:
