@@ -765,7 +765,7 @@ int icp4r_destroy(icp4r_ctx* ctx) {
                       &ctx->state, &ctx->tsort, &ctx->tinv, &ctx->tbox, &ctx->sbox, &ctx->sperm, &ctx->evals, &ctx->corr, &ctx->ticks, &ctx->nn_lu, &ctx->nn_t, &ctx->kdn, &ctx->sq, &ctx->sm, &ctx->qv, &ctx->qm, &ctx->need,
                       &ctx->miss_cnt, &ctx->plist, &ctx->plist_n, &ctx->owork, &ctx->ego_rec, &ctx->ego_off, &ctx->ego_cnt, &ctx->ego_feat,
                       &ctx->ego_pd, &ctx->ego_scores, &ctx->ego_res, &ctx->ego_mask, &ctx->ego_xyzi, &ctx->gicp_gs,
-                      &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active, &ctx->gicp_part})
+                      &ctx->gicp_cov_src, &ctx->gicp_cov_tgt, &ctx->gicp_mah, &ctx->gicp_active, &ctx->gicp_part, &ctx->gicp_sidx})
         b->release();
     for (auto* v : {&ctx->nn_events, &ctx->test_events, &ctx->upd_events, &ctx->batch_events, &ctx->gicp_events})
         for (auto& ev : *v) {
@@ -773,6 +773,8 @@ int icp4r_destroy(icp4r_ctx* ctx) {
             (void)hipEventDestroy(ev.stop);
         }
     if (ctx->gicp_hflag) (void)hipHostFree(ctx->gicp_hflag);
+    if (ctx->gicp_fork) (void)hipEventDestroy(ctx->gicp_fork);
+    if (ctx->gicp_join) (void)hipEventDestroy(ctx->gicp_join);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return ICP4R_OK;

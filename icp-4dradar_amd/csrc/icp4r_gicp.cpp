@@ -182,13 +182,59 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     const bool brute = cov_brute(opt(ctx, kOptGicpCovBrute, 0), pl);
     const int knn_lanes = opt(ctx, kOptGicpKnnLanes, 0);
     if (kev) HIP_TRY(hipEventRecord(ce->start, st));
-    // source covariances first: the target's index (built last) stays for the NN passes
-    if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences, gp.regularization, cs,
-                       st, brute, false, knn_lanes)))
-        return rc;
-    if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization, ct,
-                       st, brute, true, knn_lanes)))
-        return rc;
+    if (!brute) {
+        // The source's index on buffers of its own and its k-NN covariances on the aux stream, beside the
+        // target's chain (index, refinement, k-NN) on st: both chains are latency-bound on few pairs
+        // (the map call: the 8k source's kd build and walk ~120 µs under the submap's ~240).
+        hipStream_t aux = ctx->aux_stream[0];
+        if (!aux) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream[0], hipStreamNonBlocking));
+            aux = ctx->aux_stream[0];
+        }
+        if (!ctx->gicp_fork) HIP_TRY(hipEventCreateWithFlags(&ctx->gicp_fork, hipEventDisableTiming));
+        if (!ctx->gicp_join) HIP_TRY(hipEventCreateWithFlags(&ctx->gicp_join, hipEventDisableTiming));
+        WorkArgs ws = w;
+        const int64_t span = (int64_t)w.leaf * kSuper;
+        ws.t_stride = ((int64_t)mn + span - 1) / span * span;
+        ws.b_stride = ws.t_stride / w.leaf;
+        ws.sb_stride = ws.b_stride / kSuper;
+        ws.tbb = nullptr;  // (init_kernel's are the target's boxes: the build finds the source's own)
+        ws.mo_hist = nullptr;
+        ws.mo_rep = nullptr;
+        ws.kdn = nullptr;  // (no tree for a source order to descend)
+        ws.src_by_tgt = 0;
+        ws.ticks = nullptr;
+        const size_t n_ts = (size_t)npairs * ws.t_stride, n_b = (size_t)npairs * 2 * ws.b_stride,
+                     n_sb = (size_t)npairs * 2 * ws.sb_stride, n_q = w.qv ? (size_t)npairs * w.x_stride : 0;
+        HIP_TRY(ctx->gicp_sidx.ensure((n_ts + n_b + n_sb + n_q) * sizeof(float4) + n_ts * sizeof(int32_t)));
+        float4* sb = static_cast<float4*>(ctx->gicp_sidx.p);
+        ws.tsort = sb;
+        ws.tbox = sb + n_ts;
+        ws.sbox = ws.tbox + n_b;
+        ws.qv = w.qv ? ws.sbox + n_sb : nullptr;  // (the kd build's key scratch: the target's is in use)
+        ws.tinv = reinterpret_cast<int32_t*>(ws.sbox + n_sb + n_q);
+        PairArgs as = a;
+        as.tgt = a.src;
+        as.tgt_off = a.src_off;
+        as.tgt_n = a.src_n;
+        HIP_TRY(hipEventRecord(ctx->gicp_fork, st));
+        HIP_TRY(hipStreamWaitEvent(aux, ctx->gicp_fork, 0));
+        HIP_TRY(launch_index_cloud(as, ws, npairs, aux));
+        HIP_TRY(launch_gicp_knn_cov(a.src, a.src_off, a.src_n, ws, npairs, mn, xs, gp.k_correspondences,
+                                    gp.regularization, cs, knn_lanes, aux));
+        HIP_TRY(hipEventRecord(ctx->gicp_join, aux));
+        if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences,
+                           gp.regularization, ct, st, brute, true, knn_lanes)))
+            return rc;
+        HIP_TRY(hipStreamWaitEvent(st, ctx->gicp_join, 0));
+    } else {
+        if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences,
+                           gp.regularization, cs, st, brute, false, knn_lanes)))
+            return rc;
+        if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences,
+                           gp.regularization, ct, st, brute, true, knn_lanes)))
+            return rc;
+    }
     if (pl.pruned && brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);

@@ -114,6 +114,8 @@ struct icp4r_ctx {
     // generalized ICP (icp4r_gicp.cpp): per-pair LM state, covariances, Mahalanobis, active count
     icp4r_host::DevBuf gicp_gs, gicp_cov_src, gicp_cov_tgt, gicp_mah, gicp_active, gicp_part;
     int32_t* gicp_hflag = nullptr;  // pinned host slots the active-pair checks write (hipHostMalloc)
+    icp4r_host::DevBuf gicp_sidx;   // the source's own index (its k-NN covariances, beside the target's)
+    hipEvent_t gicp_fork = nullptr, gicp_join = nullptr;
     std::vector<icp4r_host::EventPair> gicp_events;  // covariance launches (the iterations time as UPDATE)
     size_t gicp_used = 0;
 };

@@ -192,6 +192,8 @@ hipError_t launch_init(const PairArgs& a, const WorkArgs& w, int npairs, hipStre
 hipError_t launch_nn(int q, bool packed, const PairArgs& a, const WorkArgs& w, int npairs, int max_n,
                      int fitness_pass, hipStream_t st);
 hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
+// one cloud's index alone (as pair p's target; w's index buffers), no source column or order
+hipError_t launch_index_cloud(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st);
 // chunk_sb: superblocks per target chunk (<= 64); chunks: grid.z (1: one wave searches every superblock)
 hipError_t launch_nn_pruned(int q, int chunk_sb, int chunks, const PairArgs& a, const WorkArgs& w, int npairs,
                             int max_n, int fitness_pass, int first, hipStream_t st);

@@ -1449,6 +1449,13 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_kernel(PairArgs a, WorkArgs w
     }
 }
 
+// One cloud's index alone (as the target of pair p: no source column, no source order) — the GICP
+// source's own index for its k-NN covariances, built on buffers of its own beside the target's chain.
+__global__ __launch_bounds__(kIdxWG, 4) void index_cloud_kernel(PairArgs a, WorkArgs w) {
+    __shared__ IndexShared shu;
+    index_cloud(shu, a, w, xcd_remap(blockIdx.x, gridDim.x), true);
+}
+
 // index_refine_kernel: targets too large for the in-LDS kd build (the C5 scan-to-map submap) are
 // Morton-sorted by index_kernel, then every 8192-position chunk of that order is re-ordered as a
 // balanced kd-tree on its own (one workgroup per chunk, the same builder): superblocks and blocks —
@@ -5279,6 +5286,16 @@ hipError_t launch_index(const PairArgs& a, const WorkArgs& w, int npairs, hipStr
         hipLaunchKernelGGL(src_order_kernel, dim3(npairs), dim3(kSoWG), 0, st, a, w);
     if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32))
         hipLaunchKernelGGL(index_refine_kernel, dim3(nch, npairs), dim3(kIdxWG), 0, st, a, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_cloud(const PairArgs& a, const WorkArgs& w, int npairs, hipStream_t st) {
+    if (w.mo_hist || (w.src_by_tgt && w.kdn)) return hipErrorInvalidValue;  // (the target chain's forms)
+    hipLaunchKernelGGL(index_cloud_kernel, dim3(npairs), dim3(kIdxWG), 0, st, a, w);
+    if ((w.kd_index & 1) && w.t_stride > kKdMaxN && (w.leaf == 16 || w.leaf == 32)) {
+        const unsigned nch = (unsigned)((w.t_stride + kKdMaxN - 1) / kKdMaxN);
+        hipLaunchKernelGGL(index_refine_kernel, dim3(nch, npairs), dim3(kIdxWG), 0, st, a, w);
+    }
     return hipGetLastError();
 }
 
