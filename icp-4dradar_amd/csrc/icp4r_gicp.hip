@@ -704,10 +704,15 @@ __global__ __launch_bounds__(kGicpSliceWG) void gicp_lin_kernel(PairArgs a, Work
         if (threadIdx.x < kGicpSys) gicp_publish(part + q * kGicpSys + threadIdx.x, r);
     }
     if (!gicp_last_slice(g.cnt + p, nw, &last)) return;
+    // the slices' sums staged in LDS by all threads at once (one round trip, not one per slice), then
+    // added in slice order
+    __shared__ double stage[kGicpMaxSlices * kGicpSys];
+    for (int e = threadIdx.x; e < v.ns * kGicpSys; e += kGicpSliceWG) stage[e] = part[e];
+    __syncthreads();
     double* sys = red;  // (free again)
     if (threadIdx.x < kGicpSys) {
         double t = 0.0;
-        for (int q = 0; q < v.ns; ++q) t += part[q * kGicpSys + threadIdx.x];
+        for (int q = 0; q < v.ns; ++q) t += stage[q * kGicpSys + threadIdx.x];
         sys[threadIdx.x] = t;
     }
     __syncthreads();
@@ -784,9 +789,12 @@ __global__ __launch_bounds__(kGicpSliceWG) void gicp_trial_kernel(PairArgs a, Wo
             if (threadIdx.x < kGicpSpec) gicp_publish(part + q * kGicpSpec + threadIdx.x, r);
         }
         if (!gicp_last_slice(g.cnt + p, nw, &last)) return;
+        __shared__ double stage[kGicpMaxSlices * kGicpSpec];  // (as in the linearisation)
+        for (int e = threadIdx.x; e < ns * kGicpSpec; e += kGicpSliceWG) stage[e] = part[e];
+        __syncthreads();
         if (threadIdx.x < nt) {
             double t = 0.0;
-            for (int q = 0; q < ns; ++q) t += part[q * kGicpSpec + threadIdx.x];
+            for (int q = 0; q < ns; ++q) t += stage[q * kGicpSpec + threadIdx.x];
             err[threadIdx.x] = t;
         }
     }
