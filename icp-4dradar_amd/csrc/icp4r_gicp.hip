@@ -397,6 +397,8 @@ __global__ __launch_bounds__(kCovWG) void gicp_knn_cov_kernel(const float4* __re
 // ---- per-iteration update
 constexpr int kGicpSliceWG = 256;  // threads per slice workgroup; a slice is a multiple of it
 constexpr int kGicpSliceWaves = kGicpSliceWG / 64;
+// (the linearisation's deciding workgroup hands out its copies by thread ranges up to thread 140)
+static_assert(kGicpSliceWG >= 128 + 12 && kGicpSliceWG >= kGicpSpec * 12, "slice workgroup too small");
 
 // points per slice and slices of an n-point source: at least one slice (an empty source still
 // decides), at most kGicpMaxSlices, a slice a multiple of kGicpSliceWG points
