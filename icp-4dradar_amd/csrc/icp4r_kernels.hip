@@ -2124,8 +2124,8 @@ struct OrderShared {
 // from the per-pair work words (owork) the other workgroups published — written and read with
 // agent-scope (L1-bypassing, write-through) accesses only, so no cache can hold a stale copy.
 template <int WG, bool FUSED>
-__device__ void order_items(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int all, int ncu,
-                            OrderShared& sh) {
+__device__ __forceinline__ void order_items_body(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass,
+                                                 int all, int ncu, OrderShared& sh) {
     const int tid = threadIdx.x;
     if (tid < kOrderBuckets) sh.bcnt[tid] = 0;
     if (tid == 0) sh.tot = 0;
@@ -2185,6 +2185,13 @@ __device__ void order_items(const PairArgs& a, const WorkArgs& w, int npairs, in
             for (int k = 0, np = heavy_parts(c); k < np; ++k)
                 w.plist[atomicAdd(&boff[31 - __builtin_clz((uint32_t)heavy_size(c, k))], 1)] = (p << kPartBits) | k;
     }
+}
+// (order_items_body: inlined where a call would spill the caller's live registers — fold_update_res_kernel
+// takes its kernel arguments' addresses otherwise)
+template <int WG, bool FUSED>
+__device__ void order_items(const PairArgs& a, const WorkArgs& w, int npairs, int fitness_pass, int all, int ncu,
+                            OrderShared& sh) {
+    order_items_body<WG, FUSED>(a, w, npairs, fitness_pass, all, ncu, sh);
 }
 
 __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs w, int npairs, int fitness_pass,
@@ -3330,8 +3337,10 @@ template <> struct MomLayout<kNumericsF64> {  // Σ w·d·sᵀ [9], Σ w·s [3],
     static constexpr int N = 18, MSE = 16, CNT = 17;
 };
 
+// (solve_pair_body: always inlined — fold_update_res_kernel keeps its pair in registers across the solve,
+// and a call would spill every caller-saved one of them; solve_pair: the other kernels' call)
 template <int NUM>
-__device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
+__device__ __forceinline__ void solve_pair_body(SolveShared& sh, PairState& st, const KParams& kp) {
     constexpr int I_CNT = MomLayout<NUM>::CNT;
     const int cnt = (int)sh.mom[I_CNT];
     st.ncorr = cnt;
@@ -3402,6 +3411,10 @@ __device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
     st.conv_state = cs.state;
     if (conv) st.phase = kPhaseConverged;
     sh.flag = conv ? 2 : 0;
+}
+template <int NUM>
+__device__ void solve_pair(SolveShared& sh, PairState& st, const KParams& kp) {
+    solve_pair_body<NUM>(sh, st, kp);
 }
 
 // transformCloud(*input_transformed, *input_transformed, transformation_) by the whole workgroup.
@@ -3523,6 +3536,110 @@ __device__ __forceinline__ void fold_prio(bool hi) {
 constexpr int kSumPer = ICP4R_SUMS_PER;
 constexpr int kSumRow = 192 * kSumPer + 4;  // staged points per group (192 workers x kSumPer) + pad
 constexpr int kSumBuf = 3 * kSumRow;        // one group's staging; two alternate (double buffer)
+// The end of a pair's cached-neighbour test (pair_cache_test; res_update_pair's tail): the per-wave
+// counts and work counters, then the miss records — lv / lm in LDS (the first lcap; beyond, sq / sm)
+// — placed at their ranks in the pair's query list, or the whole list left unranked in sq / sm with
+// the bitmap when it overflowed.  Returns the pair's misses.
+template <int WG>
+__device__ __forceinline__ int test_place(const WorkArgs& w, int p, int n, int hits, int misses, uint32_t* need,
+                                          int32_t* pre, float4* lv, uint2* lm, int lcap, int32_t* wcnt, bool fitness,
+                                          uint64_t* stamp) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t xs = (int64_t)p * w.x_stride;
+    hits = wave_sum(hits);
+    misses = wave_sum(misses);
+    if (lane == 0) {
+        wcnt[wave] = misses;
+        count_add(w.evals, 0, (unsigned long long)hits);
+        count_add(w.evals, 2, (unsigned long long)hits);
+        count_add(w.evals, 3, (unsigned long long)(hits + misses));
+        if (!fitness) {  // ... of which in an update's tail
+            count_add(w.evals, 5, (unsigned long long)(hits + misses));
+            count_add(w.evals, 6, (unsigned long long)hits);
+        }
+    }
+    __syncthreads();
+    if (stamp && tid == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic: the test's end
+    int tot = 0;
+    for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
+    if (tot == 0) {
+        if (tid == 0) w.miss_cnt[p] = 0;
+        return 0;
+    }
+    const int nwords = (n + 31) >> 5;
+    if (tot > lcap) {
+        // more misses than LDS records (the few slowly converging pairs): the whole list goes to
+        // sq / sm and the bitmap to global memory, and the search places it — a read-back of the
+        // overflow here sat on this workgroup's end, which sets the update's launch time
+        for (int k = tid; k < lcap; k += WG) {
+            w.sq[xs + k] = lv[k];
+            w.sm[xs + k] = lm[k];
+        }
+        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
+        for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
+        if (tid == 0) w.miss_cnt[p] = tot | kMissUnranked;
+        return tot;
+    }
+    // Rank placement: the search reads its item's queries in sorted-position order (a run of 64
+    // consecutive ones is a compact box), so every miss record goes to its rank in the bitmap — the
+    // word's prefix + the set bits below it.  Done here, where the workgroup owns the whole bitmap,
+    // instead of in the search, where it put two barriers and three dependent global round trips in
+    // front of every work item.  Word prefixes: wave 0, kNeedWords / 64 words per lane.
+    if (wave == 0) {
+        constexpr int kW = kNeedWords / 64;
+        int c[kW], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            const int wd = lane * kW + j;
+            c[j] = wd < nwords ? __builtin_popcount(need[wd]) : 0;
+            sum += c[j];
+        }
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        int run = incl - sum;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) {
+            pre[lane * kW + j] = run;
+            run += c[j];
+        }
+    }
+    if (tid == 0) w.miss_cnt[p] = tot;
+    __syncthreads();
+    float4* qv = w.qv + xs;
+    uint2* qm = w.qm + xs;
+    auto get = [&](int k, float4& r, uint2& m) {  // (tot <= lcap: every record is in LDS)
+        k = min(k, tot - 1);
+        r = lv[k];
+        m = lm[k];
+    };
+    // (unconditional: a slot past the list re-read record tot - 1 and writes its very bytes to its
+    // very rank again)
+    auto put = [&](const float4& r, const uint2& m) {
+        const uint32_t sp = min(m.y, (uint32_t)(n - 1));
+        const int rk = pre[sp >> 5] + __builtin_popcount(need[sp >> 5] & ((1u << (sp & 31)) - 1u));
+        st_v4<1>(&qv[rk], r);
+        const uint2 mm = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
+        st_sc<1>(reinterpret_cast<uint64_t*>(&qm[rk]), (uint64_t)mm.x | ((uint64_t)mm.y << 32));
+    };
+    for (int k0 = tid; k0 < tot; k0 += 4 * WG) {
+        float4 r0, r1, r2, r3;  // (named, not an array: an array went to scratch)
+        uint2 m0, m1, m2, m3;
+        get(k0, r0, m0);  // all loads of the round first
+        get(k0 + WG, r1, m1);
+        get(k0 + 2 * WG, r2, m2);
+        get(k0 + 3 * WG, r3, m3);
+        put(r0, m0);
+        put(r1, m1);
+        put(r2, m2);
+        put(r3, m3);
+    }
+    return tot;
+}
+
 template <int WG, int kPer, bool FROM_SRC, bool SUMS = false>
 __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs& w, int p, int n, const float (&T)[16],
                                                 uint32_t* need, int32_t* pre, float4* lv, uint2* lm, int lcap,
@@ -3641,98 +3758,7 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
         sums_out[lane] = fs;
         if (lane == 0 && *sums_ok != -1) *sums_ok = 1;
     }
-    hits = wave_sum(hits);
-    misses = wave_sum(misses);
-    if (lane == 0) {
-        wcnt[wave] = misses;
-        count_add(w.evals, 0, (unsigned long long)hits);
-        count_add(w.evals, 2, (unsigned long long)hits);
-        count_add(w.evals, 3, (unsigned long long)(hits + misses));
-        if (!fitness) {  // ... of which in an update's tail
-            count_add(w.evals, 5, (unsigned long long)(hits + misses));
-            count_add(w.evals, 6, (unsigned long long)hits);
-        }
-    }
-    __syncthreads();
-    if (stamp && tid == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // diagnostic: the test's end
-    int tot = 0;
-    for (int k = 0; k < WG / 64; ++k) tot += wcnt[k];
-    if (tot == 0) {
-        if (tid == 0) w.miss_cnt[p] = 0;
-        return 0;
-    }
-    const int nwords = (n + 31) >> 5;
-    if (tot > lcap) {
-        // more misses than LDS records (the few slowly converging pairs): the whole list goes to
-        // sq / sm and the bitmap to global memory, and the search places it — a read-back of the
-        // overflow here sat on this workgroup's end, which sets the update's launch time
-        for (int k = tid; k < lcap; k += WG) {
-            w.sq[xs + k] = lv[k];
-            w.sm[xs + k] = lm[k];
-        }
-        uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
-        for (int k = tid; k < nwords; k += WG) gneed[k] = need[k];
-        if (tid == 0) w.miss_cnt[p] = tot | kMissUnranked;
-        return tot;
-    }
-    // Rank placement: the search reads its item's queries in sorted-position order (a run of 64
-    // consecutive ones is a compact box), so every miss record goes to its rank in the bitmap — the
-    // word's prefix + the set bits below it.  Done here, where the workgroup owns the whole bitmap,
-    // instead of in the search, where it put two barriers and three dependent global round trips in
-    // front of every work item.  Word prefixes: wave 0, kNeedWords / 64 words per lane.
-    if (wave == 0) {
-        constexpr int kW = kNeedWords / 64;
-        int c[kW], sum = 0;
-#pragma unroll
-        for (int j = 0; j < kW; ++j) {
-            const int wd = lane * kW + j;
-            c[j] = wd < nwords ? __builtin_popcount(need[wd]) : 0;
-            sum += c[j];
-        }
-        int incl = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += o;
-        }
-        int run = incl - sum;
-#pragma unroll
-        for (int j = 0; j < kW; ++j) {
-            pre[lane * kW + j] = run;
-            run += c[j];
-        }
-    }
-    if (tid == 0) w.miss_cnt[p] = tot;
-    __syncthreads();
-    float4* qv = w.qv + xs;
-    uint2* qm = w.qm + xs;
-    auto get = [&](int k, float4& r, uint2& m) {  // (tot <= lcap: every record is in LDS)
-        k = min(k, tot - 1);
-        r = lv[k];
-        m = lm[k];
-    };
-    // (unconditional: a slot past the list re-read record tot - 1 and writes its very bytes to its
-    // very rank again)
-    auto put = [&](const float4& r, const uint2& m) {
-        const uint32_t sp = min(m.y, (uint32_t)(n - 1));
-        const int rk = pre[sp >> 5] + __builtin_popcount(need[sp >> 5] & ((1u << (sp & 31)) - 1u));
-        st_v4<1>(&qv[rk], r);
-        const uint2 mm = make_uint2((m.x & kNtIdxMask) | (sp << kNtPosShift), m.x >> kNtPosShift);
-        st_sc<1>(reinterpret_cast<uint64_t*>(&qm[rk]), (uint64_t)mm.x | ((uint64_t)mm.y << 32));
-    };
-    for (int k0 = tid; k0 < tot; k0 += 4 * WG) {
-        float4 r0, r1, r2, r3;  // (named, not an array: an array went to scratch)
-        uint2 m0, m1, m2, m3;
-        get(k0, r0, m0);  // all loads of the round first
-        get(k0 + WG, r1, m1);
-        get(k0 + 2 * WG, r2, m2);
-        get(k0 + 3 * WG, r3, m3);
-        put(r0, m0);
-        put(r1, m1);
-        put(r2, m2);
-        put(r3, m3);
-    }
-    return tot;
+    return test_place<WG>(w, p, n, hits, misses, need, pre, lv, lm, lcap, wcnt, fitness, stamp);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -4190,7 +4216,11 @@ __device__ __forceinline__ void fold_pass_b(const KParams& kp, const FoldIn& f, 
 #pragma unroll
                 for (int e = 0; e < kPerB; ++e) {
                     const int i = ch.c0 + min(tid - 64 + e * kFillB, ch.len - 1);
+#ifdef ICP4R_DIAG_REVB  // (timing diagnostic only: pass B reads the points last to first — wrong results)
+                    rec(n - 1 - i, r[e][0], r[e][1]);
+#else
                     rec(i, r[e][0], r[e][1]);
+#endif
                 }
             };
             auto store_b = [&](int c, const Chunk& ch, float4 (&r)[kPerB][2]) __attribute__((always_inline)) {
@@ -4523,7 +4553,10 @@ __device__ __forceinline__ int fold_update_pair(const PairArgs& a, const WorkArg
 // statement's "memory" clobber keeps the compiler from moving the store past the add.  An acq_rel add
 // would instead put an L2 write-back (buffer_wbl2) in every workgroup — 1.7-6.5 us each by the same
 // section's price list — for an ordering the sc1 accesses already give.
-__global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test, int order_ncu) {
+#ifndef ICP4R_UPD_OCC
+#define ICP4R_UPD_OCC 4  // (experiment) workgroups per CU of fold_update_kernel: 4, 3 or 2
+#endif
+__global__ __launch_bounds__(kFoldWG, ICP4R_UPD_OCC) void fold_update_kernel(PairArgs a, WorkArgs w, int tail_test, int order_ncu) {
     __shared__ FoldShared sh;
     __shared__ OrderShared osh;
     __shared__ int32_t last;
@@ -4539,6 +4572,395 @@ __global__ __launch_bounds__(kFoldWG, 4) void fold_update_kernel(PairArgs a, Wor
     __syncthreads();
     if (!last) return;
     order_items<kFoldWG, true>(a, w, (int)gridDim.x, 0, 0, order_ncu, osh);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fold_update_res_kernel (round 6): the batched update with the pair's points read from HBM once and
+// held on chip across pass A, pass B and the fused test.  fold_update_kernel streams X and nn_t three
+// times per launch (pass A, pass B, the tail: 1.01 GB for 268 MB of clouds at C3); here a 256-thread
+// workgroup holds its pair's 8192 points — X_i.xyz and its NN's xyz in registers (thread t, column j:
+// point t + 256 j; 192 VGPRs), L_i = X_i.w in LDS — two workgroups per CU:
+//  pass A: each column is staged from registers into two LDS rows buffers, wave 0 lanes 0..6 fold the
+//          seven sequential float chains (Σs, Σd, Σw) over them; |C| is a reduction, and the MSE sum
+//          (when a criterion is live) its exact integer form per thread (fold_update_kernel's argument),
+//          with PCL's sequential double chain as the fallback;
+//  pass B: Eigen's panels side by side (fold_pass_b<PAR>'s arithmetic): every thread writes the
+//          products of its points that fall into the chunk's steps (a point's step = its rank among
+//          the accepted correspondences mod kc) into the panel rows, 117 fold lanes sum them;
+//  tail:   the next pass's cached-neighbour test from the registers (X, L, the NN's coordinates), U
+//          read once; a miss's tag (nn_t.w: positions) read for the misses only.
+// Per point and iteration: X and nn_t read (32 B), U read (4 B), X and U written (20 B) — the
+// one-read bytes.  Results are bit-identical to fold_update_kernel (the parity tests run both).
+constexpr int kResWG = 256;
+constexpr int kResCols = kResMaxN / kResWG;  // points per thread: column j = points [256 j, 256 j + 256)
+constexpr int kResRowA = kResWG + kFoldPad;  // a pass-A chain row (one column) + pad
+constexpr int kResStage = 10240;             // staging floats (40 KB): pass A rows, pass B panel rows, the MSE
+                                             // fallback's doubles, the tail's bitmap, prefixes and records
+constexpr int kResRecs = ((kResStage - 2 * kNeedWords) * 4 / 24) & ~15;  // the tail's LDS miss records
+static_assert(kResMaxN == kResWG * kResCols, "columns");
+static_assert(2 * 7 * kResRowA <= kResStage, "pass A rows");
+struct ResShared {
+    float L[kResMaxN];  // X_i.w: the test's lower bounds
+    alignas(16) float stage[kResStage];
+    float res[8];
+    int32_t cnt[kResWG / 64];
+    uint64_t mse_s[kResWG / 64];
+    int32_t mse_e[kResWG / 64];
+    int32_t mcount;
+    SolveShared s;
+};
+
+__device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs& w, int tail_test, int p,
+                                               ResShared& sh) {
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.src_n[p];  // <= kResMaxN (launch_update)
+    clear_need(w, p, n, tid, kResWG);
+    const int64_t xs = (int64_t)p * w.x_stride;
+    const float4* Xp = w.X + xs;
+    const float4* NT = w.nn_t + xs;
+    const KParams& kp = a.kp;
+    const bool mse = kp.need_mse != 0;
+    const int ncol = (n + kResWG - 1) / kResWG;
+    float* const buf = sh.stage;
+#if ICP4R_WG_TICKS  // diagnostic build: every pair's phase stamps in its 10th update (tools/experiments/wg_ticks.py)
+    uint64_t* wt = (w.ticks && tid == 0 && st.iterations == 9) ? w.ticks + 32 + 4 * (int64_t)gridDim.x + 8 * (int64_t)p
+                                                              : nullptr;
+#define RES_TICK(k) \
+    if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RES_TICK(k)
+#endif
+    RES_TICK(0);
+
+    // the pair, read once (8 columns' loads in flight at a time: all 64 at once would need 256 registers
+    // of load destinations)
+    float px[kResCols], py[kResCols], pz[kResCols], qx[kResCols], qy[kResCols], qz[kResCols];
+    constexpr int kLB = 8;
+#pragma unroll
+    for (int j0 = 0; j0 < kResCols; j0 += kLB) {
+        float4 v[kLB], t[kLB];
+#pragma unroll
+        for (int e = 0; e < kLB; ++e) {
+            const int i = min(tid + kResWG * (j0 + e), n - 1);
+            if (j0 + e < ncol) {
+                v[e] = Xp[i];
+                t[e] = NT[i];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kLB; ++e) {
+            const int j = j0 + e;
+            if (j < ncol) {
+                px[j] = v[e].x;
+                py[j] = v[e].y;
+                pz[j] = v[e].z;
+                qx[j] = t[e].x;
+                qy[j] = t[e].y;
+                qz[j] = t[e].z;
+                sh.L[tid + kResWG * j] = v[e].w;  // (past n: point n - 1's, never read)
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    RES_TICK(7);
+    // ---- pass A: column j staged into buffer j & 1 (rows Σs.xyz, Σd.xyz, Σw), wave 0 lanes 0..6 fold
+    int cnt = 0;
+    uint64_t ms_s = 0;
+    int ms_e = INT_MAX;
+    auto stage_a = [&](int j) __attribute__((always_inline)) {
+        const int i = tid + kResWG * j;
+        if (i >= n) return;
+        float* b = buf + (j & 1) * 7 * kResRowA + tid;
+        const float d2 = l2_simple(px[j], py[j], pz[j], qx[j], qy[j], qz[j]);
+        const bool ok = !(d2 > kp.max_d2);  // (max_d2 = FLT_MAX: only an overflowing d² is rejected)
+        b[0] = ok ? px[j] : -0.0f;
+        b[kResRowA] = ok ? py[j] : -0.0f;
+        b[2 * kResRowA] = ok ? pz[j] : -0.0f;
+        b[3 * kResRowA] = ok ? qx[j] : -0.0f;
+        b[4 * kResRowA] = ok ? qy[j] : -0.0f;
+        b[5 * kResRowA] = ok ? qz[j] : -0.0f;
+        b[6 * kResRowA] = ok ? 1.0f : 0.0f;
+        cnt += ok ? 1 : 0;
+        if (mse) lane_exact_add(ok ? (double)d2 : 0.0, ms_s, ms_e);
+    };
+    float acc = (lane < 6) ? -0.0f : 0.0f;  // Eigen's rowwise().sum() from the first element; Σw from 0
+    if (ncol > 0) stage_a(0);
+#pragma unroll
+    for (int j = 0; j < kResCols; ++j) {
+        if (j < ncol) {
+            __syncthreads();  // column j staged; buffer (j + 1) & 1 folded (column j - 1)
+            if (wave == 0 && lane < 7)
+                acc = fold_row(buf + ((j & 1) * 7 + lane) * kResRowA, min(kResWG, n - j * kResWG), acc);
+            if (j + 1 < ncol) stage_a(j + 1);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (mse) wave_exact_total(ms_s, ms_e);
+    if (lane == 0) {
+        sh.cnt[wave] = cnt;
+        sh.mse_s[wave] = ms_s;
+        sh.mse_e[wave] = ms_e;
+    }
+    if (wave == 0 && lane < 7) sh.res[lane] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        int total = 0;
+        for (int k = 0; k < kResWG / 64; ++k) total += sh.cnt[k];
+        sh.s.mom[0] = (double)total;
+        // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
+        const float one_over_n = 1.0f / sh.res[6];
+        sh.s.one_over_n = one_over_n;
+        for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
+        double msum = 0.0;  // (0 without an MSE criterion: not used then)
+        if (mse) {  // the waves' exact sums combined (-1: the terms span more than 53 bits)
+            int e = INT_MAX;
+            for (int k = 0; k < kResWG / 64; ++k) e = min(e, sh.mse_e[k]);
+            uint64_t t = 0;
+            for (int k = 0; k < kResWG / 64; ++k)
+                t = min(t + (sh.mse_e[k] == INT_MAX ? 0 : exact_rescale(sh.mse_s[k], sh.mse_e[k] - e)), kExactSat);
+            msum = t >= kExactSat ? -1.0 : (e == INT_MAX ? 0.0 : ldexp((double)t, e));
+        }
+        sh.s.mse_sum = msum;
+    }
+    __syncthreads();
+    if (mse && sh.s.mse_sum < 0.0) {
+        // (rare) the terms span more than 53 bits: PCL's sequential double chain (calculateMSE) over the
+        // points' d² (rejected: +0, which changes no partial sum), re-read from HBM a column at a time so
+        // that no register of the held pair is needed; thread 0 adds them in order
+        double* db = reinterpret_cast<double*>(buf);
+        double dacc = 0.0;
+        for (int c = 0; c < ncol; ++c) {
+            const int i = c * kResWG + tid;
+            if (i < n) {
+                const float4 v = Xp[i], t = NT[i];
+                const float d2 = l2_simple(v.x, v.y, v.z, t.x, t.y, t.z);
+                db[tid] = (double)(!(d2 > kp.max_d2) ? d2 : 0.0f);
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int k = 0, len = min(kResWG, n - c * kResWG); k < len; ++k) dacc = dacc + db[k];
+            __syncthreads();
+        }
+        if (tid == 0) sh.s.mse_sum = dacc;
+        __syncthreads();
+    }
+
+    RES_TICK(1);
+    // ---- pass B: sigma in Eigen's panel order, the panels side by side (fold_pass_b<PAR>'s arithmetic)
+    const int cntA = (int)sh.s.mom[0];
+    if (cntA < n) {
+        // (rare: an overflowing d² was rejected) panel starts by rank: fold_pass_b over X and nn_t re-read
+        // from HBM, no register of the held pair needed
+        const FoldIn fin{nullptr, Xp, NT, n};
+        static_assert(2 * 9 * kFoldRow <= kResStage, "fold_pass_b buffers");
+        fold_pass_b<kResWG, kFoldChunkP, kFoldRow, false>(kp, fin, reinterpret_cast<float(*)[9][kFoldRow]>(buf), sh.s);
+    } else {
+        const float oon = sh.s.one_over_n;
+        const int kc = sigma_kc(cntA, kp.sigma_max_kc);
+        const int S = (cntA > 0 && kc > 0) ? (cntA + kc - 1) / kc : 1;
+        float sig = 0.0f;  // wave 0 lanes 0..8: sigma(a, b), the panels added in order
+        for (int s0 = 0; s0 < S; s0 += kSliceGroup) {
+            const int G = min(kSliceGroup, S - s0);
+            const int R = 9 * G;                                   // fold chains of the group
+            const int stride = (((kResStage / R) - 4) & ~7) + 4;  // one buffer: rows of T steps, ≡ 4 mod 8
+            const int T = stride - 4;
+            const int r0 = s0 * kc;                                // the group's first point (rank = index)
+            const int r1 = min((s0 + G) * kc, n);
+            const int nch = (min(kc, r1 - r0) + T - 1) / T;
+            // fold lane L = sl * 9 + ab: the chain of panel s0 + sl, coefficient ab
+            const int my_len = tid < R ? min(kc, n - (s0 + tid / 9) * kc) : 0;
+            // point t + 256 j's (panel, step) in the group, carried from column to column (kc >= 256: one
+            // wrap at most per column; smaller kc, the loop)
+            float accp = 0.0f;
+            for (int c = 0; c < nch; ++c) {
+                const int w0 = c * T;  // the chunk's first step
+                // the means, re-read per chunk as wave-uniform (SGPR) values: hoisted out of the chunk
+                // loop, the 6 x 32 demeaned coordinates had gone to scratch
+                float mv[6];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    mv[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.s.mean[k])));
+                    asm volatile("" : "+s"(mv[k]));
+                }
+                const float ms0 = mv[0], ms1 = mv[1], ms2 = mv[2], md0 = mv[3], md1 = mv[4], md2 = mv[5];
+                int sl = 0, st = tid - r0;
+                while (st < 0) { st += kc; --sl; }
+                while (st >= kc) { st -= kc; ++sl; }
+                // every thread writes the products of its points whose step lies in [w0, w0 + T)
+#pragma unroll
+                for (int j = 0; j < kResCols; ++j) {
+                    if (j < ncol) {
+                        const int tt = st - w0;
+                        if (sl >= 0 && sl < G && (unsigned)tt < (unsigned)T && tid + kResWG * j < r1) {
+                            const float sv0 = px[j] - ms0, sv1 = py[j] - ms1, sv2 = pz[j] - ms2;
+                            const float dv0 = qx[j] - md0, dv1 = qy[j] - md1, dv2 = qz[j] - md2;
+                            float* o = buf + sl * 9 * stride + tt;
+                            o[0] = dv0 * sv0;
+                            o[stride] = dv0 * sv1;
+                            o[2 * stride] = dv0 * sv2;
+                            o[3 * stride] = dv1 * sv0;
+                            o[4 * stride] = dv1 * sv1;
+                            o[5 * stride] = dv1 * sv2;
+                            o[6 * stride] = dv2 * sv0;
+                            o[7 * stride] = dv2 * sv1;
+                            o[8 * stride] = dv2 * sv2;
+                        }
+                        st += kResWG;
+                        while (st >= kc) {
+                            st -= kc;
+                            ++sl;
+                        }
+                    }
+                }
+                __syncthreads();  // the chunk staged
+                if (tid < R) {
+                    const int len = min(T, my_len - w0);
+                    if (len > 0) accp = fold_row(buf + tid * stride, len, accp);
+                }
+                __syncthreads();  // the chunk folded: the buffer is free
+            }
+            if (tid < R) buf[tid] = accp;
+            __syncthreads();
+            if (wave == 0 && lane < 9)
+                for (int sl = 0; sl < G; ++sl) sig = sig + oon * buf[sl * 9 + lane];  // res += alpha * C0
+            __syncthreads();
+        }
+        if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sig;
+    }
+
+    RES_TICK(2);
+    // ---- the solve (thread 0), the tail's bitmap cleared meanwhile
+    const bool tail = tail_test && w.nn_u;
+    uint32_t* need = reinterpret_cast<uint32_t*>(buf);  // (pass B's buffers are free)
+    int32_t* pre = reinterpret_cast<int32_t*>(need + kNeedWords);
+    float4* lv = reinterpret_cast<float4*>(pre + kNeedWords);
+    uint2* lm = reinterpret_cast<uint2*>(lv + kResRecs);
+    static_assert(2 * kNeedWords * 4 + kResRecs * 24 <= kResStage * 4, "tail records");
+    if (tail) {
+        for (int k = tid; k < ((n + 31) >> 5); k += kResWG) need[k] = 0u;
+        if (tid == 0) sh.mcount = 0;
+    }
+    __syncthreads();  // (sigmaf, and pass B's last reads of the buffer)
+    if (tid == 0) solve_pair_body<kNumericsPCL>(sh.s, st, kp);
+    __syncthreads();
+    RES_TICK(3);
+    if (sh.s.flag != 0 || !tail) return 0;  // error, converged, or no further pass
+
+    // ---- tail: the next pass's cached-neighbour test (pair_cache_test's arithmetic)
+    float T[16];  // (wave-uniform: SGPR operands of the transform)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) T[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.s.T_inc[q])));
+    float* uu = w.nn_u + xs;
+    float4* X = w.X + xs;
+    float4* sqg = w.sq + xs;
+    uint2* smg = w.sm + xs;
+    int hits = 0, misses = 0;
+    constexpr int kUB = 4;  // U loads in flight (one batch ahead)
+    float ua[kUB], ub[kUB];
+    auto load_u = [&](int j0, float (&u)[kUB]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < kUB; ++e) u[e] = (j0 + e < ncol) ? uu[min(tid + kResWG * (j0 + e), n - 1)] : 0.0f;
+    };
+    auto test = [&](int j, float U) __attribute__((always_inline)) {
+        const int i = tid + kResWG * j;
+        const bool valid = i < n;
+        float ox, oy, oz;
+        xform_pt(T, px[j], py[j], pz[j], ox, oy, oz);  // PCL transformCloud, in place
+        const float2 Lm = move_lu(make_float2(sh.L[i], U), px[j], py[j], pz[j], ox, oy, oz);
+        const float d2 = l2_simple(ox, oy, oz, qx[j], qy[j], qz[j]);
+        const bool hit = valid & cache_hit(Lm.x, d2);
+        if (valid) {
+            st_v4<1>(&X[i], make_float4(ox, oy, oz, Lm.x));
+            st_sc<1>(&uu[i], Lm.y);
+        }
+        const bool miss = valid && !hit;
+        const int k = wave_append(miss, &sh.mcount);
+        if (hit) {
+            ++hits;
+        } else if (miss) {  // the record without its positions (nn_t.w: read below, for the misses only)
+            if (k < kResRecs) {
+                lv[k] = make_float4(ox, oy, oz, Lm.y);
+                lm[k] = make_uint2((uint32_t)i, 0u);
+            } else {
+                sqg[k] = make_float4(ox, oy, oz, Lm.y);
+                smg[k] = make_uint2((uint32_t)i, 0u);
+            }
+            ++misses;
+        }
+    };
+    load_u(0, ua);
+#pragma unroll
+    for (int jb = 0; jb < kResCols; jb += 2 * kUB) {
+        if (jb + kUB < kResCols) load_u(jb + kUB, ub);
+#pragma unroll
+        for (int e = 0; e < kUB; ++e)
+            if (jb + e < ncol) test(jb + e, ua[e]);
+        if (jb + 2 * kUB < kResCols) load_u(jb + 2 * kUB, ua);
+#pragma unroll
+        for (int e = 0; e < kUB; ++e)
+            if (jb + kUB + e < ncol) test(jb + kUB + e, ub[e]);
+    }
+    RES_TICK(6);
+    // every record appended: the overflow records' stores drained before the barrier (another wave
+    // reads them back below, with L1-bypassing loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the misses' positions: nn_t.w (the NN's sorted target position | the query's sorted position)
+    const int tot = sh.mcount;
+    for (int k0 = tid; k0 < tot; k0 += 4 * kResWG) {
+        uint32_t ii[4];
+        float tg[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = min(k0 + e * kResWG, tot - 1);
+            ii[e] = k < kResRecs ? lm[k].x
+                                 : __hip_atomic_load(reinterpret_cast<uint32_t*>(smg + k), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+            ii[e] = min(ii[e], (uint32_t)(n - 1));  // (a record's index is below n)
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tg[e] = NT[ii[e]].w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = k0 + e * kResWG;
+            if (k >= tot) break;
+            const uint32_t sp = nt_pos(tg[e]);
+            atomicOr(&need[sp >> 5], 1u << (sp & 31));
+            const uint2 m = make_uint2(ii[e] | (nt_tpos(tg[e]) << kNtPosShift), sp);
+            if (k < kResRecs)
+                lm[k] = m;
+            else
+                smg[k] = m;
+        }
+    }
+    const int tp = test_place<kResWG>(w, p, n, hits, misses, need, pre, lv, lm, kResRecs, sh.cnt, false, nullptr);
+    RES_TICK(4);
+#undef RES_TICK
+    return tp;
+}
+
+__global__ __launch_bounds__(kResWG, 2) void fold_update_res_kernel(PairArgs a, WorkArgs w, int tail_test,
+                                                                     int order_ncu) {
+    __shared__ ResShared sh;
+    __shared__ OrderShared osh;
+    __shared__ int32_t last;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    const int nwork = res_update_pair(a, w, tail_test, p, sh);
+    if (order_ncu <= 0) return;
+    // the next pass's work list by the launch's last workgroup (fold_update_kernel's hand-off)
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(w.owork + p, nwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(w.plist_n + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (old + 1) % (int)gridDim.x == 0 ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    order_items_body<kResWG, true>(a, w, (int)gridDim.x, 0, 0, order_ncu, osh);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -5394,8 +5816,14 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
         if (wide && !tail_test && order_ncu <= 0)
             hipLaunchKernelGGL(fold_update_wide_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+        else if (w.res_update && !need_corr && !w.corr && max_n <= kResMaxN && w.nn_t && w.nn_u && w.defer_xform &&
+                 a.kp.huber_delta == INFINITY && a.kp.max_d2 >= FLT_MAX &&
+                 !w.sums_tail && (!tail_test || (w.sq && w.sm && w.need && w.miss_cnt)))
+            hipLaunchKernelGGL(fold_update_res_kernel, dim3(npairs), dim3(kResWG), 0, st, a, w, tail_test, order_ncu);
         else
-            hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG), 0, st, a, w, tail_test, order_ncu);
+            hipLaunchKernelGGL(fold_update_kernel, dim3(npairs), dim3(kFoldWG),
+                               ICP4R_UPD_OCC >= 4 ? 0 : (ICP4R_UPD_OCC == 3 ? 12000 : 20000), st, a, w, tail_test,
+                               order_ncu);
     } else {
         hipLaunchKernelGGL(update_f64_kernel, dim3(npairs), dim3(kUpdWG), 0, st, a, w);
     }

@@ -69,7 +69,7 @@ __device__ __forceinline__ void xform_pt(const float* T, float x, float y, float
     oz = a2;
 }
 
-__device__ inline void mat4_mul_f(const float* A, const float* B, float* C) {
+__device__ __forceinline__ void mat4_mul_f(const float* A, const float* B, float* C) {
     float R[16];
     for (int j = 0; j < 4; ++j)
         for (int i = 0; i < 4; ++i) {
@@ -82,7 +82,7 @@ __device__ inline void mat4_mul_f(const float* A, const float* B, float* C) {
     for (int k = 0; k < 16; ++k) C[k] = R[k];
 }
 
-__device__ inline void mat4_identity(float* T) {
+__device__ __forceinline__ void mat4_identity(float* T) {
     for (int k = 0; k < 16; ++k) T[k] = (k % 5 == 0) ? 1.0f : 0.0f;
 }
 
@@ -318,7 +318,7 @@ __host__ __device__ __forceinline__ void svd_swap_f32(float (&S)[3], float (&U)[
 
 // JacobiSVD<Matrix3f>(A, ComputeFullU | ComputeFullV); A, U, V row-major.  Returns false (U = V = I,
 // S = 0) for a non-finite A (Eigen: InvalidInput).
-__host__ __device__ inline bool eigen_jacobi_svd3_f32(const float (&A)[9], float (&U)[9], float (&S)[3], float (&V)[9]) {
+__host__ __device__ __forceinline__ bool eigen_jacobi_svd3_f32(const float (&A)[9], float (&U)[9], float (&S)[3], float (&V)[9]) {
     float scale = fabsf(A[0]);
 #pragma unroll
     for (int k = 1; k < 9; ++k) scale = scale < fabsf(A[k]) ? fabsf(A[k]) : scale;
@@ -365,7 +365,7 @@ __host__ __device__ inline bool eigen_jacobi_svd3_f32(const float (&A)[9], float
 }
 
 // Eigen::umeyama's rotation (with_scaling = false), Scalar = float; sigma and R row-major.
-__host__ __device__ inline void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
+__host__ __device__ __forceinline__ void umeyama_rotation_f32_reg(const float (&A)[9], float (&R)[9]) {
     float U[9], S[3], V[9];
     eigen_jacobi_svd3_f32(A, U, S, V);
     float d2 = 1.0f;
@@ -399,7 +399,7 @@ struct ConvState {
 };
 
 // returns 1 when converged; updates prev_mse only on the no-criterion path (upstream early returns)
-__device__ inline int has_converged(const ConvParams& p, int32_t iterations, const float* Tinc, double mse,
+__device__ __forceinline__ int has_converged(const ConvParams& p, int32_t iterations, const float* Tinc, double mse,
                                     ConvState& cs) {
     cs.state = 0;
     if (iterations >= p.max_iterations) {

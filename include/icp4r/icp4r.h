@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ICP4R_ABI_VERSION 5
+#define ICP4R_ABI_VERSION 6
 
 typedef enum icp4r_status {
     ICP4R_OK = 0,
@@ -261,6 +261,11 @@ typedef struct icp4r_plan_info {
     int32_t wide_update; /* 1: the PCL-numerics update runs one 1024-thread workgroup per pair
                            (fold_update_wide_kernel: at most one pair per CU, no fused cache
                            test, PCL numerics); off with plan option wide_update = 0    */
+    int32_t res_update; /* 1 (ABI 6): the batched plan's update holds each pair on chip
+                           (fold_update_res_kernel: the fused cache test, sources <= 8192,
+                           PCL numerics) for unweighted registrations without a distance
+                           threshold (PCL's defaults; the others take fold_update_kernel);
+                           off with plan option res_update = 0                        */
 } icp4r_plan_info;
 /* ctx: whose plan options and CU count apply (NULL: the defaults and 256 CUs); numerics:
  * ICP4R_NUMERICS_PCL / _F64, as icp4r_params.numerics. */

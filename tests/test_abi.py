@@ -77,7 +77,7 @@ def test_params_default_matches_pcl():
     assert math.isinf(p.huber_delta)
     assert p.fitness_max_range == sys.float_info.max
     L = icp4r.load()
-    assert L.icp4r_abi_version() == 5
+    assert L.icp4r_abi_version() == 6
     assert b"gfx950" in L.icp4r_version()
 
 
@@ -144,6 +144,13 @@ def test_plan_geometry():
         assert not plan(1024, 8192, 8192)["wide_update"]
         ctx.set_plan_option("wide_update", 0)
         assert not plan(1, 8192, 8192)["wide_update"]
+        # the on-chip batched update: the batched plan with its fused test, sources <= 8192
+        ctx.set_plan_option("res_update", 1)
+        assert plan(1024, 8192, 8192)["res_update"] and not plan(1024, 8193, 8192)["res_update"]
+        assert not plan(1, 8192, 8192)["res_update"]
+        assert not plan(1024, 8192, 8192, numerics=icp4r.NUMERICS_F64)["res_update"]
+        ctx.set_plan_option("res_update", 0)
+        assert not plan(1024, 8192, 8192)["res_update"]
         # without a context: the defaults
         assert icp4r.plan(1, 8192, 8192) == icp4r.plan(1, 8192, 8192, ctx=icp4r.Context(icp4r.NO_DEVICE))
     finally:

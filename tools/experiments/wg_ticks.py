@@ -86,6 +86,10 @@ def main():
     if (t6 > 0).all():  # the tail split at the test's end: the test, then the misses' rank placement
         out["tail_test"] = pct(t6 - t[:, 3])
         out["tail_place"] = pct(t[:, 4] - t6)
+    t7 = raw[ok, 7].astype(np.int64).astype(np.float64) * 0.01
+    if (t7 > 0).all():  # fold_update_res_kernel: pass A split at the end of the pair's loads
+        out["load"] = pct(t7 - t[:, 0])
+        out["passA_folds"] = pct(t[:, 1] - t7)
     out["total"] = pct(t[:, 4] - t[:, 0])
     print(json.dumps(out))
     ctx.close()
