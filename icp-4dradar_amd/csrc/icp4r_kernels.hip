@@ -4578,29 +4578,34 @@ __global__ __launch_bounds__(kFoldWG, ICP4R_UPD_OCC) void fold_update_kernel(Pai
 // fold_update_res_kernel (round 6): the batched update with the pair's points read from HBM once and
 // held on chip across pass A, pass B and the fused test.  fold_update_kernel streams X and nn_t three
 // times per launch (pass A, pass B, the tail: 1.01 GB for 268 MB of clouds at C3); here a 256-thread
-// workgroup holds its pair's 8192 points — X_i.xyz and its NN's xyz in registers (thread t, column j:
-// point t + 256 j; 192 VGPRs), L_i = X_i.w in LDS — two workgroups per CU:
-//  pass A: each column is staged from registers into two LDS rows buffers, wave 0 lanes 0..6 fold the
-//          seven sequential float chains (Σs, Σd, Σw) over them; |C| is a reduction, and the MSE sum
-//          (when a criterion is live) its exact integer form per thread (fold_update_kernel's argument),
-//          with PCL's sequential double chain as the fallback;
+// workgroup holds its pair's <= 8192 points — thread t, column j: point t + 256 j — two workgroups per
+// CU: X_i.xyz and the NN's x, y in registers (160 VGPRs), the NN's z and L_i = X_i.w in LDS (L rounded
+// down to half precision: a lower bound stays a lower bound, so the cached-neighbour test stays exact —
+// a miss is searched — and every result is unchanged).
+//  loads:  8 columns' X and nn_t in flight at a time, one batch ahead of pass A's folds;
+//  pass A: two columns at a time staged from registers into LDS rows, wave 0 lanes 0..6 fold the seven
+//          sequential float chains (Σs, Σd, Σw) over them; |C| is a reduction, and the MSE sum (when a
+//          criterion is live) its exact integer form per thread (fold_update_kernel's argument), with
+//          PCL's sequential double chain over re-read points as the fallback;
 //  pass B: Eigen's panels side by side (fold_pass_b<PAR>'s arithmetic): every thread writes the
-//          products of its points that fall into the chunk's steps (a point's step = its rank among
-//          the accepted correspondences mod kc) into the panel rows, 117 fold lanes sum them;
-//  tail:   the next pass's cached-neighbour test from the registers (X, L, the NN's coordinates), U
-//          read once; a miss's tag (nn_t.w: positions) read for the misses only.
+//          products of its points whose step (index mod kc) falls into the chunk into the panel rows,
+//          117 fold lanes sum them (a correspondence rejected for an overflowing d²: fold_pass_b over
+//          re-read points);
+//  tail:   the next pass's cached-neighbour test from the held points, U read once; a miss's tag
+//          (nn_t.w: positions) read for the misses only.
 // Per point and iteration: X and nn_t read (32 B), U read (4 B), X and U written (20 B) — the
 // one-read bytes.  Results are bit-identical to fold_update_kernel (the parity tests run both).
 constexpr int kResWG = 256;
 constexpr int kResCols = kResMaxN / kResWG;  // points per thread: column j = points [256 j, 256 j + 256)
-constexpr int kResRowA = kResWG + kFoldPad;  // a pass-A chain row (one column) + pad
-constexpr int kResStage = 10240;             // staging floats (40 KB): pass A rows, pass B panel rows, the MSE
-                                             // fallback's doubles, the tail's bitmap, prefixes and records
+constexpr int kResRowA = kResWG + kFoldPad;  // pass A: one column per chunk
+constexpr int kResStage = 7680;              // staging floats (30 KB): pass A rows, pass B panel rows, the
+                                             // fallbacks' buffers, the tail's bitmap, prefixes and records
 constexpr int kResRecs = ((kResStage - 2 * kNeedWords) * 4 / 24) & ~15;  // the tail's LDS miss records
-static_assert(kResMaxN == kResWG * kResCols, "columns");
+static_assert(kResMaxN == kResWG * kResCols && kResCols % 8 == 0 && kResCols <= 32, "columns");
 static_assert(2 * 7 * kResRowA <= kResStage, "pass A rows");
 struct ResShared {
-    float L[kResMaxN];  // X_i.w: the test's lower bounds
+    float qz[kResMaxN];     // the NN's z
+    _Float16 L[kResMaxN];   // X_i.w rounded down: the test's lower bounds
     alignas(16) float stage[kResStage];
     float res[8];
     int32_t cnt[kResWG / 64];
@@ -4609,6 +4614,113 @@ struct ResShared {
     int32_t mcount;
     SolveShared s;
 };
+
+#ifndef ICP4R_RES_LB
+#define ICP4R_RES_LB 4  // columns' loads in flight at a time
+#endif
+#ifndef ICP4R_RES_FOLD
+#define ICP4R_RES_FOLD fold_row  // pass A's fold (fold_row8 / fold_row3: fewer / more registers)
+#endif
+typedef float fcols __attribute__((ext_vector_type(kResCols)));  // one coordinate of a thread's columns
+typedef uint32_t ucols __attribute__((ext_vector_type(kResCols)));
+__device__ __forceinline__ int uni(int j) { return __builtin_amdgcn_readfirstlane(j); }
+
+// x rounded toward -inf to half precision (a lower bound stays one)
+__device__ __forceinline__ _Float16 half_down(float x) {
+    _Float16 h = (_Float16)x;
+    if ((float)h > x) {
+        uint16_t b = __builtin_bit_cast(uint16_t, h);
+        b = (b & 0x8000u) ? (uint16_t)(b + 1) : (b == 0 ? (uint16_t)0x8001u : (uint16_t)(b - 1));
+        h = __builtin_bit_cast(_Float16, b);
+    }
+    return h;
+}
+
+// fold_row with three register sets of 16 in rotation (two groups' loads in flight while one is summed)
+__device__ __forceinline__ float fold_row3(const float* f, int len, float acc) {
+    int k = 0;
+    if (len >= 48) {
+        float4 a[4], b[4], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + 16 + 4 * u);
+        for (; k + 48 <= len; k += 48) {
+            // the loads past this round re-read group 0 harmlessly when nothing follows
+            const int n1 = (k + 64 <= len) ? k + 48 : 0, n2 = (k + 80 <= len) ? k + 64 : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const float4*>(f + k + 32 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = chain_add4(acc, a[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = *reinterpret_cast<const float4*>(f + n1 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = chain_add4(acc, b[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(f + n2 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = chain_add4(acc, c[u]);
+        }
+        // a, b hold [k, k + 16) and [k + 16, k + 32) when they exist
+        if (k + 16 <= len) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = chain_add4(acc, a[u]);
+            k += 16;
+            if (k + 16 <= len) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc = chain_add4(acc, b[u]);
+                k += 16;
+            }
+        }
+    }
+    return k < len ? fold_row(f + k, len - k, acc) : acc;
+}
+
+// A chain's step over an LDS row (16-B aligned) with three register sets of 8 in rotation (two groups'
+// loads in flight while one is summed): 24 registers — the on-chip update's fold lane shares its wave's
+// allocation with the held points
+__device__ __forceinline__ float fold_row8(const float* f, int len, float acc) {
+    int k = 0;
+    if (len >= 24) {
+        float4 a[2], b[2], c[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) a[u] = *reinterpret_cast<const float4*>(f + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) b[u] = *reinterpret_cast<const float4*>(f + 8 + 4 * u);
+        for (; k + 24 <= len; k += 24) {
+            const int n1 = (k + 32 <= len) ? k + 24 : 0, n2 = (k + 40 <= len) ? k + 32 : 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) c[u] = *reinterpret_cast<const float4*>(f + k + 16 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) acc = chain_add4(acc, a[u]);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) a[u] = *reinterpret_cast<const float4*>(f + n1 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) acc = chain_add4(acc, b[u]);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) b[u] = *reinterpret_cast<const float4*>(f + n2 + 4 * u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) acc = chain_add4(acc, c[u]);
+        }
+        if (k + 8 <= len) {  // a holds [k, k + 8)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) acc = chain_add4(acc, a[u]);
+            k += 8;
+            if (k + 8 <= len) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) acc = chain_add4(acc, b[u]);
+                k += 8;
+            }
+        }
+    }
+    return k < len ? fold_tail<float>(f + k, len - k, acc) : acc;
+}
 
 __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs& w, int tail_test, int p,
                                                ResShared& sh) {
@@ -4629,73 +4741,93 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
                                                               : nullptr;
 #define RES_TICK(k) \
     if (wt) wt[k] = __builtin_amdgcn_s_memrealtime()
+    // pair 0's finer stamps (pass A per column, pass B per chunk) after every pair's 8 slots
+    uint64_t* wx = (wt && p == 0) ? w.ticks + 32 + 12 * (int64_t)gridDim.x : nullptr;
+#define RES_TICKX(k) \
+    if (wx) wx[k] = __builtin_amdgcn_s_memrealtime()
 #else
 #define RES_TICK(k)
+#define RES_TICKX(k)
 #endif
     RES_TICK(0);
 
-    // the pair, read once (8 columns' loads in flight at a time: all 64 at once would need 256 registers
-    // of load destinations)
-    float px[kResCols], py[kResCols], pz[kResCols], qx[kResCols], qy[kResCols], qz[kResCols];
-    constexpr int kLB = 8;
-#pragma unroll
-    for (int j0 = 0; j0 < kResCols; j0 += kLB) {
-        float4 v[kLB], t[kLB];
-#pragma unroll
-        for (int e = 0; e < kLB; ++e) {
-            const int i = min(tid + kResWG * (j0 + e), n - 1);
-            if (j0 + e < ncol) {
-                v[e] = Xp[i];
-                t[e] = NT[i];
-            }
-        }
+    // ---- the pair, read once, in batches of 8 columns one batch ahead of pass A's folds.  The columns
+    // are register vectors indexed by a wave-uniform column number (s_set_gpr_idx: one instruction per
+    // access), so every loop over them is a loop, not 32 unrolled copies — an unrolled kernel's code
+    // (~0.5 MB) had been fetched from L2 instruction by instruction
+    fcols px, py, pz, qx, qy;
+    constexpr int kLB = ICP4R_RES_LB;
+    float4 lv_[kLB], lt_[kLB];  // a batch in flight
+    auto issue = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < kLB; ++e) {
-            const int j = j0 + e;
+            const int j = uni(b * kLB + e), i = min(tid + kResWG * j, n - 1);
             if (j < ncol) {
-                px[j] = v[e].x;
-                py[j] = v[e].y;
-                pz[j] = v[e].z;
-                qx[j] = t[e].x;
-                qy[j] = t[e].y;
-                qz[j] = t[e].z;
-                sh.L[tid + kResWG * j] = v[e].w;  // (past n: point n - 1's, never read)
+                lv_[e] = Xp[i];
+                lt_[e] = NT[i];
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-
+    };
+    auto extract = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < kLB; ++e) {
+            const int j = uni(b * kLB + e), i = tid + kResWG * j;
+            if (j < ncol) {
+                px[j] = lv_[e].x;
+                py[j] = lv_[e].y;
+                pz[j] = lv_[e].z;
+                qx[j] = lt_[e].x;
+                qy[j] = lt_[e].y;
+                sh.qz[i] = lt_[e].z;  // (past n: point n - 1's, never read)
+                sh.L[i] = half_down(lv_[e].w);
+            }
+        }
+    };
+    issue(0);
+    extract(0);
+    if (ncol > kLB) issue(1);
     RES_TICK(7);
-    // ---- pass A: column j staged into buffer j & 1 (rows Σs.xyz, Σd.xyz, Σw), wave 0 lanes 0..6 fold
+
+    // ---- pass A: chunk K = columns 2K, 2K + 1 staged into buffer K & 1 (rows Σs.xyz, Σd.xyz, Σw)
     int cnt = 0;
+    uint32_t amask = 0;  // bit j: point t + 256 j is a correspondence (d² <= max_d2)
     uint64_t ms_s = 0;
     int ms_e = INT_MAX;
-    auto stage_a = [&](int j) __attribute__((always_inline)) {
+    auto stage_col = [&](int j) __attribute__((always_inline)) {
+        j = uni(j);
         const int i = tid + kResWG * j;
         if (i >= n) return;
         float* b = buf + (j & 1) * 7 * kResRowA + tid;
-        const float d2 = l2_simple(px[j], py[j], pz[j], qx[j], qy[j], qz[j]);
+        const float z = sh.qz[i];
+        const float d2 = l2_simple(px[j], py[j], pz[j], qx[j], qy[j], z);
         const bool ok = !(d2 > kp.max_d2);  // (max_d2 = FLT_MAX: only an overflowing d² is rejected)
         b[0] = ok ? px[j] : -0.0f;
         b[kResRowA] = ok ? py[j] : -0.0f;
         b[2 * kResRowA] = ok ? pz[j] : -0.0f;
         b[3 * kResRowA] = ok ? qx[j] : -0.0f;
         b[4 * kResRowA] = ok ? qy[j] : -0.0f;
-        b[5 * kResRowA] = ok ? qz[j] : -0.0f;
+        b[5 * kResRowA] = ok ? z : -0.0f;
         b[6 * kResRowA] = ok ? 1.0f : 0.0f;
         cnt += ok ? 1 : 0;
+        amask |= ok ? 1u << j : 0u;
         if (mse) lane_exact_add(ok ? (double)d2 : 0.0, ms_s, ms_e);
     };
     float acc = (lane < 6) ? -0.0f : 0.0f;  // Eigen's rowwise().sum() from the first element; Σw from 0
-    if (ncol > 0) stage_a(0);
-#pragma unroll
-    for (int j = 0; j < kResCols; ++j) {
-        if (j < ncol) {
-            __syncthreads();  // column j staged; buffer (j + 1) & 1 folded (column j - 1)
-            if (wave == 0 && lane < 7)
-                acc = fold_row(buf + ((j & 1) * 7 + lane) * kResRowA, min(kResWG, n - j * kResWG), acc);
-            if (j + 1 < ncol) stage_a(j + 1);
+    if (ncol > 0) stage_col(0);
+    for (int K = 0; K < ncol; ++K) {
+        __syncthreads();  // column K staged; buffer (K + 1) & 1 folded (column K - 1)
+        if (wave == 0 && lane < 7) {
+            fold_prio(true);
+            acc = ICP4R_RES_FOLD(buf + ((K & 1) * 7 + lane) * kResRowA, min(kResWG, n - K * kResWG), acc);
+            fold_prio(false);
         }
+        RES_TICKX(K);
+        // the next batch of columns arrives before column K + 1 needs it; the one after goes in flight
+        if ((K + 1) % kLB == 0 && K + 1 < ncol) {
+            extract((K + 1) / kLB);
+            if (K + 1 + kLB < ncol) issue((K + 1) / kLB + 1);
+        }
+        if (K + 1 < ncol) stage_col(K + 1);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
@@ -4711,7 +4843,7 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
         int total = 0;
         for (int k = 0; k < kResWG / 64; ++k) total += sh.cnt[k];
         sh.s.mom[0] = (double)total;
-        // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly); Huber: 1/Σw
+        // unweighted: one_over_n = 1/(float)n (fold of 1.0f == n exactly)
         const float one_over_n = 1.0f / sh.res[6];
         sh.s.one_over_n = one_over_n;
         for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
@@ -4748,38 +4880,89 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
         if (tid == 0) sh.s.mse_sum = dacc;
         __syncthreads();
     }
-
     RES_TICK(1);
-    // ---- pass B: sigma in Eigen's panel order, the panels side by side (fold_pass_b<PAR>'s arithmetic)
-    const int cntA = (int)sh.s.mom[0];
-    if (cntA < n) {
-        // (rare: an overflowing d² was rejected) panel starts by rank: fold_pass_b over X and nn_t re-read
-        // from HBM, no register of the held pair needed
-        const FoldIn fin{nullptr, Xp, NT, n};
-        static_assert(2 * 9 * kFoldRow <= kResStage, "fold_pass_b buffers");
-        fold_pass_b<kResWG, kFoldChunkP, kFoldRow, false>(kp, fin, reinterpret_cast<float(*)[9][kFoldRow]>(buf), sh.s);
-    } else {
+
+    // ---- pass B: sigma in Eigen's panel order, the panels side by side (fold_pass_b<PAR>'s arithmetic).
+    // A point's step is its rank among the correspondences (its index when every point is one) mod kc.
+    {
+        const int cntA = (int)sh.s.mom[0];
+        const bool plain = cntA >= n;
+        int32_t* base = reinterpret_cast<int32_t*>(buf);  // (rejections: rank of (column, wave)'s first point)
+        if (!plain) {
+            for (int j = 0; j < ncol; ++j) {
+                const uint64_t bal = __ballot((amask >> j) & 1u);
+                if (lane == 0) base[j * 4 + wave] = __builtin_popcountll(bal);
+            }
+            __syncthreads();
+            if (wave == 0) {  // exclusive scan in point order (column-major, then wave)
+                const int c0 = lane < 2 * ncol ? base[2 * lane] : 0, c1 = lane < 2 * ncol ? base[2 * lane + 1] : 0;
+                int incl = c0 + c1;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int o = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += o;
+                }
+                if (lane < 2 * ncol) {
+                    base[2 * lane] = incl - c0 - c1;
+                    base[2 * lane + 1] = incl - c1;
+                }
+            }
+            __syncthreads();
+        }
+        // rank of point t + 256 j among the correspondences (-1: rejected); every lane calls it
+        auto rank = [&](int j) __attribute__((always_inline)) -> int {
+            if (plain) return tid + kResWG * j < n ? tid + kResWG * j : -1;
+            const uint32_t on = (amask >> j) & 1u;
+            const uint64_t bal = __ballot(on);
+            const int r = base[j * 4 + wave] +
+                          (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            return on ? r : -1;
+        };
         const float oon = sh.s.one_over_n;
         const int kc = sigma_kc(cntA, kp.sigma_max_kc);
         const int S = (cntA > 0 && kc > 0) ? (cntA + kc - 1) / kc : 1;
+        const float invkc = 1.0f / (float)kc;
         float sig = 0.0f;  // wave 0 lanes 0..8: sigma(a, b), the panels added in order
         for (int s0 = 0; s0 < S; s0 += kSliceGroup) {
             const int G = min(kSliceGroup, S - s0);
             const int R = 9 * G;                                   // fold chains of the group
             const int stride = (((kResStage / R) - 4) & ~7) + 4;  // one buffer: rows of T steps, ≡ 4 mod 8
             const int T = stride - 4;
-            const int r0 = s0 * kc;                                // the group's first point (rank = index)
-            const int r1 = min((s0 + G) * kc, n);
+            const int r0 = s0 * kc;                                // the group's first rank
+            const int r1 = min((s0 + G) * kc, cntA);
             const int nch = (min(kc, r1 - r0) + T - 1) / T;
             // fold lane L = sl * 9 + ab: the chain of panel s0 + sl, coefficient ab
-            const int my_len = tid < R ? min(kc, n - (s0 + tid / 9) * kc) : 0;
-            // point t + 256 j's (panel, step) in the group, carried from column to column (kc >= 256: one
-            // wrap at most per column; smaller kc, the loop)
+            const int my_len = tid < R ? min(kc, cntA - (s0 + tid / 9) * kc) : 0;
+            const float invT = 1.0f / (float)T;
+            // (rejections) each column's point in this group: chunk | panel << 8 | step in the chunk << 16
+            // (chunk 255: none) — one register per column, read by the chunk scan with the column index
+            ucols info;
+            if (!plain) {
+#pragma unroll
+            for (int j = 0; j < kResCols; ++j) {
+                uint32_t v = 255u;
+                if (j < ncol) {
+                    const int r = rank(j) - r0;
+                    if (r >= 0 && r < r1 - r0) {
+                        int sl = (int)((float)r * invkc);  // r / kc, corrected (exact for these r)
+                        int sp = r - sl * kc;
+                        if (sp >= kc) { ++sl; sp -= kc; }
+                        if (sp < 0) { --sl; sp += kc; }
+                        int c = (int)((float)sp * invT);
+                        if (c * T > sp) --c;
+                        if ((c + 1) * T <= sp) ++c;
+                        v = (uint32_t)min(c, 254) | ((uint32_t)sl << 8) | ((uint32_t)(sp - c * T) << 16);
+                    }
+                }
+                info[j] = v;
+            }
+            }
+            if (s0 == 0) RES_TICK(5);
             float accp = 0.0f;
             for (int c = 0; c < nch; ++c) {
                 const int w0 = c * T;  // the chunk's first step
                 // the means, re-read per chunk as wave-uniform (SGPR) values: hoisted out of the chunk
-                // loop, the 6 x 32 demeaned coordinates had gone to scratch
+                // loop, the demeaned coordinates had gone to scratch
                 float mv[6];
 #pragma unroll
                 for (int k = 0; k < 6; ++k) {
@@ -4787,60 +4970,74 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
                     asm volatile("" : "+s"(mv[k]));
                 }
                 const float ms0 = mv[0], ms1 = mv[1], ms2 = mv[2], md0 = mv[3], md1 = mv[4], md2 = mv[5];
-                int sl = 0, st = tid - r0;
-                while (st < 0) { st += kc; --sl; }
-                while (st >= kc) { st -= kc; ++sl; }
                 // every thread writes the products of its points whose step lies in [w0, w0 + T)
-#pragma unroll
-                for (int j = 0; j < kResCols; ++j) {
-                    if (j < ncol) {
-                        const int tt = st - w0;
-                        if (sl >= 0 && sl < G && (unsigned)tt < (unsigned)T && tid + kResWG * j < r1) {
-                            const float sv0 = px[j] - ms0, sv1 = py[j] - ms1, sv2 = pz[j] - ms2;
-                            const float dv0 = qx[j] - md0, dv1 = qy[j] - md1, dv2 = qz[j] - md2;
-                            float* o = buf + sl * 9 * stride + tt;
-                            o[0] = dv0 * sv0;
-                            o[stride] = dv0 * sv1;
-                            o[2 * stride] = dv0 * sv2;
-                            o[3 * stride] = dv1 * sv0;
-                            o[4 * stride] = dv1 * sv1;
-                            o[5 * stride] = dv1 * sv2;
-                            o[6 * stride] = dv2 * sv0;
-                            o[7 * stride] = dv2 * sv1;
-                            o[8 * stride] = dv2 * sv2;
+                auto put = [&](int j, uint32_t sl, uint32_t tt) __attribute__((always_inline)) {
+                    const int i = tid + kResWG * j;
+                    const float sv0 = px[j] - ms0, sv1 = py[j] - ms1, sv2 = pz[j] - ms2;
+                    const float dv0 = qx[j] - md0, dv1 = qy[j] - md1, dv2 = sh.qz[i] - md2;
+                    float* o = buf + sl * 9 * stride + tt;
+                    o[0] = dv0 * sv0;
+                    o[stride] = dv0 * sv1;
+                    o[2 * stride] = dv0 * sv2;
+                    o[3 * stride] = dv1 * sv0;
+                    o[4 * stride] = dv1 * sv1;
+                    o[5 * stride] = dv1 * sv2;
+                    o[6 * stride] = dv2 * sv0;
+                    o[7 * stride] = dv2 * sv1;
+                    o[8 * stride] = dv2 * sv2;
+                };
+                if (plain) {
+                    // a point's rank is its index: panel sl's steps [w0, w0 + T) are the points [a, b), in
+                    // one or two columns (wave-uniform bounds)
+                    for (int sl = 0; sl < G; ++sl) {
+                        const int a = r0 + sl * kc + w0;
+                        const int b = min(a + T, min(r0 + (sl + 1) * kc, r1));
+                        for (int j0 = a / kResWG; a < b && j0 <= (b - 1) / kResWG; ++j0) {
+                            const int j = uni(j0);
+                            const int i = tid + kResWG * j;
+                            if (i >= a && i < b) put(j, (uint32_t)sl, (uint32_t)(i - a));
                         }
-                        st += kResWG;
-                        while (st >= kc) {
-                            st -= kc;
-                            ++sl;
-                        }
+                    }
+                } else {
+                    for (int j0 = 0; j0 < ncol; ++j0) {
+                        const int j = uni(j0);
+                        const uint32_t v = info[j];
+                        if ((v & 255u) == (uint32_t)c) put(j, (v >> 8) & 255u, v >> 16);
                     }
                 }
                 __syncthreads();  // the chunk staged
+                if (s0 == 0) RES_TICKX(32 + 2 * c);
                 if (tid < R) {
                     const int len = min(T, my_len - w0);
                     if (len > 0) accp = fold_row(buf + tid * stride, len, accp);
                 }
                 __syncthreads();  // the chunk folded: the buffer is free
+                if (s0 == 0) RES_TICKX(33 + 2 * c);
             }
             if (tid < R) buf[tid] = accp;
             __syncthreads();
             if (wave == 0 && lane < 9)
-                for (int sl = 0; sl < G; ++sl) sig = sig + oon * buf[sl * 9 + lane];  // res += alpha * C0
+                for (int k = 0; k < G; ++k) sig = sig + oon * buf[k * 9 + lane];  // res += alpha * C0
             __syncthreads();
         }
         if (wave == 0 && lane < 9) sh.s.sigmaf[lane] = sig;
     }
-
     RES_TICK(2);
+
     // ---- the solve (thread 0), the tail's bitmap cleared meanwhile
-    const bool tail = tail_test && w.nn_u;
     uint32_t* need = reinterpret_cast<uint32_t*>(buf);  // (pass B's buffers are free)
     int32_t* pre = reinterpret_cast<int32_t*>(need + kNeedWords);
     float4* lv = reinterpret_cast<float4*>(pre + kNeedWords);
     uint2* lm = reinterpret_cast<uint2*>(lv + kResRecs);
     static_assert(2 * kNeedWords * 4 + kResRecs * 24 <= kResStage * 4, "tail records");
+    // the tail's U, every column in flight across the solve (one register per column)
+    const bool tail = tail_test && w.nn_u;
+    float* uu = w.nn_u + xs;
+    fcols uv;
     if (tail) {
+#pragma unroll
+        for (int j = 0; j < kResCols; ++j)
+            if (j < ncol) uv[j] = uu[min(tid + kResWG * j, n - 1)];
         for (int k = tid; k < ((n + 31) >> 5); k += kResWG) need[k] = 0u;
         if (tid == 0) sh.mcount = 0;
     }
@@ -4854,24 +5051,18 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
     float T[16];  // (wave-uniform: SGPR operands of the transform)
 #pragma unroll
     for (int q = 0; q < 16; ++q) T[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh.s.T_inc[q])));
-    float* uu = w.nn_u + xs;
     float4* X = w.X + xs;
     float4* sqg = w.sq + xs;
     uint2* smg = w.sm + xs;
     int hits = 0, misses = 0;
-    constexpr int kUB = 4;  // U loads in flight (one batch ahead)
-    float ua[kUB], ub[kUB];
-    auto load_u = [&](int j0, float (&u)[kUB]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < kUB; ++e) u[e] = (j0 + e < ncol) ? uu[min(tid + kResWG * (j0 + e), n - 1)] : 0.0f;
-    };
-    auto test = [&](int j, float U) __attribute__((always_inline)) {
+    for (int j0 = 0; j0 < ncol; ++j0) {
+        const int j = uni(j0);
         const int i = tid + kResWG * j;
         const bool valid = i < n;
         float ox, oy, oz;
         xform_pt(T, px[j], py[j], pz[j], ox, oy, oz);  // PCL transformCloud, in place
-        const float2 Lm = move_lu(make_float2(sh.L[i], U), px[j], py[j], pz[j], ox, oy, oz);
-        const float d2 = l2_simple(ox, oy, oz, qx[j], qy[j], qz[j]);
+        const float2 Lm = move_lu(make_float2((float)sh.L[i], uv[j]), px[j], py[j], pz[j], ox, oy, oz);
+        const float d2 = l2_simple(ox, oy, oz, qx[j], qy[j], sh.qz[i]);
         const bool hit = valid & cache_hit(Lm.x, d2);
         if (valid) {
             st_v4<1>(&X[i], make_float4(ox, oy, oz, Lm.x));
@@ -4891,18 +5082,6 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
             }
             ++misses;
         }
-    };
-    load_u(0, ua);
-#pragma unroll
-    for (int jb = 0; jb < kResCols; jb += 2 * kUB) {
-        if (jb + kUB < kResCols) load_u(jb + kUB, ub);
-#pragma unroll
-        for (int e = 0; e < kUB; ++e)
-            if (jb + e < ncol) test(jb + e, ua[e]);
-        if (jb + 2 * kUB < kResCols) load_u(jb + 2 * kUB, ua);
-#pragma unroll
-        for (int e = 0; e < kUB; ++e)
-            if (jb + kUB + e < ncol) test(jb + kUB + e, ub[e]);
     }
     RES_TICK(6);
     // every record appended: the overflow records' stores drained before the barrier (another wave
@@ -4940,6 +5119,7 @@ __device__ __forceinline__ int res_update_pair(const PairArgs& a, const WorkArgs
     const int tp = test_place<kResWG>(w, p, n, hits, misses, need, pre, lv, lm, kResRecs, sh.cnt, false, nullptr);
     RES_TICK(4);
 #undef RES_TICK
+#undef RES_TICKX
     return tp;
 }
 

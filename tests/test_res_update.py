@@ -46,8 +46,8 @@ def _run_both(gpu_ctx, plan, args, params):
 @pytest.mark.parametrize("early", [False, True])
 def test_res_update_identical(gpu_ctx, oracle_mod, early, plan):
     """Ragged batch (8192, 8191, 8000, 4097, 4096, 2048, 1000, 300, 256, 37, 5 sources): the on-chip
-    update equals the streaming one bit for bit — results, and the cached-neighbour test's hit and
-    tested counts (the same misses go to the same searches) — and sampled pairs equal the oracle."""
+    update equals the streaming one bit for bit — results, and the cached-neighbour test's tested
+    counts (its hits within 1 %: L is held rounded down) — and sampled pairs equal the oracle."""
     import icp4r
 
     shapes = [(8192, 8192)] * 200 + [(8191, 8000), (8000, 8100), (4097, 5000), (4096, 8192), (2048, 600),
@@ -60,8 +60,12 @@ def test_res_update_identical(gpu_ctx, oracle_mod, early, plan):
     p = icp4r.default_params(max_iterations=20, **kw)
     out = _run_both(gpu_ctx, plan, args, p)
     assert out[1].tobytes() == out[0].tobytes()
-    for key in ("cache_hits", "cache_tested", "tested_in_update", "hits_in_update"):
+    # (the on-chip kernel holds L rounded down to half precision: a few more misses, searched exactly —
+    # the same queries tested, within 1 % of the hits)
+    for key in ("cache_tested", "tested_in_update"):
         assert out["st1"][key] == out["st0"][key], key
+    for key in ("cache_hits", "hits_in_update"):
+        assert abs(out["st1"][key] - out["st0"][key]) <= 0.01 * out["st0"][key], key
     assert out["st1"]["tested_in_update"] > 0
     res = out[1]
     assert (res["status"] == 0).all()

@@ -52,14 +52,15 @@ def main():
     for _ in range(2):
         ctx.align_batch_device(batch, params, results.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
-    k = 32 + 12 * Pg
+    k = 32 + 12 * Pg + 64
     buf = (C.c_uint64 * k)()
     lib = icp4r.load()
     lib.icp4r__debug_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32]
     if lib.icp4r__debug_ticks(ctx._h, buf, k):
         raise RuntimeError(lib.icp4r_last_error())
-    raw = np.array(buf[32 + 4 * Pg:], dtype=np.uint64).reshape(Pg, 8)
-    hw = raw[:, 5]
+    raw = np.array(buf[32 + 4 * Pg:32 + 12 * Pg], dtype=np.uint64).reshape(Pg, 8)
+    fine = np.array(buf[32 + 12 * Pg:], dtype=np.uint64).astype(np.int64)
+    hw = raw[:, 5] if os.environ.get("ICP4R_RES_UPDATE", "0") == "0" else np.zeros(Pg, np.uint64)
     if hw.any():  # fold-wave placement: per CU, how many fold waves share each SIMD
         hid = (hw & 0xffffffff).astype(np.int64)
         xcc = (hw >> np.uint64(32)).astype(np.int64) & 0xf
@@ -86,11 +87,23 @@ def main():
     if (t6 > 0).all():  # the tail split at the test's end: the test, then the misses' rank placement
         out["tail_test"] = pct(t6 - t[:, 3])
         out["tail_place"] = pct(t[:, 4] - t6)
+    t5 = raw[ok, 5].astype(np.int64).astype(np.float64) * 0.01
+    if not hw.any() and (t5 > 0).all():  # fold_update_res_kernel: pass B split after its prologue
+        out["passB_prologue"] = pct(t5 - t[:, 1])
+        out["passB_chunks"] = pct(t[:, 2] - t5)
     t7 = raw[ok, 7].astype(np.int64).astype(np.float64) * 0.01
     if (t7 > 0).all():  # fold_update_res_kernel: pass A split at the end of the pair's loads
         out["load"] = pct(t7 - t[:, 0])
         out["passA_folds"] = pct(t[:, 1] - t7)
     out["total"] = pct(t[:, 4] - t[:, 0])
+    if fine[0] > 0:  # fold_update_res_kernel, pair 0: pass A per column, pass B per chunk (fill end, fold end)
+        r0 = int(raw[0, 7]) if raw[0, 7] else int(raw[0, 0])
+        colA = [f for f in fine[:32] if f > 0]
+        out["pair0_passA_col_us"] = [round((b - a) * 0.01, 2) for a, b in zip([r0] + colA[:-1], colA)]
+        pb = [f for f in fine[32:64]]
+        t5 = int(raw[0, 5])
+        seq = [t5] + [f for f in pb if f > 0]
+        out["pair0_passB_fill_fold_us"] = [round((b - a) * 0.01, 2) for a, b in zip(seq[:-1], seq[1:])]
     print(json.dumps(out))
     ctx.close()
 
