@@ -705,7 +705,7 @@ def run_gpu(args) -> int:
         ctx.set_kernel_timing(False)
         ctx.set_plan_option("groups", groups_prev)
     single_group_equal = bool((results.cpu().numpy() == (timed[rank * P:(rank + 1) * P] if world > 1 else timed)).all())
-    nn_ms, nn_launches = ctx.kernel_time_ms()  # the dominant kernel: the batched search
+    nn_ms, nn_launches = ctx.kernel_time_ms()  # the NN launches (the batched search); the update below
     test_ms, test_launches = ctx.stage_time_ms(icp4r.STAGE_NN_TEST)
     upd_ms, upd_launches = ctx.stage_time_ms(icp4r.STAGE_UPDATE)
     st = ctx.nn_stats()  # work the NN kernels performed in the single-group steps

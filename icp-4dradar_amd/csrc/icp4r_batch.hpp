@@ -17,15 +17,15 @@ struct Plan {
     int splits;   // brute force: target splits
     bool pruned;  // Morton-block pruned exact search
     bool lds;     // pruned, batched: nn_lds_kernel (whole target set in LDS, per-query work lists)
-    bool cache;   // lds: cached-neighbour test + second-nearest search (ICP4R_NN_CACHE=0 disables)
+    bool cache;   // lds: cached-neighbour test + second-nearest search (plan option nn_cache = 0 disables)
     int leaf;     // pruned: targets per block
     int chunk_sb; // pruned (streamed): superblocks per target chunk (<= 64)
     int chunks;   // pruned (streamed): target chunks searched by separate waves (merged by atomicMin)
-    bool tile;    // pruned, not batched: nn_tile_kernel (LDS target tiles x query parts; ICP4R_NN_TILE=0: the stream)
+    bool tile;    // pruned, not batched: nn_tile_kernel (LDS target tiles x query parts; plan option nn_tile = 0: the stream)
     int max_m;    // the plan's largest target (tile grid)
     int tile_run; // tile: queries per wave run (64, 32, 16): 16 runs per workgroup
     bool solo;    // run_pairs: the whole registration of each pair in one workgroup (solo_kernel; PCL
-                  // numerics, one target tile, sources <= kCacheMaxN; ICP4R_SOLO=0 disables)
+                  // numerics, one target tile, sources <= kCacheMaxN; plan option solo = 0 disables)
     int64_t blocks;
 };
 

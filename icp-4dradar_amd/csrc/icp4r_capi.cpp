@@ -155,7 +155,7 @@ Plan make_plan(const icp4r_ctx* ctx, int npairs, int max_n, int max_m, int nn_mo
         pl.chunk_sb = cs;
         pl.chunks = nsb > 0 ? (nsb + cs - 1) / cs : 1;
         pl.blocks *= pl.chunks;
-        // batches whose targets fit in LDS: one workgroup per pair (ICP4R_NN_LDS=0|1 overrides).  Its
+        // batches whose targets fit in LDS: one workgroup per pair (plan option nn_lds = 0|1 overrides).  Its
         // query records pack the source index and sorted position in 14 bits each (kLdsMaxSources),
         // so larger sources take the tiled search instead.
         const int lds = opt(ctx, kOptNnLds, -1);
@@ -173,7 +173,7 @@ Plan make_plan(const icp4r_ctx* ctx, int npairs, int max_n, int max_m, int nn_mo
                 pl.chunks = (max_m + 8191) / 8192;
                 // queries per wave run: shorter runs (more workgroups, each staging its tile) until the
                 // grid covers the CUs — a single pair's search is latency-bound per run (C2 1.85 ->
-                // 1.75 ms, C5 2.35 -> 2.20 ms at 16; C1 0.457 -> 0.449 ms at 8; ICP4R_TILE_RUN=64 / 32 /
+                // 1.75 ms, C5 2.35 -> 2.20 ms at 16; C1 0.457 -> 0.449 ms at 8; plan option tile_run = 64 / 32 /
                 // 16 / 8 forces one)
                 const int tr = opt(ctx, kOptTileRun, 0);
                 auto parts = [&](int run) { return (int64_t)npairs * ((max_n + 16 * run - 1) / (16 * run)) * pl.chunks; };
@@ -185,12 +185,12 @@ Plan make_plan(const icp4r_ctx* ctx, int npairs, int max_n, int max_m, int nn_mo
                 pl.blocks = parts(pl.tile_run);
             }
             // a PCL-numerics registration whose targets fit one LDS tile: the whole registration of
-            // each pair in one workgroup (solo_kernel; ICP4R_SOLO=0: the multi-launch plan)
+            // each pair in one workgroup (solo_kernel; plan option solo = 0: the multi-launch plan)
             // (up to kSoloMaxN sources: beyond, the one CU's search of the first pass' queries and the
             // misses costs more than the multi-launch plan's boundaries since its search spreads over
             // the CUs in runs of 16 — C1's 2k pair 0.55 ms solo vs 0.50 multi at PCL's 10 iterations;
             // solo stays ahead on long fixed runs up to 3k sources, 0.78 vs 0.81 ms at 20 — see
-            // tools/experiments/solo_sweep.py, profiles/round3/s4/solo_sweep_r16.jsonl; ICP4R_SOLO=1 forces it up to
+            // tools/experiments/solo_sweep.py, profiles/round3/s4/solo_sweep_r16.jsonl; plan option solo = 1 forces it up to
             // kCacheMaxN, 0 disables it)
             const int solo_env = opt(ctx, kOptSolo, -1);
             pl.solo = registration && pl.tile && pl.chunks == 1 && solo_env != 0 &&
@@ -316,7 +316,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         w.tbb = reinterpret_cast<float*>(w.kdn + (size_t)npairs * kKdnStride);
         // a target too large for the in-LDS kd build, for few pairs: its Morton sort on several
         // workgroups (one 8192-point chunk each) before index_refine_kernel re-orders every chunk
-        // (ICP4R_MORTON_MWG=0: one workgroup per target, as for the batches)
+        // (plan option morton_mwg = 0: one workgroup per target, as for the batches)
         constexpr int kChunk = 8192;
         const int64_t mog = (w.t_stride + kChunk - 1) / kChunk;
         if ((w.kd_index & 1) && w.t_stride > kChunk && (pl.leaf == 16 || pl.leaf == 32) &&
@@ -395,7 +395,7 @@ int nn_pass(icp4r_ctx* ctx, const Plan& pl, const PairArgs& a, const WorkArgs& w
             int fitness_pass, int first, hipStream_t st, int ncu, int test_fused, int pass, int ordered) {
     EventPair* ne;
     int r;
-    WorkArgs w = w0;  // debug: the pass' own event slots (ICP4R_PHASE_TICKS=1)
+    WorkArgs w = w0;  // debug: the pass' own event slots (plan option phase_ticks = 1)
     w.pass_ticks = (w0.ticks && pass >= 0 && pass < kMaxTickPasses)
                        ? w0.ticks + pass_tick_base(npairs) + (int64_t)pass * kPassTickSlots
                        : nullptr;
@@ -508,7 +508,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // multi-tile plan (the scan-to-map target), PCL numerics: seeds written by the update's transform
     w.seed_next = (pl.tile && pl.chunks > 1 && pcl && w.corr && opt(ctx, kOptFuseSeed, 1) != 0) ? 1 : 0;
     // one-tile plan (C1, C2), PCL numerics: the update's transformCloud(T_inc) deferred into the next
-    // search, which reads every query anyway (nn_tile_kernel; ICP4R_TILE_DEFER=0: the update does it)
+    // search, which reads every query anyway (nn_tile_kernel; plan option tile_defer = 0: the update does it)
     if (pl.tile && pl.chunks == 1 && !pl.solo && pcl && w.corr && opt(ctx, kOptTileOwn, 1) != 0 &&
         opt(ctx, kOptTileDefer, 1) != 0)
         w.defer_xform = 1;
@@ -565,13 +565,13 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // PCL's do { ... } while (!converged): at least one iteration even for max_iterations == 0.
     const int iters = max_iterations > 0 ? max_iterations : 1;
     // the cached-neighbour test of iteration passes 2.. runs in the tail of the previous update
-    // (fold_update_kernel, PCL numerics; ICP4R_FUSE_TEST=0: its own kernel)
+    // (fold_update_kernel, PCL numerics; plan option fuse_test = 0: its own kernel)
     const bool fuse = pl.lds && pl.cache && pcl && opt(ctx, kOptFuseTest, 1) != 0;
-    // ... and the work list of those passes is built by the update's last workgroup (ICP4R_FUSE_ORDER=0:
+    // ... and the work list of those passes is built by the update's last workgroup (plan option fuse_order = 0:
     // nn_order_kernel)
     const bool ford = fuse && opt(ctx, kOptFuseOrder, 1) != 0;
     // ... and folds the next pass A's source centroid sums over the X it writes, so that pass A reads
-    // nn_t only (every correspondence kept, unweighted, no MSE criterion).  Off unless ICP4R_SUMS_TAIL=1:
+    // nn_t only (every correspondence kept, unweighted, no MSE criterion).  Off unless plan option sums_tail = 1:
     // the three n-long chains are serial, and in pass A they run beside the other chains for free, while
     // in the tail they lengthen the pair's critical path (C3: update 177 -> 190 us)
     for (int g = 0; g < groups; ++g)
@@ -588,7 +588,7 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
                                 : 0;
     const bool kev = ctx->kernel_timing;  // per-kernel events (icp4r_set_kernel_timing; nn_pass: the same)
     // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
-    // by side (ICP4R_WIDE_UPDATE=0: fold_update_kernel's 256 threads)
+    // by side (plan option wide_update = 0: fold_update_kernel's 256 threads)
     const bool wide = pcl && !fuse && npairs <= ctx->ncu && opt(ctx, kOptWideUpdate, 1) != 0;
     // ... which, on the multi-tile plan (the scan-to-map target), forms the correspondence records in
     // its pass A instead of corr_kernel after every search (plan option fold_keys = 0: corr_kernel)
@@ -1179,10 +1179,10 @@ int icp4r_nn_stats(icp4r_ctx* ctx, icp4r_nn_stats_t* out) {
 }
 
 // Internal debug hook (not in icp4r.h): the last fold_update phase timestamps of pair 0 (100 MHz
-// ticks; needs ICP4R_PHASE_TICKS=1 in the environment when the registration ran).
+// ticks; needs plan option phase_ticks = 1 on the context when the registration ran).
 int icp4r__debug_ticks(icp4r_ctx* ctx, uint64_t* out, int32_t k) {
     if (!ctx || !out || k <= 0 || (size_t)k * sizeof(uint64_t) > ctx->ticks.cap) return fail(ICP4R_E_INVALID, "bad arguments");
-    if (!ctx->ticks.p) return fail(ICP4R_E_INVALID, "phase ticks not enabled (ICP4R_PHASE_TICKS=1)");
+    if (!ctx->ticks.p) return fail(ICP4R_E_INVALID, "phase ticks not enabled (plan option phase_ticks = 1)");
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, ctx->ticks.p, (size_t)k * sizeof(uint64_t), hipMemcpyDeviceToHost));

@@ -18,6 +18,7 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <sched.h>
 #include <string.h>
 
 #include <vector>
@@ -40,22 +41,27 @@ namespace {
 // (Every 4 with a blocking read had left the device idle ~37 µs per check on the map call.)
 constexpr int kActiveCheck = 2;
 
-// the count a check wrote into the pinned slot, once it has; an error if the stream drained without it
-int wait_active(volatile int32_t* slot, hipStream_t st, int32_t* out) {
+// The count check `seq` wrote into the pinned slot, once it has; an error if the stream drained without
+// it.  A value with another sequence number is a stale one — an earlier call's check still in flight
+// when this call reset the slot (the device API returns before its queued work has run) — and is
+// waited past.  The loop yields the core between polls.
+int wait_active(volatile int64_t* slot, uint32_t seq, hipStream_t st, int32_t* out) {
+    auto mine = [&](int64_t v) { return v != -1 && (uint32_t)((uint64_t)v >> 32) == seq; };
     for (;;) {
-        const int32_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-        if (v != -1) {
-            *out = v;
+        const int64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+        if (mine(v)) {
+            *out = (int32_t)(uint32_t)v;
             return ICP4R_OK;
         }
         const hipError_t q = hipStreamQuery(st);
         if (q == hipSuccess) {
-            const int32_t v2 = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-            if (v2 == -1) return fail(ICP4R_E_HIP, "GICP active-pair check not written");
-            *out = v2;
+            const int64_t v2 = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+            if (!mine(v2)) return fail(ICP4R_E_HIP, "GICP active-pair check %u not written", seq);
+            *out = (int32_t)(uint32_t)v2;
             return ICP4R_OK;
         }
         if (q != hipErrorNotReady) return fail(ICP4R_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
+        sched_yield();
     }
 }
 
@@ -223,10 +229,13 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
         HIP_TRY(launch_gicp_knn_cov(a.src, a.src_off, a.src_n, ws, npairs, mn, xs, gp.k_correspondences,
                                     gp.regularization, cs, knn_lanes, aux));
         HIP_TRY(hipEventRecord(ctx->gicp_join, aux));
-        if ((rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences,
-                           gp.regularization, ct, st, brute, true, knn_lanes)))
-            return rc;
-        HIP_TRY(hipStreamWaitEvent(st, ctx->gicp_join, 0));
+        rc = cov_pass(pl, a, w, a.tgt, a.tgt_off, a.tgt_n, npairs, mm, ts, gp.k_correspondences, gp.regularization,
+                      ct, st, brute, true, knn_lanes);
+        // joined on every path: a failed target pass must not leave the source's chain (which writes
+        // gicp_cov_src and gicp_sidx) running past the call
+        const hipError_t je = hipStreamWaitEvent(st, ctx->gicp_join, 0);
+        if (rc) return rc;
+        HIP_TRY(je);
     } else {
         if ((rc = cov_pass(pl, a, w, a.src, a.src_off, a.src_n, npairs, mn, xs, gp.k_correspondences,
                            gp.regularization, cs, st, brute, false, knn_lanes)))
@@ -238,9 +247,10 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
     if (pl.pruned && brute) HIP_TRY(launch_index(a, w, npairs, st));
     if (kev) HIP_TRY(hipEventRecord(ce->stop, st));
     int32_t* active = static_cast<int32_t*>(ctx->gicp_active.p);
-    if (!ctx->gicp_hflag) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->gicp_hflag), 2 * sizeof(int32_t), hipHostMallocCoherent));
-    volatile int32_t* hf = ctx->gicp_hflag;
+    if (!ctx->gicp_hflag) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->gicp_hflag), 2 * sizeof(int64_t), hipHostMallocCoherent));
+    volatile int64_t* hf = ctx->gicp_hflag;
     int nchk = 0, prev_slot = -1;
+    uint32_t prev_seq = 0;
     for (int it = 0; it < gp.max_iterations; ++it) {
         if ((rc = nn_pass(ctx, pl, a, w, npairs, mn, 0, it == 0, st))) return rc;
         EventPair* ue = nullptr;
@@ -253,13 +263,15 @@ int run_gicp(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_m
         if ((it + 1) % kActiveCheck == 0 && it + 1 < gp.max_iterations) {
             const int slot = nchk++ & 1;  // (the previous check's slot is the other one; the one before
             hf[slot] = -1;                // was read before that check was queued)
-            HIP_TRY(launch_gicp_active(w.state, npairs, active, const_cast<int32_t*>(hf + slot), st));
+            const uint32_t seq = ++ctx->gicp_seq;
+            HIP_TRY(launch_gicp_active(w.state, npairs, active, const_cast<int64_t*>(hf + slot), seq, st));
             if (prev_slot >= 0) {
                 int32_t h = 0;
-                if ((rc = wait_active(hf + prev_slot, st, &h))) return rc;
+                if ((rc = wait_active(hf + prev_slot, prev_seq, st, &h))) return rc;
                 if (h == 0) break;
             }
             prev_slot = slot;
+            prev_seq = seq;
         }
     }
     if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(a, w, npairs, st));

@@ -759,6 +759,16 @@ __global__ __launch_bounds__(kGicpSliceWG) void gicp_lin_kernel(PairArgs a, Work
         gicp_make_trial(sys, lambda, R, t, tr);
         gc.c[k] = tr;
     }
+    if (threadIdx.x == 63) {  // (independent of nt: gicp_spec = 0 runs every trial one by one from it)
+        double lambda = gs.lambda;
+        if (lambda < 0.0) {
+            double mx = 0.0;
+            const int diag[6] = {0, 6, 11, 15, 18, 20};
+            for (int q = 0; q < 6; ++q) mx = fmax(mx, fabs(sys[diag[q]]));
+            lambda = g.lm_init * mx;
+        }
+        gc.lambda0 = lambda;
+    }
     if (threadIdx.x >= 64 && threadIdx.x < 64 + kGicpSys) gc.sys[threadIdx.x - 64] = sys[threadIdx.x - 64];
     if (threadIdx.x >= 128 && threadIdx.x < 140) {
         const int q = threadIdx.x - 128;
@@ -849,7 +859,7 @@ __global__ __launch_bounds__(kGicpSliceWG) void gicp_trial_kernel(PairArgs a, Wo
         for (int k = 0; k < 3; ++k) x0[9 + k] = gc.t0[k];
         stop = 0;
         nuv = 2.0;
-        lam = nt > 0 ? gc.c[0].lambda : 0.0;
+        lam = gc.lambda0;  // (== gc.c[0].lambda when trials were solved up front)
         for (int k = 0; k < nt && !stop; ++k) {
             cur = gc.c[k];
             decide(err[k]);
@@ -939,7 +949,7 @@ __global__ void gicp_init_kernel(const float* guess, GicpState* gs, int npairs) 
 
 // number of pairs still iterating -> *out, and (host_out) with a system-scope store into pinned host
 // memory the host polls (the host's early exit between runs of iterations)
-__global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out, int32_t* host_out) {
+__global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out, int64_t* host_out, uint32_t seq) {
     __shared__ int32_t tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
@@ -949,12 +959,15 @@ __global__ void gicp_active_kernel(const PairState* st, int npairs, int32_t* out
     __syncthreads();
     if (threadIdx.x == 0) {
         *out = tot;
-        if (host_out) __hip_atomic_store(host_out, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (host_out)
+            __hip_atomic_store(host_out, (int64_t)(((uint64_t)seq << 32) | (uint32_t)tot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int32_t* host_out, hipStream_t s) {
-    hipLaunchKernelGGL(gicp_active_kernel, dim3(1), dim3(1024), 0, s, st, npairs, out, host_out);
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int64_t* host_out, uint32_t seq,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(gicp_active_kernel, dim3(1), dim3(1024), 0, s, st, npairs, out, host_out, seq);
     return hipGetLastError();
 }
 

@@ -113,7 +113,9 @@ struct icp4r_ctx {
     icp4r_host::DevBuf ego_rec, ego_off, ego_cnt, ego_feat, ego_pd, ego_scores, ego_res, ego_mask, ego_xyzi;
     // generalized ICP (icp4r_gicp.cpp): per-pair LM state, covariances, Mahalanobis, active count
     icp4r_host::DevBuf gicp_gs, gicp_cov_src, gicp_cov_tgt, gicp_mah, gicp_active, gicp_part;
-    int32_t* gicp_hflag = nullptr;  // pinned host slots the active-pair checks write (hipHostMalloc)
+    int64_t* gicp_hflag = nullptr;  // pinned host slots the active-pair checks write (hipHostMalloc):
+                                    // (check sequence << 32) | active count
+    uint32_t gicp_seq = 0;          // the last active-pair check's sequence number (grows across calls)
     icp4r_host::DevBuf gicp_sidx;   // the source's own index (its k-NN covariances, beside the target's)
     hipEvent_t gicp_fork = nullptr, gicp_join = nullptr;
     std::vector<icp4r_host::EventPair> gicp_events;  // covariance launches (the iterations time as UPDATE)

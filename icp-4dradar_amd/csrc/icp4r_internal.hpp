@@ -180,9 +180,9 @@ struct WorkArgs {
                         // plist holds items (pair << 10 | part)
     unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,
                                 // cached-neighbour hits (count_add; the host sums the slots)
-    uint64_t* ticks;    // debug (ICP4R_PHASE_TICKS=1): s_memrealtime (100 MHz) at fold_update phase
+    uint64_t* ticks;    // debug (plan option phase_ticks = 1): s_memrealtime (100 MHz) at fold_update phase
                         // boundaries of pair 0 — start, pass A, pass B, solve, transform
-    uint64_t* pass_ticks;  // debug (ICP4R_PHASE_TICKS=1): this NN pass' own slots [kPassTickSlots] of the
+    uint64_t* pass_ticks;  // debug (plan option phase_ticks = 1): this NN pass' own slots [kPassTickSlots] of the
                            // batched search's event counts / clocks (tools/experiments/nn_events.py), or nullptr
 };
 constexpr int kPassTickSlots = 16;  // per NN pass: 11 event counters / clocks + 4 per-item walls
@@ -286,6 +286,7 @@ struct GicpTrial {
 };
 struct GicpCand {  // written by the linearisation's last slice, read by the trial kernel
     GicpTrial c[kGicpSpec];
+    double lambda0;        // the iteration's first damping (lm_init * max|diag H| on the first iteration)
     double sys[kGicpSys];  // H, g, y0, |valid| at x0
     double R0[9], t0[3];   // x0
 };
@@ -313,7 +314,10 @@ hipError_t launch_gicp_knn_cov(const float4* cloud, const int64_t* off, const in
                                int npairs, int max_n, int64_t stride, int k, int reg, double* cov, int lanes,
                                hipStream_t st);
 // the number of pairs still iterating into *out and, if host_out, into pinned host memory
-hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int32_t* host_out, hipStream_t s);
+// host_out (pinned): (seq << 32) | the active count, one 64-bit store — a check's value is told apart from a
+// stale one of an earlier call still in flight by its sequence number
+hipError_t launch_gicp_active(const PairState* st, int npairs, int32_t* out, int64_t* host_out, uint32_t seq,
+                              hipStream_t s);
 hipError_t launch_gicp_iter(const PairArgs& a, const WorkArgs& w, const GicpArgs& g, int npairs, int max_n, int it,
                             hipStream_t st);
 

@@ -824,7 +824,7 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
         if (kdn)
             for (int k = tid; k < kKdnStride; k += kIdxWG) kdn[k] = 0u;  // (kd_order syncs before writing)
         // the quantised keys' scratch (3 x kKdMaxN u16): the pair's query-record area, unused until
-        // the source order / first search writes it (ICP4R_KD_KEYS=0: the levels re-read the points)
+        // the source order / first search writes it (compile-time ICP4R_KD_KEYS=0: the levels re-read the points)
         // (targets only: a pair's source build may run beside it on the same area)
         uint16_t* gk = (ICP4R_KD_KEYS && is_tgt && w.qv && (int64_t)w.x_stride * (int64_t)sizeof(float4) >= 3 * kKdMaxN * 2)
                            ? reinterpret_cast<uint16_t*>(w.qv + (int64_t)p * w.x_stride)
@@ -2201,7 +2201,7 @@ __global__ __launch_bounds__(kOrderWG) void nn_order_kernel(PairArgs a, WorkArgs
 }
 
 // Counters of the LDS search runs (device work counts; per-wave events and clocks for
-// ICP4R_PHASE_TICKS=1 — tools/experiments/nn_events.py)
+// plan option phase_ticks = 1 — tools/experiments/nn_events.py)
 struct RunStats {
     unsigned long long evals = 0, tests = 0;
     uint32_t ev_runs = 0, ev_q = 0, ev_sbv = 0, ev_sbp = 0, ev_blk = 0, ev_push = 0, ev_drain = 0, ev_items = 0;
@@ -2610,7 +2610,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     // keys: without the cached-neighbour state the next search's seed and the records read them
     const bool want_key = !CACHE || keys_read(a, fitness_pass);
     const int npl = uload(w.plist_n);
-    // work counters; debug event counters and per-phase clocks of every wave (ICP4R_PHASE_TICKS=1:
+    // work counters; debug event counters and per-phase clocks of every wave (plan option phase_ticks = 1:
     // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
     // tools/experiments/nn_events.py): wave-uniform adds, stored once at the end
     RunStats rs;
@@ -2619,7 +2619,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         __syncthreads();
         const int idx = sh.cur;
         if (idx >= npl) break;  // uniform: every wave read the same sh.cur
-        // debug (ICP4R_PHASE_TICKS=1): per-pair compaction / staging / search wall time, summed over
+        // debug (plan option phase_ticks = 1): per-pair compaction / staging / search wall time, summed over
         // the pairs of the launch into ticks[8..10], pairs in ticks[11]
         const bool tk = w.ticks != nullptr && tid == 0;
         uint64_t tk0 = tk ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = tk0, tk2 = tk0;
@@ -5150,7 +5150,7 @@ __global__ __launch_bounds__(kResWG, 2) void fold_update_res_kernel(PairArgs a, 
 // chains over larger chunks; pass B runs the sigma panels side by side (fold_pass_b<PAR>: up to 14
 // panels, 9 chains each, over chunks of 128 steps per panel), so its chain is one panel (kc) long
 // instead of |C|, and the 14 filler waves stage a chunk in one round trip.  Same results bit for bit
-// as fold_update_kernel (the parity tests run both; ICP4R_WIDE_UPDATE=0 selects the narrow one).
+// as fold_update_kernel (the parity tests run both; plan option wide_update = 0 selects the narrow one).
 constexpr int kWideWG = 1024;
 constexpr int kWideChunkP = 1792;  // points per pass-A chunk; pass B: 9 x 14 panel rows of 128 steps
 constexpr int kWideRow = kWideChunkP + kFoldPad;
@@ -5500,7 +5500,7 @@ __global__ __launch_bounds__(kFinWG) void finish_kernel(PairArgs a, WorkArgs w) 
 constexpr int kSoloWG = kLdsWG;
 constexpr int kSoloFitChunk = 960;  // fitness chunk: 15 waves fill, wave 0 lane 0 folds
 constexpr int kSoloGrp = 4;         // the first pass' sorted positions in flight per thread
-// LDS.  ICP4R_SOLO_RESIDENT=1: the pair's target tile stays resident for the whole registration,
+// LDS.  (compile-time) ICP4R_SOLO_RESIDENT=1: the pair's target tile stays resident for the whole registration,
 // and the search's per-wave state, the update's fold buffers (192-point chunks), the test's bitmap
 // and records and the fitness chunks take turns in the 18 KB beside it.  0: the tile and the
 // update's 512-point fold buffers (fold_update_kernel's) take turns in one region, the tile
@@ -5688,7 +5688,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
                        isl, ish, a, w, p, xs0, w.X + xs0, w.nn_key + xs0, keys, false, rs);
         __syncthreads();
     };
-    // debug (ICP4R_PHASE_TICKS=1): pair 0's phase walls summed over the registration (s_memrealtime,
+    // debug (plan option phase_ticks = 1): pair 0's phase walls summed over the registration (s_memrealtime,
     // 100 MHz) into ticks[0..9]: staging, test, search, pass A, pass B, solve, fitness test, fitness
     // search, fitness sum, iterations (tools/experiments/solo_phases.py)
     unsigned long long* tk = (w.ticks && p == 0 && tid == 0) ? reinterpret_cast<unsigned long long*>(w.ticks) : nullptr;
@@ -5712,7 +5712,7 @@ __global__ __launch_bounds__(kSoloWG) void solo_kernel(PairArgs a, WorkArgs w, i
         tick(0);
         for (int it = 0; it < iters && flag == 0; ++it) {
             // (first pass: src_order_kernel wrote the records, seeded at the source's kd leaf in the
-            // target's tree, when the sources are ordered by it — ICP4R_SRC_ORDER=1)
+            // target's tree, when the sources are ordered by it — plan option src_order = 1)
             const int nlist = it > 0 ? solo_cache_test<false>(a, w, p, n, T, sh, tk)
                               : (w.stage_first && src_by_tgt_tree(a, w, p)) ? n : solo_first_list(a, w, p, n, m);
             tick(1);

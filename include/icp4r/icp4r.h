@@ -174,10 +174,11 @@ int icp4r_nearest(icp4r_ctx* ctx, const float* query, int32_t n, int32_t query_s
 int icp4r_synchronize(icp4r_ctx* ctx, void* hip_stream);
 
 /* Device-time accounting with HIP events on the launch stream (used by bench.py for the roofline):
- * icp4r_kernel_time_ms: average duration of the NN kernel launches (the dominant kernel: the batched
- *                       search nn_lds_kernel, the tiled search nn_tile_kernel, or the whole NN
- *                       launch of the other plans)
- *                       recorded since the last reset, and how many there were;
+ * icp4r_kernel_time_ms: average duration of the NN kernel launches (the batched search
+ *                       nn_lds_kernel, the tiled search nn_tile_kernel, or the whole NN launch of the
+ *                       other plans) recorded since the last reset, and how many there were — the
+ *                       update's launches are icp4r_stage_time_ms(ICP4R_STAGE_UPDATE); which of the
+ *                       two dominates a step depends on the plan (at C3 it is the update);
  * icp4r_batch_time_ms:  average duration of whole registration calls (all launches of a batch). */
 int icp4r_kernel_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* launches);
 int icp4r_batch_time_ms(icp4r_ctx* ctx, double* avg_ms, int32_t* calls);

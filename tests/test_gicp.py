@@ -217,7 +217,7 @@ def test_gpu_lm_trials_speculative_equals_one_by_one(gpu_ctx, oracle_mod, plan):
     """The iteration evaluates its first LM trials together (plan option gicp_spec, default 2) and any
     further trial one by one, each summed slice by slice in the same order: every gicp_spec gives
     bit-identical results, and so does every spread of the slices over workgroups (gicp_grid). Cases: far initial poses (rejected trials), lm_max_iterations = 1 and 0,
-    and a source of 17k points (512-point slices)."""
+    a large initial damping (lm_init_lambda_factor 1e-2), and a source of 17k points (512-point slices)."""
     gicp = _gicp()
     cases = []
     for seed in (0, 3):
@@ -228,6 +228,9 @@ def test_gpu_lm_trials_speculative_equals_one_by_one(gpu_ctx, oracle_mod, plan):
         guess[:3, 3] = [0.8, -0.5, 0.3]
         for lm in (10, 1, 0):
             cases.append((src, tgt, guess, gicp.default_params(k_correspondences=5, lm_max_iterations=lm)))
+        # a damping large enough to change every step: the first λ must be the same whether the trials
+        # are solved up front (gicp_spec > 0) or one by one (gicp_spec = 0)
+        cases.append((src, tgt, guess, gicp.default_params(k_correspondences=5, lm_init_lambda_factor=1e-2)))
     src, tgt, _ = _scene(9, 17000)
     cases.append((src, tgt, None, gicp.default_params(k_correspondences=5)))
     for src, tgt, guess, p in cases:
@@ -277,6 +280,54 @@ def test_gpu_batch_device_equals_single(gpu_ctx):
         np.testing.assert_array_equal(out[i]["T"], np.array(r.T, np.float32))
         assert out[i]["iterations"] == r.iterations and out[i]["converged"] == r.converged
         assert out[i]["fitness"] == r.fitness
+
+
+@pytest.mark.gpu
+def test_gpu_device_calls_back_to_back(gpu_ctx):
+    """Two device-API calls on one context with no synchronisation between them (the API returns with
+    its work queued): the second must not read the first's late active-pair check — each check carries
+    a sequence number — and both equal the same pairs registered alone."""
+    import torch
+
+    import icp4r
+
+    gicp = _gicp()
+    dev = torch.device("cuda:0")
+
+    def batch(pairs):
+        src = np.concatenate([np.pad(p[0], ((0, 0), (0, 1))) for p in pairs]).astype(np.float32)
+        tgt = np.concatenate([np.pad(p[1], ((0, 0), (0, 1))) for p in pairs]).astype(np.float32)
+        sn = np.array([len(p[0]) for p in pairs], np.int32)
+        tn = np.array([len(p[1]) for p in pairs], np.int32)
+        so = np.concatenate([[0], np.cumsum(sn)[:-1]]).astype(np.int64)
+        to = np.concatenate([[0], np.cumsum(tn)[:-1]]).astype(np.int64)
+        ts = {k: torch.from_numpy(v).to(dev) for k, v in dict(src=src, tgt=tgt, sn=sn, tn=tn, so=so, to=to).items()}
+        b = icp4r.Batch()
+        b.src, b.tgt = ts["src"].data_ptr(), ts["tgt"].data_ptr()
+        b.src_off, b.src_n, b.tgt_off, b.tgt_n = ts["so"].data_ptr(), ts["sn"].data_ptr(), ts["to"].data_ptr(), ts["tn"].data_ptr()
+        b.npairs, b.max_src_n, b.max_tgt_n = len(pairs), int(sn.max()), int(tn.max())
+        return b, ts
+
+    # the first batch stops early (identical clouds converge at once) while the second needs many
+    # iterations: a late check of the first would read "0 active" and stop the second
+    first = [(p[1].copy(), p[1], None) for p in (_scene(s, 1200) for s in range(3))]
+    second = [_scene(10 + s, 1500) for s in range(3)]
+    p1 = gicp.default_params(k_correspondences=5)
+    p2 = gicp.default_params(k_correspondences=5, max_iterations=40)
+    b1, keep1 = batch(first)
+    b2, keep2 = batch(second)
+    r1 = torch.zeros(len(first) * icp4r.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    r2 = torch.zeros(len(second) * icp4r.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        gicp.align_batch_device(b1, p1, r1.data_ptr(), ctx=gpu_ctx)
+        gicp.align_batch_device(b2, p2, r2.data_ptr(), ctx=gpu_ctx)
+    gpu_ctx.synchronize()
+    for res, pairs, p in ((r1, first, p1), (r2, second, p2)):
+        out = np.frombuffer(res.cpu().numpy().tobytes(), icp4r.RESULT_DTYPE)
+        for i, (s, t, _) in enumerate(pairs):
+            r, _ = gicp.align(s, t, p, ctx=gpu_ctx)
+            np.testing.assert_array_equal(out[i]["T"], np.array(r.T, np.float32))
+            assert out[i]["iterations"] == r.iterations and out[i]["converged"] == r.converged
 
 
 @pytest.mark.gpu
