@@ -269,12 +269,22 @@ def pmc_traffic(config: str, kernel: str, sha: str | None):
             pmc = json.load(f)
     except (OSError, ValueError):
         return None, "no profiles/pmc_traffic.json"
-    if not sha or pmc.get("library_sha256") != sha:
-        return None, "profiles/pmc_traffic.json was measured on another build of the library (sha256 differs)"
+    if sha and pmc.get("library_sha256") == sha:
+        same = "same library build"
+    else:
+        # the library differs: the row still holds when the ICP kernels' sources, their launch code,
+        # headers and build flags are the ones profiled (a rebuild after a GICP / map / ego change)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from srchash import icp_sources_sha256
+
+        src = icp_sources_sha256()
+        if not src or pmc.get("icp_sources_sha256") != src:
+            return None, "profiles/pmc_traffic.json was measured on another build of the ICP kernels (sha256 differs)"
+        same = "same ICP kernel sources and build flags (library sha256 differs elsewhere)"
     row = pmc.get("configs", {}).get(config, {}).get(kernel)
     if not row or "hbm_bytes_per_launch" not in row:
         return None, f"no PMC row for {kernel} in {config}"
-    return row["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({pmc.get('tag')}), same library build"
+    return row["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({pmc.get('tag')}), {same}"
 
 
 # The sequential float folds of the PCL-numerics update (Eigen's rowwise().sum() and

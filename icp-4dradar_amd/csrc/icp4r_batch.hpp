@@ -37,7 +37,8 @@ enum PlanOpt : int {
     kOptNnQ, kOptLeaf, kOptChunkSb, kOptNnLds, kOptNnCache, kOptNnTile, kOptTileRun, kOptSolo, kOptXpad,
     kOptPhaseTicks, kOptKd, kOptMortonMwg, kOptPart, kOptSrcOrder, kOptFuseSeed, kOptTileOwn, kOptTileDefer,
     kOptGroups, kOptSearchCuDiv, kOptFuseTest, kOptFuseOrder, kOptSumsTail, kOptWideUpdate, kOptGatherPadded,
-    kOptGicpCovBrute, kOptFoldKeys, kOptGicpSpec, kOptGicpGrid, kOptGicpKnnLanes, kOptResUpdate, kNumPlanOpts
+    kOptGicpCovBrute, kOptFoldKeys, kOptGicpSpec, kOptGicpGrid, kOptGicpKnnLanes, kOptResUpdate, kOptHeldUpdate,
+    kNumPlanOpts
 };
 static_assert(kNumPlanOpts <= 32, "icp4r_ctx::plan_set is a 32-bit mask");
 extern const char* const kPlanOptNames[kNumPlanOpts];

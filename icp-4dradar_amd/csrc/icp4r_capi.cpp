@@ -104,7 +104,8 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad",
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
-    "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update"};
+    "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update",
+    "held_update"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
     return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
@@ -590,6 +591,10 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     // at most one pair per CU: the update in one 1024-thread workgroup per pair, its sigma panels side
     // by side (plan option wide_update = 0: fold_update_kernel's 256 threads)
     const bool wide = pcl && !fuse && npairs <= ctx->ncu && opt(ctx, kOptWideUpdate, 1) != 0;
+    // ... with the records held in registers from pass A to pass B for sources of at most kHeldMaxN
+    // points (fold_update_held_kernel; plan option held_update = 0: fold_update_wide_kernel)
+    for (int g = 0; g < groups; ++g)
+        wg[g].held_update = (wide && mn <= kHeldMaxN && opt(ctx, kOptHeldUpdate, kDefaultHeldUpdate) != 0) ? 1 : 0;
     // ... which, on the multi-tile plan (the scan-to-map target), forms the correspondence records in
     // its pass A instead of corr_kernel after every search (plan option fold_keys = 0: corr_kernel)
     if (wide && pl.tile && !pl.lds && w.corr && (pl.chunks > 1 || !w.tile_own) && opt(ctx, kOptFoldKeys, 1) != 0)
@@ -1104,7 +1109,7 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
             0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid,
-            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate};
+            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;
@@ -1132,6 +1137,7 @@ int icp4r_plan(const icp4r_ctx* ctx, int32_t npairs, int32_t max_src_n, int32_t 
     const int ncu = ctx ? ctx->ncu : 256;
     const bool fuse = pl.lds && pl.cache && pcl && opt(ctx, kOptFuseTest, 1) != 0;
     out->wide_update = (pcl && !pl.solo && !fuse && npairs <= ncu && opt(ctx, kOptWideUpdate, 1) != 0) ? 1 : 0;
+    out->held_update = (out->wide_update && max_src_n <= kHeldMaxN && opt(ctx, kOptHeldUpdate, kDefaultHeldUpdate) != 0) ? 1 : 0;
     out->res_update = (fuse && max_src_n <= kResMaxN && opt(ctx, kOptSumsTail, 0) == 0 && opt(ctx, kOptResUpdate, kDefaultResUpdate) != 0) ? 1 : 0;
     out->q = pl.q;
     out->splits = pl.splits;

@@ -159,6 +159,8 @@ struct WorkArgs {
                           // targets and writes them for pass B
     int32_t res_update;   // 1 (batched plan, sources <= kResMaxN): fold_update_res_kernel, the pair held on
                           // chip across the update (plan option res_update = 0: fold_update_kernel)
+    int32_t held_update;  // 1 (wide update, sources <= kHeldMaxN): fold_update_held_kernel, the records held
+                          // in the fillers' registers from pass A to pass B (plan option held_update)
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |
                         // the query's sorted position << 14 (nt_pack)
     float4* sq;         // [npairs * x_stride] the pass's miss list in the order the test found them: a
@@ -215,6 +217,8 @@ constexpr int kLdsMinPairs = 256;     // ... used for batches of at least this m
 constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (14-bit index / position fields)
 constexpr int kResMaxN = 8192;            // fold_update_res_kernel: sources of at most this many points
 constexpr int kDefaultResUpdate = 0;      // ... plan option res_update's default
+constexpr int kHeldMaxN = 3 * 896;        // fold_update_held_kernel: sources of at most this many points
+constexpr int kDefaultHeldUpdate = 1;     // ... plan option held_update's default
 constexpr int kSoloMaxN = 1024;           // solo_kernel by default for single pairs of at most this many sources
 // wide: one 1024-thread workgroup per pair (fold_update_wide_kernel) — plans with at most one pair
 // per CU and neither the fused test nor the fused work list

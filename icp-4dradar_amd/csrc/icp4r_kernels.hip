@@ -2834,72 +2834,98 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     const int nb = (tm + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
     const int64_t xs0 = (int64_t)p * w.x_stride;
     unsigned long long evals = 0, tests = 0;
+    // debug (plan option phase_ticks = 1): workgroup (0, 0, 0)'s stamps in the pass' slots 0..4, and
+    // over every workgroup the earliest start (slot 6, as its complement) and the latest end (slot 5)
+    unsigned long long* tk = (w.pass_ticks && tid == 0) ? reinterpret_cast<unsigned long long*>(w.pass_ticks) : nullptr;
+    const bool tk0 = tk && tile == 0 && part == 0 && p == 0;
+    const unsigned long long tk_in = tk ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (tk0) tk[0] = tk_in;
+    if (tk) atomicMax(tk + 6, ~tk_in);
 
-    // Stage the tile (whole superblocks: tsort is padded to them), every load before the first store.
-    v4f isl, ish;
-    {
-        const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride + t0);
-        const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride) + 2 * (t0 / kLdsLeaf);
-        const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride) + 2 * (t0 / (kLdsLeaf * kSuper));
-        const int nt = nsb * kSuper * kLdsLeaf;
-        constexpr int kPerT = kLdsTargets / kLdsWG;
-        v4f tv[kPerT];
-#pragma unroll
-        for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * kLdsWG, nt - 1)];
-        const int nbx = nsb * (kSuper + 1);
-        const int bq = min(tid, nbx - 1);
-        const bool blk = bq < nsb * kSuper;
-        const int kb = blk ? bq : bq - nsb * kSuper;
-        const v4f blo = blk ? tb[2 * kb] : sbg[2 * kb], bhi = blk ? tb[2 * kb + 1] : sbg[2 * kb + 1];
-#pragma unroll
-        for (int k = 0; k < kPerT; ++k) {
-            const int i = tid + k * kLdsWG;
-            if (i < nt) {
-                sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
-            }
-        }
-        if (tid < nbx) {
-            const bool empty = !(blo.x <= bhi.x);
-            float* d = blk ? sh.bx[kb] : sh.sbx[kb];
-            d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
-            d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
-        }
-        const int sbl = min(lane, nsb - 1);
-        isl = sbg[2 * sbl];
-        ish = sbg[2 * sbl + 1];
-    }
-    __syncthreads();
+    // Stage the tile (whole superblocks: tsort is padded to them), every load before the first store,
+    // with the query's chain of dependent loads beside it: the query's sorted position goes out first,
+    // then the tile, then its point and key (behind the position only: the tile's loads stay in
+    // flight), the seed target, and the tile's LDS stores while that last load is out.  (The chain had
+    // started after the staging barrier: ~1.2 us of a 2k pass' 5.4 per workgroup; behind the tile's
+    // loads it would wait for them at its first step.)
     const int r0 = q0 + wave * qrun;  // this wave's run: sorted sources [r0, r0 + qrun)
-    if (r0 >= n) return;              // (no barrier follows)
+    const bool wrun = r0 < n;         // (wave-uniform)
+    const bool live = wrun && lane < qrun && r0 + lane < n;
+    const int sq = live ? r0 + lane : min(r0, n - 1);
+    // (unconditional loads, clamped: a load under a branch merges into a copy that waits for it)
+    const int o = w.sperm[xs0 + sq];  // idle lanes shadow the run's first query
+    __builtin_amdgcn_sched_barrier(0);  // (the order of issue above and below is the point)
+    const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride + t0);
+    const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride) + 2 * (t0 / kLdsLeaf);
+    const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride) + 2 * (t0 / (kLdsLeaf * kSuper));
+    const int nt = nsb * kSuper * kLdsLeaf;
+    constexpr int kPerT = kLdsTargets / kLdsWG;
+    v4f tv[kPerT];
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) tv[k] = tsg[min(tid + k * kLdsWG, nt - 1)];
+    const int nbx = nsb * (kSuper + 1);
+    const int bq = min(tid, nbx - 1);
+    const bool blk = bq < nsb * kSuper;
+    const int bk = blk ? bq : bq - nsb * kSuper;
+    const v4f blo = blk ? tb[2 * bk] : sbg[2 * bk], bhi = blk ? tb[2 * bk + 1] : sbg[2 * bk + 1];
+    const int sbl = min(lane, nsb - 1);
+    const v4f isl = sbg[2 * sbl], ish = sbg[2 * sbl + 1];
+    __builtin_amdgcn_sched_barrier(0);
+
     unsigned long long* bestl = sh.best[wave];
     uint16_t* ring = sh.items[wave];
     NNKey* key = w.nn_key + xs0;
-    const bool live = lane < qrun && r0 + lane < n;
-    const int sq = live ? r0 + lane : r0;
-    const int o = w.sperm[xs0 + sq];  // idle lanes shadow the run's first query
+    float x = 0.f, y = 0.f, z = 0.f;
+    NNKey init = 0;
     float4 v = w.X[xs0 + o];
-    if (own && first == 0 && !fitness_pass && w.defer_xform) {
-        // the previous update's transformCloud(T_inc), deferred to here (one read and write of X
-        // per pass instead of a pass over the cloud by the update's one workgroup); every query
-        // belongs to one lane of one workgroup of the single tile, which writes it back
-        float T[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].T_inc[q]);
-        xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
-        if (live) w.X[xs0 + o] = v;
-    }
     NNKey k0 = key[o];
-    const float x = v.x, y = v.y, z = v.z;
-    if (own) {  // the seed (nn_seed_kernel's rule), evaluated at the query's current position
-        const uint32_t j = (first && !seed_key(k0, m))
-                               ? __float_as_uint(w.tsort[(int64_t)p * w.t_stride + ((int64_t)sq * m) / n].w)
-                               : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
-        const float4 t = a.tgt[uload(a.tgt_off + p) + j];
-        k0 = make_key(l2_simple(x, y, z, t.x, t.y, t.z), j);
+    uint32_t j = 0;
+    float4 t;
+    {
+        if (own && first == 0 && !fitness_pass && w.defer_xform) {
+            // the previous update's transformCloud(T_inc), deferred to here (one read and write of X
+            // per pass instead of a pass over the cloud by the update's one workgroup); every query
+            // belongs to one lane of one workgroup of the single tile, which writes it back
+            float T[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].T_inc[q]);
+            xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
+            if (live) w.X[xs0 + o] = v;
+        }
+        x = v.x;
+        y = v.y;
+        z = v.z;
+        // the seed (nn_seed_kernel's rule, own: evaluated at the query's current position); loaded on
+        // every plan for the same reason (the multi-tile plan does not use it)
+        j = (own && first && !seed_key(k0, m)) ? __float_as_uint(w.tsort[(int64_t)p * w.t_stride + ((int64_t)sq * m) / n].w)
+                                               : min((uint32_t)key_idx(k0), (uint32_t)(m - 1));
+        t = a.tgt[uload(a.tgt_off + p) + j];
     }
-    // the current key in the tile's encoding, ranked after every real target of the same (d², index)
-    const NNKey init = make_key(key_d2(k0), ((uint32_t)key_idx(k0) << kLdsPosBits) | ((1u << kLdsPosBits) - 1));
-    bestl[lane] = init;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) {
+        const int i = tid + k * kLdsWG;
+        if (i < nt) {
+            sh.tl[lds_swz(i)] = tl_slot(tv[k], (__float_as_uint(tv[k].w) << kLdsPosBits) | (uint32_t)i);
+        }
+    }
+    if (tid < nbx) {
+        const bool empty = !(blo.x <= bhi.x);
+        float* d = blk ? sh.bx[bk] : sh.sbx[bk];
+        d[0] = empty ? FLT_MAX : blo.x; d[1] = empty ? FLT_MAX : blo.y; d[2] = empty ? FLT_MAX : blo.z;
+        d[3] = empty ? FLT_MAX : bhi.x; d[4] = empty ? FLT_MAX : bhi.y; d[5] = empty ? FLT_MAX : bhi.z;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (wrun) {
+        if (own) k0 = make_key(l2_simple(x, y, z, t.x, t.y, t.z), j);
+        // the current key in the tile's encoding, ranked after every real target of the same (d², index)
+        init = make_key(key_d2(k0), ((uint32_t)key_idx(k0) << kLdsPosBits) | ((1u << kLdsPosBits) - 1));
+        bestl[lane] = init;  // (sh.best: not staged)
+    }
+    if (tk0) tk[2] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (tk0) tk[1] = __builtin_amdgcn_s_memrealtime();
+    if (!wrun) return;  // (no barrier follows)
     float bnd = live ? key_d2(k0) * kLbGrow : -1.0f;
     float qlo[3] = {x, y, z}, qhi[3] = {x, y, z};
 #pragma unroll
@@ -2972,6 +2998,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     }
     if (tail != head) drain(tail - head);
     const NNKey kb = bestl[lane];
+    if (tk0) tk[3] = __builtin_amdgcn_s_memrealtime();
     if (own) {
         // the seed target lies in the tile and its block's bound cannot prune it, so the winner is a
         // real LDS slot; the sentinel position (kb == init) is handled all the same
@@ -2992,6 +3019,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     if (lane == 0) {
         count_add(w.evals, 0, evals);
         count_add(w.evals, 1, tests);
+    }
+    if (tk) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        if (tk0) tk[4] = t;
+        atomicMax(tk + 5, t);
     }
 }
 
@@ -5217,6 +5249,288 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
 }
 
 // ---------------------------------------------------------------------------------------------
+// fold_update_held_kernel (round 6): fold_update_wide_kernel for sources of at most kHeldMaxN points
+// (the node's C1 scan), with the pair's correspondence records read from HBM once per update.  The
+// 896 filler threads (waves 2..15) load their records (up to kHeldMax each: record i is filler
+// i mod 896's slot i / 896) before the first barrier, every load in flight together, and keep them in
+// registers: pass A's chunk c is slot c of every filler (LDS stores only, no round trip per chunk),
+// and pass B's panel chunks take each record's nine products from the filler that holds it — the
+// wide kernel's fill of every pass-B chunk was a global round trip (2.3 us of its 7.5 on C1).
+// Waves 0 and 1 (the fold lanes, the MSE wave) hold nothing: the roles run as separate wave-uniform
+// loops, so the held records are never live beside fold_seq's 96 registers.  The chains, their
+// orders and the panel adds are fold_pass_a / fold_pass_b<PAR>'s, so the results are the wide
+// kernel's bit for bit; pass B takes that kernel's global path when a correspondence was rejected or
+// weighted (the panels then start by rank), for one panel, or for more panels than one group.
+constexpr int kHeldFill0 = 128;                       // first filler thread
+constexpr int kHeldFillers = kWideWG - kHeldFill0;    // 896
+constexpr int kHeldMax = kHeldMaxN / kHeldFillers;    // records per filler
+constexpr int kHeldCH = 2 * kHeldFillers;             // pass A chunk: two slots of every filler
+static_assert(kHeldCH <= kWideChunkP, "pass A's chunk fits the wide buffers");
+
+__global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, WorkArgs w) {
+    __shared__ WideShared sh;
+    const int p = xcd_remap(blockIdx.x, gridDim.x);
+    PairState& st = w.state[p];
+    if (st.phase != kPhaseActive) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int n = a.src_n[p];
+    const int64_t xs = w.x_stride;
+    const KParams& kp = a.kp;
+    const float4* C = w.corr ? w.corr + (int64_t)p * xs * 2 : nullptr;
+    const float4* Xp = w.X + (int64_t)p * xs;
+    const float4* NT = w.nn_t ? w.nn_t + (int64_t)p * xs : nullptr;
+    const bool ticks = w.ticks != nullptr && p == 0 && tid == 0;
+    // key mode (w.fold_keys): X and the merged keys' targets; the records are written for pass B's
+    // global path (corr_kernel's work, as in the wide kernel)
+    const bool keys = w.fold_keys && C;
+    const NNKey* K = keys ? w.nn_key + (int64_t)p * xs : nullptr;
+    const float4* TG = keys ? a.tgt + a.tgt_off[p] : nullptr;
+    const bool weighted = kp.huber_delta < INFINITY;
+    const bool mse = kp.need_mse != 0;
+    const float ident = weighted ? 0.0f : -0.0f;
+    const int nch = (n + kHeldCH - 1) / kHeldCH;
+    const int f = tid - kHeldFill0;  // filler slot column (waves 2..15)
+
+    // the records (fillers only): loaded inside pass A's filler branch, so that they are never live
+    // in the fold wave's branch (a load ahead of the role branches kept them live there, beside
+    // fold_seq's registers)
+    float4 r0[kHeldMax], r1[kHeldMax];
+    clear_need(w, p, n, tid, kWideWG);
+    if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- pass A (fold_pass_a's chains over chunks of kHeldFillers points)
+    int cnt = 0;
+    auto store_a = [&](int c) __attribute__((always_inline)) {  // slots 2c, 2c + 1 of this filler -> chunk c
+        float(*b)[kWideRow] = sh.buf[c & 1];
+#pragma unroll
+        for (int k = 0; k < kHeldMax; ++k) {
+            if ((k >> 1) != c) continue;
+            const int i = k * kHeldFillers + f;
+            if (i >= n) continue;
+            const int o = i - c * kHeldCH;
+            const float d2 = r1[k].w;
+            const float sv[6] = {r0[k].x, r0[k].y, r0[k].z, r1[k].x, r1[k].y, r1[k].z};
+            float v[6], wt = 0.0f, dd = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) v[q] = ident;
+            if (!(d2 > kp.max_d2)) {
+                wt = r0[k].w;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) v[q] = weighted ? wt * sv[q] : sv[q];
+                dd = d2;
+                ++cnt;
+            }
+#pragma unroll
+            for (int q = 0; q < 6; ++q) b[q][o] = v[q];
+            b[6][o] = wt;
+            reinterpret_cast<double*>(b[7])[o] = (double)dd;
+        }
+    };
+    float acc = (lane < 6) ? ident : 0.0f;
+    double dacc = 0.0;
+    if (wv == 0) {
+        fold_prio(true);
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (ticks && c < 4) w.ticks[20 + c] = __builtin_amdgcn_s_memrealtime();
+            if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], min(kHeldCH, n - c * kHeldCH), acc);
+        }
+        fold_prio(false);
+        if (ticks) w.ticks[24] = __builtin_amdgcn_s_memrealtime();
+    } else if (wv == 1) {
+        if (mse) {  // the MSE sum's exact form (fold_pass_a), the whole wave per chunk
+            uint64_t xsum = 0;
+            int xe = INT_MAX;
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                const double* dv = reinterpret_cast<const double*>(sh.buf[c & 1][7]);
+                const int len = min(kHeldCH, n - c * kHeldCH);
+                for (int o = lane; o < len; o += 64) lane_exact_add(dv[o], xsum, xe);
+            }
+            wave_exact_total(xsum, xe);
+            dacc = xsum >= kExactSat ? -1.0 : (xe == INT_MAX ? 0.0 : ldexp((double)xsum, xe));
+        } else {
+            for (int c = 0; c < nch; ++c) __syncthreads();
+        }
+    } else {
+        // the held records, every load in flight together
+        if (keys) {
+            uint32_t ti[kHeldMax];
+#pragma unroll
+            for (int k = 0; k < kHeldMax; ++k) {
+                const int i = min(f + k * kHeldFillers, n - 1);
+                r0[k] = Xp[i];
+                ti[k] = (uint32_t)key_idx(K[i]);
+            }
+#pragma unroll
+            for (int k = 0; k < kHeldMax; ++k) r1[k] = TG[ti[k]];
+        } else {
+            // (one 16-B load per float4: with the two modes' loads merged, the second one's pointer
+            // lost its alignment and was split into four dword loads — 2.4 us more for the chunk)
+#pragma unroll
+            for (int k = 0; k < kHeldMax; ++k) {
+                const int i = min(f + k * kHeldFillers, n - 1);
+                const float4* q0 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i : Xp + i, 16));
+                const float4* q1 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i + 1 : NT + i, 16));
+                r0[k] = *q0;
+                r1[k] = *q1;
+            }
+        }
+        // d² and the weight of the cached-neighbour form (X, NT) and of key mode, once per record
+#pragma unroll
+        for (int k = 0; k < kHeldMax; ++k) {
+            if (!C || keys) {
+                const float d2 = l2_simple(r0[k].x, r0[k].y, r0[k].z, r1[k].x, r1[k].y, r1[k].z);
+                r0[k].w = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
+                r1[k].w = d2;
+            }
+            const int i = f + k * kHeldFillers;
+            if (keys && i < n) {
+                w.corr[(int64_t)p * xs * 2 + 2 * i] = r0[k];
+                w.corr[(int64_t)p * xs * 2 + 2 * i + 1] = r1[k];
+            }
+        }
+        store_a(0);
+        if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[25] = __builtin_amdgcn_s_memrealtime();
+        if (w.ticks != nullptr && p == 0 && lane == 0)
+            atomicMax(reinterpret_cast<unsigned long long*>(w.ticks) + 27, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            if (c + 1 < nch) store_a(c + 1);
+        }
+    }
+    // |C|: exact integer reduction of the fillers' counts
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0) sh.cnt[wave] = cnt;
+    if (wave == 0 && lane < 7) sh.res[lane] = acc;
+    if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;
+    __syncthreads();
+    if (tid == 0) {
+        int total = 0;
+        for (int k = 0; k < kWideWG / 64; ++k) total += sh.cnt[k];
+        sh.s.mom[0] = (double)total;
+        const float one_over_n = 1.0f / sh.res[6];
+        sh.s.one_over_n = one_over_n;
+        for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
+    }
+    __syncthreads();
+    if (ticks) w.ticks[26] = __builtin_amdgcn_s_memrealtime();
+    if (mse && sh.s.mse_sum < 0.0) {  // (uniform) PCL's sequential double chain over the chunks again
+        dacc = 0.0;
+        if (wv == 0) {
+            for (int c = 0; c < nch; ++c) __syncthreads();
+        } else if (wv == 1) {
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (lane == 0)
+                    dacc = fold_seq_d(reinterpret_cast<const double*>(sh.buf[c & 1][7]), min(kHeldCH, n - c * kHeldCH), dacc);
+            }
+        } else {
+            store_a(0);
+            for (int c = 0; c < nch; ++c) {
+                __syncthreads();
+                if (c + 1 < nch) store_a(c + 1);
+            }
+        }
+        __syncthreads();
+        if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;
+        __syncthreads();
+    }
+    if (ticks) w.ticks[1] = __builtin_amdgcn_s_memrealtime();
+
+    // ---- pass B
+    SolveShared& s = sh.s;
+    const int cntC = (int)s.mom[0];
+    const int kc = sigma_kc(cntC, kp.sigma_max_kc);
+    const int S = (cntC > 0 && kc > 0) ? (cntC + kc - 1) / kc : 1;
+    if (ticks) w.ticks[5] = __builtin_amdgcn_s_memrealtime();
+    if (weighted || cntC < n || S <= 1 || S > kSliceGroup) {
+        const FoldIn fin{C, Xp, NT, n};
+        fold_pass_b<kWideWG, kWideChunkP, kWideRow, true>(kp, fin, sh.buf, s);
+    } else {
+        // every correspondence kept, unweighted: panel sl = [sl kc, min((sl + 1) kc, n)), one group of
+        // S panels (fold_pass_b<PAR>'s layout: row (panel, ab) of T steps, rows strided = 4 mod 8)
+        const float ms[3] = {s.mean[0], s.mean[1], s.mean[2]};
+        const float md[3] = {s.mean[3], s.mean[4], s.mean[5]};
+        const float oon = s.one_over_n;
+        constexpr int CAP = 9 * kWideRow;
+        auto bufs = [&](int k) -> float* { return &sh.buf[k & 1][0][0]; };
+        const int G = S, R = 9 * G, FW = (R + 63) / 64;
+        const int stride = (((CAP / R) - 4) & ~7) + 4;
+        const int T = stride - 4;
+        const int nchb = (kc + T - 1) / T;  // the first panel is the longest
+        float sig = 0.0f, pacc = 0.0f;
+        if (wv < 2) {
+            const int L = tid;
+            const int my_sl = L / 9;
+            const int my_len = (wv < FW && L < R) ? min(kc, n - my_sl * kc) : 0;
+            for (int c = 0; c < nchb; ++c) {
+                __syncthreads();
+                if (ticks && c < 2) w.ticks[28 + c] = __builtin_amdgcn_s_memrealtime();
+                const int len = min(T, my_len - c * T);
+                if (wv < FW && L < R && len > 0) pacc = fold_row(bufs(c) + L * stride, len, pacc);
+            }
+            if (ticks) w.ticks[30] = __builtin_amdgcn_s_memrealtime();
+        } else {
+            // each held record's panel and step (the panel by a float reciprocal, corrected)
+            int P[kHeldMax], stp[kHeldMax];
+            const float invkc = 1.0f / (float)kc;
+#pragma unroll
+            for (int k = 0; k < kHeldMax; ++k) {
+                const int i = f + k * kHeldFillers;
+                int q = (int)((float)i * invkc);
+                int t = i - q * kc;
+                if (t >= kc) { ++q; t -= kc; }
+                if (t < 0) { --q; t += kc; }
+                P[k] = i < n ? q : -1;
+                stp[k] = t;
+            }
+            auto fill = [&](int c) __attribute__((always_inline)) {
+                float* b = bufs(c);
+#pragma unroll
+                for (int k = 0; k < kHeldMax; ++k) {
+                    const int t = stp[k] - c * T;
+                    if (P[k] < 0 || t < 0 || t >= T) continue;
+                    const float sv[3] = {r0[k].x - ms[0], r0[k].y - ms[1], r0[k].z - ms[2]};
+                    const float dv[3] = {r1[k].x - md[0], r1[k].y - md[1], r1[k].z - md[2]};
+                    float* o = b + P[k] * 9 * stride + t;
+#pragma unroll
+                    for (int ra = 0; ra < 3; ++ra)
+#pragma unroll
+                        for (int rb = 0; rb < 3; ++rb) o[(ra * 3 + rb) * stride] = dv[ra] * sv[rb];
+                }
+            };
+            if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[6] = __builtin_amdgcn_s_memrealtime();
+            fill(0);
+            if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[7] = __builtin_amdgcn_s_memrealtime();
+            if (w.ticks != nullptr && p == 0 && lane == 0)
+                atomicMax(reinterpret_cast<unsigned long long*>(w.ticks) + 8, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+            for (int c = 0; c < nchb; ++c) {
+                __syncthreads();
+                if (c + 1 < nchb) fill(c + 1);
+            }
+        }
+        __syncthreads();  // every chunk folded: the buffer of chunk nchb (unused) takes the chains
+        float* cs = bufs(nchb);
+        if (wv < FW && tid < R) cs[tid] = pacc;
+        __syncthreads();
+        if (wave == 0 && lane < 9)
+            for (int sl = 0; sl < G; ++sl) sig = sig + oon * cs[sl * 9 + lane];  // res += alpha * C0
+        if (wave == 0 && lane < 9) s.sigmaf[lane] = sig;
+        __syncthreads();
+    }
+    if (ticks) w.ticks[2] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) solve_pair_body<kNumericsPCL>(sh.s, st, kp);  // (inline: no call's register saves)
+    __syncthreads();
+    if (ticks) w.ticks[3] = __builtin_amdgcn_s_memrealtime();
+    if (sh.s.flag == 1) return;  // error: PCL breaks before transforming
+    if (!w.defer_xform) transform_pair<kWideWG>(w, p, n, sh.s.T_inc, w.seed_next && w.corr);
+    if (ticks) w.ticks[4] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---------------------------------------------------------------------------------------------
 // update_kernel (F64 numerics): one workgroup per active pair: correspondences -> double moments
 // (fixed-order block reduction) -> solve -> convergence -> X := T_inc * X.
 constexpr int kUpdWG = 512;
@@ -5994,7 +6308,9 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
     if (a.kp.numerics == kNumericsPCL) {
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
-        if (wide && !tail_test && order_ncu <= 0)
+        if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldMaxN)
+            hipLaunchKernelGGL(fold_update_held_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+        else if (wide && !tail_test && order_ncu <= 0)
             hipLaunchKernelGGL(fold_update_wide_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (w.res_update && !need_corr && !w.corr && max_n <= kResMaxN && w.nn_t && w.nn_u && w.defer_xform &&
                  a.kp.huber_delta == INFINITY && a.kp.max_d2 >= FLT_MAX &&

@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = [
 PLAN_OPTIONS = (
     "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad", "phase_ticks", "kd",
     "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer", "groups", "search_cu_div",
-    "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded", "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update",
+    "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded", "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update", "held_update",
 )
 # include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
 EGO_EXPORTED_SYMBOLS = [
@@ -138,7 +138,8 @@ class Batch(C.Structure):
 class PlanInfo(C.Structure):
     _fields_ = [("pruned", C.c_int32), ("q", C.c_int32), ("splits", C.c_int32), ("leaf", C.c_int32),
                 ("lds", C.c_int32), ("cache", C.c_int32), ("nn_blocks", C.c_int64), ("solo", C.c_int32),
-                ("wide_update", C.c_int32), ("res_update", C.c_int32)]
+                ("wide_update", C.c_int32), ("res_update", C.c_int32),
+                ("held_update", C.c_int32)]
 
 
 assert C.sizeof(Result) == 96
@@ -405,7 +406,8 @@ def plan(npairs: int, max_src_n: int, max_tgt_n: int, nn_mode: int = NN_AUTO, nu
                              C.byref(info)), "icp4r_plan")
     return {"pruned": bool(info.pruned), "lds": bool(info.lds), "cache": bool(info.cache), "q": info.q, "splits": info.splits,
             "leaf": info.leaf, "nn_blocks": info.nn_blocks, "solo": bool(info.solo),
-            "wide_update": bool(info.wide_update), "res_update": bool(info.res_update)}
+            "wide_update": bool(info.wide_update), "res_update": bool(info.res_update),
+            "held_update": bool(info.held_update)}
 
 
 _default_ctx: Context | None = None

@@ -8,7 +8,8 @@
   read on gfx950, so it is doubled; WRITE_SIZE is taken as-is.  Units: FETCH_SIZE / WRITE_SIZE are
   in KiB.  Launches differ per ICP pass: the mean over the launches matches the average launch time.
   -> profiles/pmc_traffic.json, under configs[<config>][<kernel>], stamped with the sha256 of the
-  library build that was profiled (bench.py uses a row only when its own library has that hash).
+  library build that was profiled and of the ICP kernels' sources (tools/srchash.py): bench.py uses a
+  row only when its own library, or failing that its ICP kernel sources, have that hash.
 """
 from __future__ import annotations
 
@@ -77,8 +78,12 @@ def main():
             doc = json.load(f)
     except (OSError, ValueError):
         doc = {}
+    from srchash import icp_sources_sha256
+
+    src = icp_sources_sha256()
     if doc.get("library_sha256") != sha:  # rows of another build are stale: start over
         doc = {"library_sha256": sha, "configs": {}}
+    doc["icp_sources_sha256"] = src  # (tools/srchash.py: the ICP kernels' sources, headers and flags)
     doc["tag"] = a.tag
     doc["note"] = ("HBM bytes per launch: FETCH_SIZE x 2 (gfx950: FETCH_SIZE reports half of a wide streaming "
                    "read) + WRITE_SIZE, KiB -> bytes, mean over the launches of the profiled run "
