@@ -411,7 +411,9 @@ def single_pair_measure(ctx, name: str, workload: str, src, tgt, params, oparams
         roof["hbm_counter"] = {"achieved": traffic / (nn_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": traffic / (nn_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
     floor_ms = update_chain_floor_ms(n)
-    update = {"bound": "latency", "kernel": "fold_update_wide_kernel" if plan.get("wide_update") else "fold_update_kernel",
+    ukernel = ("fold_update_held_kernel" if plan.get("held_update") else "fold_update_wide_kernel") if plan.get("wide_update") \
+        else "fold_update_kernel"
+    update = {"bound": "latency", "kernel": ukernel,
               "achieved": floor_ms, "peak": upd_ms, "unit": "ms",
               "frac": floor_ms / upd_ms if upd_ms > 0 else None, "chain_floor_ms": floor_ms, "avg_launch_ms": upd_ms,
               "launches_per_registration": upd_launches / max(calls, 1),

@@ -5249,24 +5249,47 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
 }
 
 // ---------------------------------------------------------------------------------------------
-// fold_update_held_kernel (round 6): fold_update_wide_kernel for sources of at most kHeldMaxN points
-// (the node's C1 scan), with the pair's correspondence records read from HBM once per update.  The
-// 896 filler threads (waves 2..15) load their records (up to kHeldMax each: record i is filler
-// i mod 896's slot i / 896) before the first barrier, every load in flight together, and keep them in
-// registers: pass A's chunk c is slot c of every filler (LDS stores only, no round trip per chunk),
-// and pass B's panel chunks take each record's nine products from the filler that holds it — the
-// wide kernel's fill of every pass-B chunk was a global round trip (2.3 us of its 7.5 on C1).
-// Waves 0 and 1 (the fold lanes, the MSE wave) hold nothing: the roles run as separate wave-uniform
-// loops, so the held records are never live beside fold_seq's 96 registers.  The chains, their
-// orders and the panel adds are fold_pass_a / fold_pass_b<PAR>'s, so the results are the wide
-// kernel's bit for bit; pass B takes that kernel's global path when a correspondence was rejected or
-// weighted (the panels then start by rank), for one panel, or for more panels than one group.
+// fold_update_held_kernel<HOLD> (round 6): fold_update_wide_kernel for sources of at most
+// HOLD x 896 points (HOLD = 3: the node's 2k C1 scan; 10: the 8k scans of C2 / C5), with the pair's
+// correspondence records read from HBM once per update.  The 896 filler threads (waves 2..15) load
+// their records (record i is filler i mod 896's slot i / 896) before the first barrier, every load in
+// flight together, and keep each as six floats in registers (s and d; d² and the weight are
+// recomputed — the search formed the record's d² as l2_simple(s, d) and its weight from that, with
+// contraction off, so the same bits): pass A's chunk c is slots 2c and 2c + 1 of every filler (LDS
+// stores only, no round trip per chunk), and pass B's panel chunks take each record's nine products
+// from the filler that holds it — the wide kernel's fill of every pass-B chunk was a global round trip
+// (C1: pass B 7.7 -> 5.2 us; 2.3 us of it had been the first fill).  Waves 0 and 1 (the fold lanes,
+// the MSE wave) hold nothing: the roles run as separate wave-uniform loops, so the held records are
+// never live beside fold_seq's 96 registers.  The chains, their orders and the panel adds are
+// fold_pass_a / fold_pass_b<PAR>'s, so the results are the wide kernel's bit for bit; pass B takes that
+// kernel's global path when a correspondence was rejected or weighted (the panels then start by rank),
+// for one panel, or for more panels than one group.
 constexpr int kHeldFill0 = 128;                       // first filler thread
 constexpr int kHeldFillers = kWideWG - kHeldFill0;    // 896
-constexpr int kHeldMax = kHeldMaxN / kHeldFillers;    // records per filler
 constexpr int kHeldCH = 2 * kHeldFillers;             // pass A chunk: two slots of every filler
 static_assert(kHeldCH <= kWideChunkP, "pass A's chunk fits the wide buffers");
+static_assert(kHeldMaxN == 10 * kHeldFillers && kHeldSmallN == 3 * kHeldFillers, "held sizes");
 
+// PCL's sequential double chain over LDS, few registers (the MSE fallback beside the held records)
+__device__ __forceinline__ double fold_seq_d_lite(const double* f, int len, double acc) {
+    int k = 0;
+    for (; k + 8 <= len; k += 8) {
+        const double2 g0 = *reinterpret_cast<const double2*>(f + k), g1 = *reinterpret_cast<const double2*>(f + k + 2);
+        const double2 g2 = *reinterpret_cast<const double2*>(f + k + 4), g3 = *reinterpret_cast<const double2*>(f + k + 6);
+        acc = acc + g0.x;
+        acc = acc + g0.y;
+        acc = acc + g1.x;
+        acc = acc + g1.y;
+        acc = acc + g2.x;
+        acc = acc + g2.y;
+        acc = acc + g3.x;
+        acc = acc + g3.y;
+    }
+    for (; k < len; ++k) acc = acc + f[k];
+    return acc;
+}
+
+template <int HOLD>
 __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, WorkArgs w) {
     __shared__ WideShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
@@ -5292,30 +5315,67 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
     const int nch = (n + kHeldCH - 1) / kHeldCH;
     const int f = tid - kHeldFill0;  // filler slot column (waves 2..15)
 
-    // the records (fillers only): loaded inside pass A's filler branch, so that they are never live
-    // in the fold wave's branch (a load ahead of the role branches kept them live there, beside
-    // fold_seq's registers)
-    float4 r0[kHeldMax], r1[kHeldMax];
+    // the records (fillers only: loaded inside pass A's filler branch, so that they are never live in
+    // the fold wave's branch — a load ahead of the role branches had kept them live there)
+    float sx[HOLD], sy[HOLD], sz[HOLD], dx[HOLD], dy[HOLD], dz[HOLD];
+    // pass B's layout (fold_pass_b<PAR>: S panels of kc, rows of T steps strided stride) and each held
+    // record's place in it, packed: offset << 4 | chunk + 1 (0: none)
+    constexpr int CAP = 9 * kWideRow;
+    auto layout = [&](int cnt_, int& kc, int& S, int& stride, int& T, int& nchb) __attribute__((always_inline)) {
+        kc = sigma_kc(cnt_, kp.sigma_max_kc);
+        S = (cnt_ > 0 && kc > 0) ? (cnt_ + kc - 1) / kc : 1;
+        stride = (((CAP / max(9 * S, 18)) - 4) & ~7) + 4;
+        T = stride - 4;
+        nchb = (kc + T - 1) / T;  // the first panel is the longest
+    };
+    int pk[HOLD];
+    auto held_offsets = [&](int cnt_) __attribute__((always_inline)) {
+        int kc, S, stride, T, nchb;
+        layout(cnt_, kc, S, stride, T, nchb);
+        // (the quotients by float reciprocals, corrected: exact for these small operands)
+        const float invkc = 1.0f / (float)kc, invT = 1.0f / (float)T;
+#pragma unroll
+        for (int k = 0; k < HOLD; ++k) {
+            const int i = f + k * kHeldFillers;
+            int q = (int)((float)i * invkc);
+            int t = i - q * kc;
+            if (t >= kc) { ++q; t -= kc; }
+            if (t < 0) { --q; t += kc; }
+            int c = (int)((float)t * invT);
+            int u = t - c * T;
+            if (u >= T) { ++c; u -= T; }
+            if (u < 0) { --c; u += T; }
+            pk[k] = i < n ? ((q * 9 * stride + u) << 4) | (c + 1) : 0;
+        }
+    };
     clear_need(w, p, n, tid, kWideWG);
     if (ticks) w.ticks[0] = __builtin_amdgcn_s_memrealtime();
 
-    // ---- pass A (fold_pass_a's chains over chunks of kHeldFillers points)
+    // ---- pass A (fold_pass_a's chains over chunks of kHeldCH points)
     int cnt = 0;
-    auto store_a = [&](int c) __attribute__((always_inline)) {  // slots 2c, 2c + 1 of this filler -> chunk c
+    // slots 2c, 2c + 1 of this filler -> chunk c (first staging, key mode: and corr_kernel's record pair
+    // {s.xyz, w}, {d.xyz, d²} for pass B's global path — per chunk, so that chunk 0 waits for its own
+    // slots' gathers only)
+    auto store_a = [&](int c, bool first) __attribute__((always_inline)) {
         float(*b)[kWideRow] = sh.buf[c & 1];
 #pragma unroll
-        for (int k = 0; k < kHeldMax; ++k) {
+        for (int k = 0; k < HOLD; ++k) {
             if ((k >> 1) != c) continue;
             const int i = k * kHeldFillers + f;
             if (i >= n) continue;
             const int o = i - c * kHeldCH;
-            const float d2 = r1[k].w;
-            const float sv[6] = {r0[k].x, r0[k].y, r0[k].z, r1[k].x, r1[k].y, r1[k].z};
+            const float d2 = l2_simple(sx[k], sy[k], sz[k], dx[k], dy[k], dz[k]);
+            const float sv[6] = {sx[k], sy[k], sz[k], dx[k], dy[k], dz[k]};
+            if (keys && first) {
+                const float w0 = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
+                w.corr[(int64_t)p * xs * 2 + 2 * i] = make_float4(sx[k], sy[k], sz[k], w0);
+                w.corr[(int64_t)p * xs * 2 + 2 * i + 1] = make_float4(dx[k], dy[k], dz[k], d2);
+            }
             float v[6], wt = 0.0f, dd = 0.0f;
 #pragma unroll
             for (int q = 0; q < 6; ++q) v[q] = ident;
             if (!(d2 > kp.max_d2)) {
-                wt = r0[k].w;
+                wt = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) v[q] = weighted ? wt * sv[q] : sv[q];
                 dd = d2;
@@ -5333,11 +5393,11 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         fold_prio(true);
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (ticks && c < 4) w.ticks[20 + c] = __builtin_amdgcn_s_memrealtime();
+            if (ticks && c < 6) w.ticks[20 + c] = __builtin_amdgcn_s_memrealtime();
             if (lane < 7) acc = fold_seq<float>(sh.buf[c & 1][lane], min(kHeldCH, n - c * kHeldCH), acc);
         }
         fold_prio(false);
-        if (ticks) w.ticks[24] = __builtin_amdgcn_s_memrealtime();
+        if (ticks) w.ticks[26] = __builtin_amdgcn_s_memrealtime();
     } else if (wv == 1) {
         if (mse) {  // the MSE sum's exact form (fold_pass_a), the whole wave per chunk
             uint64_t xsum = 0;
@@ -5354,51 +5414,60 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
             for (int c = 0; c < nch; ++c) __syncthreads();
         }
     } else {
-        // the held records, every load in flight together
-        if (keys) {
-            uint32_t ti[kHeldMax];
+        // the held records, every load in flight together (16-B loads: with the two modes' loads
+        // merged, a pointer that lost its alignment was split into four dword loads — 2.4 us more)
+        // (chunk 0's two slots first, staged, then the other slots' loads, which land during chunk 0's
+        // fold: issued all together, every wave's later slots queued ahead of the other waves' first
+        // ones and chunk 0 waited for nearly all of them — the fold started 3.6 us in at 8k)
+        auto load = [&](int k0, int k1) __attribute__((always_inline)) {
+            if (keys) {
+                uint32_t ti[HOLD];
 #pragma unroll
-            for (int k = 0; k < kHeldMax; ++k) {
-                const int i = min(f + k * kHeldFillers, n - 1);
-                r0[k] = Xp[i];
-                ti[k] = (uint32_t)key_idx(K[i]);
-            }
+                for (int k = 0; k < HOLD; ++k) {
+                    if (k < k0 || k >= k1) continue;
+                    const int i = min(f + k * kHeldFillers, n - 1);
+                    const float4 x = Xp[i];
+                    sx[k] = x.x;
+                    sy[k] = x.y;
+                    sz[k] = x.z;
+                    ti[k] = (uint32_t)key_idx(K[i]);
+                }
 #pragma unroll
-            for (int k = 0; k < kHeldMax; ++k) r1[k] = TG[ti[k]];
-        } else {
-            // (one 16-B load per float4: with the two modes' loads merged, the second one's pointer
-            // lost its alignment and was split into four dword loads — 2.4 us more for the chunk)
+                for (int k = 0; k < HOLD; ++k) {
+                    if (k < k0 || k >= k1) continue;
+                    const float4 t = TG[ti[k]];
+                    dx[k] = t.x;
+                    dy[k] = t.y;
+                    dz[k] = t.z;
+                }
+            } else {
 #pragma unroll
-            for (int k = 0; k < kHeldMax; ++k) {
-                const int i = min(f + k * kHeldFillers, n - 1);
-                const float4* q0 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i : Xp + i, 16));
-                const float4* q1 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i + 1 : NT + i, 16));
-                r0[k] = *q0;
-                r1[k] = *q1;
+                for (int k = 0; k < HOLD; ++k) {
+                    if (k < k0 || k >= k1) continue;
+                    const int i = min(f + k * kHeldFillers, n - 1);
+                    const float4* q0 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i : Xp + i, 16));
+                    const float4* q1 = static_cast<const float4*>(__builtin_assume_aligned(C ? C + 2 * i + 1 : NT + i, 16));
+                    const float4 r0 = *q0, r1 = *q1;
+                    sx[k] = r0.x;
+                    sy[k] = r0.y;
+                    sz[k] = r0.z;
+                    dx[k] = r1.x;
+                    dy[k] = r1.y;
+                    dz[k] = r1.z;
+                }
             }
-        }
-        // d² and the weight of the cached-neighbour form (X, NT) and of key mode, once per record
-#pragma unroll
-        for (int k = 0; k < kHeldMax; ++k) {
-            if (!C || keys) {
-                const float d2 = l2_simple(r0[k].x, r0[k].y, r0[k].z, r1[k].x, r1[k].y, r1[k].z);
-                r0[k].w = weighted ? (float)huber_w(d2, kp.huber_delta) : 1.0f;
-                r1[k].w = d2;
-            }
-            const int i = f + k * kHeldFillers;
-            if (keys && i < n) {
-                w.corr[(int64_t)p * xs * 2 + 2 * i] = r0[k];
-                w.corr[(int64_t)p * xs * 2 + 2 * i + 1] = r1[k];
-            }
-        }
-        store_a(0);
-        if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[25] = __builtin_amdgcn_s_memrealtime();
-        if (w.ticks != nullptr && p == 0 && lane == 0)
-            atomicMax(reinterpret_cast<unsigned long long*>(w.ticks) + 27, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        };
+        load(0, 2);
+        store_a(0, true);
         for (int c = 0; c < nch; ++c) {
             __syncthreads();
-            if (c + 1 < nch) store_a(c + 1);
+            if (c == 0) load(2, HOLD);  // (after the barrier: the fold of chunk 0 starts meanwhile)
+            if (c + 1 < nch) store_a(c + 1, true);
         }
+        // pass B's chunk offsets for the plain case (every correspondence kept: kc = sigma_kc(n)),
+        // while the fold wave finishes (14 filler waves on 4 SIMDs: ~1.3 us of VALU at 8k if left to
+        // pass B's critical path)
+        held_offsets(n);
     }
     // |C|: exact integer reduction of the fillers' counts
 #pragma unroll
@@ -5416,7 +5485,6 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
     }
     __syncthreads();
-    if (ticks) w.ticks[26] = __builtin_amdgcn_s_memrealtime();
     if (mse && sh.s.mse_sum < 0.0) {  // (uniform) PCL's sequential double chain over the chunks again
         dacc = 0.0;
         if (wv == 0) {
@@ -5425,13 +5493,14 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
             for (int c = 0; c < nch; ++c) {
                 __syncthreads();
                 if (lane == 0)
-                    dacc = fold_seq_d(reinterpret_cast<const double*>(sh.buf[c & 1][7]), min(kHeldCH, n - c * kHeldCH), dacc);
+                    dacc = fold_seq_d_lite(reinterpret_cast<const double*>(sh.buf[c & 1][7]), min(kHeldCH, n - c * kHeldCH),
+                                           dacc);
             }
         } else {
-            store_a(0);
+            store_a(0, false);
             for (int c = 0; c < nch; ++c) {
                 __syncthreads();
-                if (c + 1 < nch) store_a(c + 1);
+                if (c + 1 < nch) store_a(c + 1, false);
             }
         }
         __syncthreads();
@@ -5443,10 +5512,10 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
     // ---- pass B
     SolveShared& s = sh.s;
     const int cntC = (int)s.mom[0];
-    const int kc = sigma_kc(cntC, kp.sigma_max_kc);
-    const int S = (cntC > 0 && kc > 0) ? (cntC + kc - 1) / kc : 1;
-    if (ticks) w.ticks[5] = __builtin_amdgcn_s_memrealtime();
-    if (weighted || cntC < n || S <= 1 || S > kSliceGroup) {
+    int kc, S, stride, T, nchb;
+    layout(cntC, kc, S, stride, T, nchb);
+    const int G = S, R = 9 * G, FW = (R + 63) / 64;
+    if (weighted || cntC < n || S <= 1 || S > kSliceGroup || nchb > 14) {
         const FoldIn fin{C, Xp, NT, n};
         fold_pass_b<kWideWG, kWideChunkP, kWideRow, true>(kp, fin, sh.buf, s);
     } else {
@@ -5455,12 +5524,7 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         const float ms[3] = {s.mean[0], s.mean[1], s.mean[2]};
         const float md[3] = {s.mean[3], s.mean[4], s.mean[5]};
         const float oon = s.one_over_n;
-        constexpr int CAP = 9 * kWideRow;
         auto bufs = [&](int k) -> float* { return &sh.buf[k & 1][0][0]; };
-        const int G = S, R = 9 * G, FW = (R + 63) / 64;
-        const int stride = (((CAP / R) - 4) & ~7) + 4;
-        const int T = stride - 4;
-        const int nchb = (kc + T - 1) / T;  // the first panel is the longest
         float sig = 0.0f, pacc = 0.0f;
         if (wv < 2) {
             const int L = tid;
@@ -5474,39 +5538,26 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
             }
             if (ticks) w.ticks[30] = __builtin_amdgcn_s_memrealtime();
         } else {
-            // each held record's panel and step (the panel by a float reciprocal, corrected)
-            int P[kHeldMax], stp[kHeldMax];
-            const float invkc = 1.0f / (float)kc;
-#pragma unroll
-            for (int k = 0; k < kHeldMax; ++k) {
-                const int i = f + k * kHeldFillers;
-                int q = (int)((float)i * invkc);
-                int t = i - q * kc;
-                if (t >= kc) { ++q; t -= kc; }
-                if (t < 0) { --q; t += kc; }
-                P[k] = i < n ? q : -1;
-                stp[k] = t;
-            }
+            // each held record's LDS offset in its chunk's buffer and the chunk (-1: none), by a
+            // float reciprocal of kc, corrected
+            // (pk: from pass A — cntC == n here, the layout it assumed)
             auto fill = [&](int c) __attribute__((always_inline)) {
                 float* b = bufs(c);
 #pragma unroll
-                for (int k = 0; k < kHeldMax; ++k) {
-                    const int t = stp[k] - c * T;
-                    if (P[k] < 0 || t < 0 || t >= T) continue;
-                    const float sv[3] = {r0[k].x - ms[0], r0[k].y - ms[1], r0[k].z - ms[2]};
-                    const float dv[3] = {r1[k].x - md[0], r1[k].y - md[1], r1[k].z - md[2]};
-                    float* o = b + P[k] * 9 * stride + t;
+                for (int k = 0; k < HOLD; ++k) {
+                    if ((pk[k] & 15) != c + 1) continue;
+                    const int off = pk[k] >> 4;
+                    const float sv[3] = {sx[k] - ms[0], sy[k] - ms[1], sz[k] - ms[2]};
+                    const float dv[3] = {dx[k] - md[0], dy[k] - md[1], dz[k] - md[2]};
+                    float* o = b + off;
 #pragma unroll
                     for (int ra = 0; ra < 3; ++ra)
 #pragma unroll
                         for (int rb = 0; rb < 3; ++rb) o[(ra * 3 + rb) * stride] = dv[ra] * sv[rb];
                 }
             };
-            if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[6] = __builtin_amdgcn_s_memrealtime();
             fill(0);
-            if (w.ticks != nullptr && p == 0 && tid == kHeldFill0) w.ticks[7] = __builtin_amdgcn_s_memrealtime();
-            if (w.ticks != nullptr && p == 0 && lane == 0)
-                atomicMax(reinterpret_cast<unsigned long long*>(w.ticks) + 8, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+            if (w.ticks != nullptr && p == 0 && lane == 0) w.ticks[32 + wave - 2] = __builtin_amdgcn_s_memrealtime();
             for (int c = 0; c < nchb; ++c) {
                 __syncthreads();
                 if (c + 1 < nchb) fill(c + 1);
@@ -6308,8 +6359,10 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
     if (a.kp.numerics == kNumericsPCL) {
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
-        if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldMaxN)
-            hipLaunchKernelGGL(fold_update_held_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+        if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldSmallN)
+            hipLaunchKernelGGL(fold_update_held_kernel<3>, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+        else if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldMaxN)
+            hipLaunchKernelGGL(fold_update_held_kernel<10>, dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (wide && !tail_test && order_ncu <= 0)
             hipLaunchKernelGGL(fold_update_wide_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (w.res_update && !need_corr && !w.corr && max_n <= kResMaxN && w.nn_t && w.nn_u && w.defer_xform &&

@@ -269,7 +269,7 @@ typedef struct icp4r_plan_info {
                            off with plan option res_update = 0                        */
     int32_t held_update; /* 1 (ABI 6): the wide update keeps each correspondence record in a
                            register from pass A to pass B (fold_update_held_kernel: sources
-                           <= 2688); off with plan option held_update = 0             */
+                           <= 8960); off with plan option held_update = 0             */
 } icp4r_plan_info;
 /* ctx: whose plan options and CU count apply (NULL: the defaults and 256 CUs); numerics:
  * ICP4R_NUMERICS_PCL / _F64, as icp4r_params.numerics. */

@@ -142,8 +142,8 @@ def test_plan_geometry():
         assert plan(1, 8192, 8192)["wide_update"] and plan(200, 8192, 8192)["wide_update"]
         assert not plan(1, 8192, 8192, numerics=icp4r.NUMERICS_F64)["wide_update"]
         assert not plan(1024, 8192, 8192)["wide_update"]
-        # ... with the records held in registers for sources of at most 2688 points
-        assert plan(1, 2688, 8192)["held_update"] and not plan(1, 2689, 8192)["held_update"]
+        # ... with the records held in registers for sources of at most 8960 points
+        assert plan(1, 8960, 8192)["held_update"] and not plan(1, 8961, 8192)["held_update"]
         assert not plan(1024, 2048, 2048)["held_update"]
         ctx.set_plan_option("held_update", 0)
         assert not plan(1, 2048, 2048)["held_update"] and plan(1, 2048, 2048)["wide_update"]

@@ -1,10 +1,10 @@
 """fold_update_held_kernel (round 6): the wide update with the correspondence records held in the
-fillers' registers from pass A to pass B (sources of at most 2688 points: the node's C1 scan) —
-needs a real MI355X.
+fillers' registers from pass A to pass B (sources of at most 8960 points: 3 records per filler up to
+2688 — the node's C1 scan — and 10 for the 8k scans of C2 / C5) — needs a real MI355X.
 
 Every registration must be bit-identical to fold_update_wide_kernel (plan option held_update = 0)
 and to the oracle: sources across the 896-point slot boundaries (a handful of points, one slot, a
-partial second slot, C1's 2048, the 2688 maximum and one past it), PCL's early stops live (the MSE
+partial second slot, C1's 2048, both forms' maxima and one past each), PCL's early stops live (the MSE
 sum's exact form and its sequential fallback), and the forms whose pass B takes the wide kernel's
 global path (a distance threshold: panels by rank; Huber weights) or whose records come from the
 merged keys (the multi-tile target, plan option fold_keys).
@@ -42,8 +42,13 @@ def _both(gpu_ctx, plan, src, tgt, p):
     (1000, 1200, {}),                                     # a partial second slot
     (2048, 2048, {}),                                     # C1: PCL defaults, 4 panels
     (2048, 2048, {"max_iterations": 20, "mse_threshold_absolute": -1.0, "transformation_epsilon": -1.0}),
-    (2688, 3000, {"max_iterations": 15}),                 # the largest held source
-    (2689, 3000, {"max_iterations": 8}),                  # one past it: the wide kernel
+    (2688, 3000, {"max_iterations": 15}),                 # the largest 3-record source
+    (2689, 3000, {"max_iterations": 8}),                  # one past it: the 10-record form
+    (8192, 8192, {"max_iterations": 20}),                 # C2: 13 panels
+    (8192, 8192, {}),                                     # PCL defaults (MSE live) at 8k
+    (8960, 9000, {"max_iterations": 6}),                  # the largest held source: 15 panels, pass B's global path
+    (8961, 9000, {"max_iterations": 6}),                  # one past it: the wide kernel
+    (6000, 7000, {"eigen_l1_bytes": 49152, "eigen_gebp_mr": 16}),  # other panel widths
     (2048, 2048, {"max_correspondence_distance": 0.6}),   # rejections: pass B's global ranked path
     (2400, 2048, {"huber_delta": 0.4}),                   # Huber: the same
 ])
@@ -52,7 +57,7 @@ def test_held_update_identical(gpu_ctx, oracle_mod, plan, n, m, kw):
 
     plan(solo=0)
     pl = icp4r.plan(1, n, m, ctx=gpu_ctx)
-    assert pl["wide_update"] and pl["held_update"] == (n <= 2688)
+    assert pl["wide_update"] and pl["held_update"] == (n <= 8960)
     src, tgt = _pair(4100 + n % 89, n, m)
     p = icp4r.default_params(**kw)
     b = _both(gpu_ctx, plan, src, tgt, p)
@@ -95,11 +100,11 @@ def test_held_update_fold_keys(gpu_ctx, oracle_mod, plan, huber):
 
 
 def test_held_update_small_batch(gpu_ctx, oracle_mod, plan):
-    """A ragged batch of fewer pairs than CUs (one held workgroup per pair, a large source beside
-    them: the whole launch takes the wide kernel then)."""
+    """A ragged batch of fewer pairs than CUs (one held workgroup per pair, an 8k source beside
+    them: the launch takes the form its largest source needs)."""
     import icp4r
 
-    shapes = [(2048, 2048), (37, 500), (1793, 1800), (2688, 2000), (900, 4000)]
+    shapes = [(2048, 2048), (37, 500), (1793, 1800), (2688, 2000), (900, 4000), (8192, 6000)]
     pairs = [_pair(4500 + k, n, m) for k, (n, m) in enumerate(shapes)]
     src = np.concatenate([s for s, _ in pairs]).astype(np.float32)
     tgt = np.concatenate([t for _, t in pairs]).astype(np.float32)

@@ -25,7 +25,7 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "icp-4dradar_amd", "icp4r", "_lib", "libicp4r.so")
 OUT = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-KERNELS = ("nn_lds_kernel,nn_tile_kernel,fold_update_kernel,fold_update_wide_kernel,index_kernel,src_order_kernel,index_refine_kernel,"
+KERNELS = ("nn_lds_kernel,nn_tile_kernel,fold_update_kernel,fold_update_wide_kernel,fold_update_held_kernel,fold_update_res_kernel,index_kernel,src_order_kernel,index_refine_kernel,"
            "nn_seed_kernel,nn_cache_test_kernel,nn_order_kernel,init_kernel,fitness_prep_kernel,finish_kernel,"
            "solo_kernel,corr_kernel")
 
