@@ -2823,6 +2823,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     __shared__ TileShared sh;
     const bool own = first >= 0;  // (single tile: launched with gridDim.x == 1)
     const int tile = blockIdx.x, part = blockIdx.y, p = blockIdx.z;
+    const unsigned long long tk_entry = w.pass_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
@@ -2840,6 +2841,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     const bool tk0 = tk && tile == 0 && part == 0 && p == 0;
     const unsigned long long tk_in = tk ? __builtin_amdgcn_s_memrealtime() : 0;
     if (tk0) tk[0] = tk_in;
+    if (tk0) tk[7] = tk_entry;
     if (tk) atomicMax(tk + 6, ~tk_in);
 
     // Stage the tile (whole superblocks: tsort is padded to them), every load before the first store,
@@ -5293,6 +5295,7 @@ template <int HOLD>
 __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, WorkArgs w) {
     __shared__ WideShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
+    if (w.ticks != nullptr && p == 0 && threadIdx.x == 0) w.ticks[9] = __builtin_amdgcn_s_memrealtime();
     PairState& st = w.state[p];
     if (st.phase != kPhaseActive) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -86,6 +86,35 @@ def test_oracle_vs_numpy_twin(oracle_mod):
             assert min(abs(dh[i] - 60), abs(dh[i] - 300)) < EDGE_TOL_DEG, i
 
 
+def test_submap_order_does_not_change_registrations(oracle_mod):
+    """ikd-Tree's Search_by_sector returns the kept set in its tree's pre-order
+    (ikd_Tree.cpp:1114-1138); the restatement returns insertion order.  The set is the same, and the
+    registrations are invariant to the target's order: the correspondences are formed and summed in
+    SOURCE index order (icp.hpp / fast_gicp), each source's nearest target is the same point whatever
+    the order unless two DISTINCT points tie exactly in distance (the (d², index) key then picks by
+    position; identical duplicates — accumulated scans — give the same coordinates either way), and
+    GICP's target covariances are k-NN sets of the same kind.  So any permutation of the submap — the
+    pre-order being one — gives bit-identical ICP and GICP results; checked here on the radar_odometry
+    scene (submap of the synthetic map around the pose, several seeded permutations)."""
+    from icp4r import synth
+
+    mp = synth.make_map_pair(2)
+    map_pts, scan = mp.tgt_xyzi(), mp.src_xyzi()
+    kept = oracle_mod.sector_search(map_pts, [0.0, 0.0, 0.0], 80.0, 0.0)
+    sub = map_pts[kept]
+    assert len(sub) > 1000
+    ref = oracle_mod.align(scan, sub, numerics=oracle_mod.NUM_F32, max_iterations=15)
+    gref = oracle_mod.gicp_align(scan[:1500], sub, k=10)
+    rng = np.random.default_rng(17)
+    for rep in range(3):
+        perm = rng.permutation(len(sub))
+        o = oracle_mod.align(scan, sub[perm], numerics=oracle_mod.NUM_F32, max_iterations=15)
+        assert (o["T"] == ref["T"]).all() and o["fitness"] == ref["fitness"], rep
+        assert o["iterations"] == ref["iterations"] and o["n_correspondences"] == ref["n_correspondences"], rep
+        g = oracle_mod.gicp_align(scan[:1500], sub[perm], k=10)
+        assert (g["T"] == gref["T"]).all() and g["iterations"] == gref["iterations"], rep
+
+
 # ------------------------------------------------------------------------------------------- device
 def _edge_ok(oracle_mod, pts, c, heading, idx):
     h = oracle_mod.calc_heading(pts[idx], np.asarray(c, np.float32))

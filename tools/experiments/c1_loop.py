@@ -1,0 +1,18 @@
+"""Registrations of one single pair back to back (for a kernel trace): python3 c1_loop.py [n] [reps]."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "icp-4dradar_amd"))
+import icp4r  # noqa: E402
+from icp4r import synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+ctx = icp4r.Context(0, plan=icp4r.env_plan())
+pr = synth.make_pair(0, n)
+p = icp4r.default_params() if n == 2048 else icp4r.default_params(
+    max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
+for _ in range(reps):
+    ctx.align(pr.src_xyzi(), pr.tgt_xyzi(), p)
+print("done", flush=True)

@@ -32,6 +32,6 @@ for held in (1, 0):
         buf = (C.c_uint64 * 48)()
         lib.icp4r__debug_ticks(ctx._h, buf, 48)
         t = [int(v) for v in buf]
-        keys = [1, 2, 3] + (list(range(20, 27)) + [6, 28, 29, 30] + list(range(32, 46)) if held else [])
-        rel = {k: round((t[k] - t[0]) * 0.01, 2) for k in keys if t[k] > t[0]}
+        keys = [1, 2, 3] + ([9] if held else []) + (list(range(20, 27)) + [6, 28, 29, 30] + list(range(32, 46)) if held else [])
+        rel = {k: round((t[k] - t[0]) * 0.01, 2) for k in keys if t[k] > t[0] or k == 9}
         print(json.dumps({"n": n, "held": held, "rep": rep, "rel_us": rel}), flush=True)

@@ -50,8 +50,9 @@ def main():
                          "seed": ((s[2] - s[0]) if seed_first else (s[2] - s[1])) * 0.01,
                          "traverse": (s[3] - max(s[1], s[2])) * 0.01, "write": (s[4] - s[3]) * 0.01,
                          "wg0": (s[4] - s[0]) * 0.01, "launch_span": (s[5] - first) * 0.01 if first else None,
-                         "wg0_start_lag": (s[0] - first) * 0.01 if first else None})
-        keys = ["stage", "seed", "traverse", "write", "wg0", "launch_span", "wg0_start_lag"]
+                         "wg0_start_lag": (s[0] - first) * 0.01 if first else None,
+                         "entry_to_start": (s[0] - s[7]) * 0.01 if s[7] else None})
+        keys = ["stage", "seed", "traverse", "write", "wg0", "launch_span", "wg0_start_lag", "entry_to_start"]
         mean = {kk: round(sum(r[kk] for r in rows[1:]) / max(1, len(rows) - 1), 2) for kk in keys}
         print(json.dumps({"n": n, "rep": rep, "pass0": rows[0] if rows else None, "later_mean": mean}), flush=True)
         ctx.close()
