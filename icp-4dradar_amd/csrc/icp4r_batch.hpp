@@ -38,7 +38,7 @@ enum PlanOpt : int {
     kOptPhaseTicks, kOptKd, kOptMortonMwg, kOptPart, kOptSrcOrder, kOptFuseSeed, kOptTileOwn, kOptTileDefer,
     kOptGroups, kOptSearchCuDiv, kOptFuseTest, kOptFuseOrder, kOptSumsTail, kOptWideUpdate, kOptGatherPadded,
     kOptGicpCovBrute, kOptFoldKeys, kOptGicpSpec, kOptGicpGrid, kOptGicpKnnLanes, kOptResUpdate, kOptHeldUpdate,
-    kNumPlanOpts
+    kOptFitXform, kNumPlanOpts
 };
 static_assert(kNumPlanOpts <= 32, "icp4r_ctx::plan_set is a 32-bit mask");
 extern const char* const kPlanOptNames[kNumPlanOpts];

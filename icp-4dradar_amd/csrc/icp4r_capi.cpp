@@ -105,7 +105,7 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
     "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update",
-    "held_update"};
+    "held_update", "fit_xform"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
     return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
@@ -620,9 +620,16 @@ int run_pairs(icp4r_ctx* ctx, const PairArgs& a, int npairs, int max_n, int max_
     }
     icp4r_host::Range fit_range("icp4r fitness pass");
     for (int g = 0; g < groups; ++g) {
-        // the fitness pass' cached-neighbour test runs inside fitness_prep_kernel when fused
+        // the fitness pass' cached-neighbour test runs inside fitness_prep_kernel when fused; on the
+        // one-tile plan (no cache, no seeds) the search forms X := final * input itself, one launch and
+        // one boundary fewer (plan option fit_xform = 0: fitness_prep_kernel)
         const int ftest = fuse && a.kp.compute_fitness ? 1 : 0;
-        if (a.kp.compute_fitness || a.aligned) HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g], ftest));
+        wg[g].fit_xform = (a.kp.compute_fitness && pl.tile && !pl.lds && pl.max_m <= kLdsMaxTargets && wg[g].tile_own &&
+                           !wg[g].nn_u && !wg[g].seed_next && opt(ctx, kOptFitXform, 1) != 0)
+                              ? 1
+                              : 0;
+        if ((a.kp.compute_fitness || a.aligned) && !wg[g].fit_xform)
+            HIP_TRY(launch_fitness_prep(ag[g], wg[g], gn[g], gs[g], ftest));
         if (a.kp.compute_fitness && (rc = nn_pass(ctx, pl, ag[g], wg[g], gn[g], mn, 1, 0, gs[g], search_cu, ftest, iters)))
             return rc;
         HIP_TRY(launch_finish(ag[g], wg[g], gn[g], gs[g]));
@@ -1109,7 +1116,7 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
             0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid,
-            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate};
+            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate, 1};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

@@ -161,6 +161,8 @@ struct WorkArgs {
                           // chip across the update (plan option res_update = 0: fold_update_kernel)
     int32_t held_update;  // 1 (wide update, sources <= kHeldMaxN): fold_update_held_kernel, the records held
                           // in the fillers' registers from pass A to pass B (plan option held_update)
+    int32_t fit_xform;    // 1 (one-tile plan, no cache, no seeds): the fitness pass' nn_tile_kernel forms
+                          // X := final * input itself (fitness_prep_kernel's work; plan option fit_xform)
     float4* nn_t;       // [npairs * x_stride] the NN target of X_i: xyz, .w = its sorted target position |
                         // the query's sorted position << 14 (nt_pack)
     float4* sq;         // [npairs * x_stride] the pass's miss list in the order the test found them: a

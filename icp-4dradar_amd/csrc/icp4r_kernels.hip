@@ -2879,11 +2879,21 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     NNKey* key = w.nn_key + xs0;
     float x = 0.f, y = 0.f, z = 0.f;
     NNKey init = 0;
-    float4 v = w.X[xs0 + o];
+    // the fitness pass with w.fit_xform (own plans): the query is final * input_i, formed here as
+    // fitness_prep_kernel did (Registration::getFitnessScore's transformPointCloud) and written to X
+    const bool fitx = own && fitness_pass && w.fit_xform;
+    float4 v = fitx ? a.src[uload(a.src_off + p) + o] : w.X[xs0 + o];
     NNKey k0 = key[o];
     uint32_t j = 0;
     float4 t;
     {
+        if (fitx) {
+            float T[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].final_T[q]);
+            xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
+            if (live) w.X[xs0 + o] = v;
+        }
         if (own && first == 0 && !fitness_pass && w.defer_xform) {
             // the previous update's transformCloud(T_inc), deferred to here (one read and write of X
             // per pass instead of a pass over the cloud by the update's one workgroup); every query

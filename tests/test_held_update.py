@@ -122,3 +122,25 @@ def test_held_update_small_batch(gpu_ctx, oracle_mod, plan):
         o = oracle_mod.align(s, t, numerics=oracle_mod.NUM_F32, max_iterations=12)
         assert (np.array(out[1][k]["T"], np.float32).reshape(4, 4).T == o["T"]).all(), k
         assert out[1][k]["iterations"] == o["iterations"], k
+
+
+@pytest.mark.parametrize("n,m,kw", [(2048, 2048, {}), (8192, 8192, {"max_iterations": 20}),
+                                    (3000, 5000, {"huber_delta": 0.5})])
+def test_fitness_transform_in_search_identical(gpu_ctx, oracle_mod, plan, n, m, kw):
+    """Round 6: on the one-tile plan the fitness pass' search forms X := final * input itself (plan
+    option fit_xform, the default) instead of fitness_prep_kernel: fitness, the aligned cloud and the
+    result bit-identical to fit_xform = 0 and to the oracle."""
+    import icp4r
+
+    src, tgt = _pair(4700 + n % 83, n, m)
+    p = icp4r.default_params(**kw)
+    out = {}
+    for fx in (0, 1):
+        plan(fit_xform=fx, solo=0)
+        r, al = gpu_ctx.align(src, tgt, p, want_aligned=True)
+        out[fx] = (r.matrix().copy(), r.fitness, r.iterations, al.view(np.uint32).copy())
+    assert (out[0][0] == out[1][0]).all() and out[0][1:3] == out[1][1:3]
+    assert (out[0][3] == out[1][3]).all()
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True, **kw)
+    assert out[1][1] == o["fitness"] and (out[1][0] == o["T"]).all()
+    assert (out[1][3] == o["aligned"].view(np.uint32)).all()
