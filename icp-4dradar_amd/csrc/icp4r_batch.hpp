@@ -38,9 +38,9 @@ enum PlanOpt : int {
     kOptPhaseTicks, kOptKd, kOptMortonMwg, kOptPart, kOptSrcOrder, kOptFuseSeed, kOptTileOwn, kOptTileDefer,
     kOptGroups, kOptSearchCuDiv, kOptFuseTest, kOptFuseOrder, kOptSumsTail, kOptWideUpdate, kOptGatherPadded,
     kOptGicpCovBrute, kOptFoldKeys, kOptGicpSpec, kOptGicpGrid, kOptGicpKnnLanes, kOptResUpdate, kOptHeldUpdate,
-    kOptFitXform, kNumPlanOpts
+    kOptFitXform, kOptCounters, kNumPlanOpts
 };
-static_assert(kNumPlanOpts <= 32, "icp4r_ctx::plan_set is a 32-bit mask");
+static_assert(kNumPlanOpts <= 64, "icp4r_ctx::plan_set is a 64-bit mask");
 extern const char* const kPlanOptNames[kNumPlanOpts];
 // The context's value of option k, or dflt when it was never set (ctx may be NULL: dflt).
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt);

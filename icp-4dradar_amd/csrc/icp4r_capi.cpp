@@ -105,10 +105,10 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
     "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update",
-    "held_update", "fit_xform"};
+    "held_update", "fit_xform", "counters"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
-    return (ctx && (ctx->plan_set >> k & 1u)) ? ctx->plan_val[k] : dflt;
+    return (ctx && (ctx->plan_set >> k & 1ull)) ? ctx->plan_val[k] : dflt;
 }
 
 // Geometry of the NN pass.
@@ -281,7 +281,10 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
         HIP_TRY(ctx->evals.ensure(kCountBytes));
         HIP_TRY(hipMemsetAsync(ctx->evals.p, 0, kCountBytes, st));
     }
-    w.evals = static_cast<unsigned long long*>(ctx->evals.p);
+    // the NN work counters: diagnostics, off unless asked for (plan option counters = 1, or per-kernel
+    // timing on): their per-wave atomics at every search launch's end cost C1 2 %, C2 1.4 % (round 6)
+    w.evals = (opt(ctx, kOptCounters, 0) != 0 || ctx->kernel_timing) ? static_cast<unsigned long long*>(ctx->evals.p)
+                                                                      : nullptr;
     if (opt(ctx, kOptPhaseTicks, 0)) {
         // (see the kernels' debug tick slots; then kPassTickSlots per NN pass)
         const size_t nt = (size_t)pass_tick_base(npairs) + (size_t)kMaxTickPasses * kPassTickSlots;
@@ -1101,7 +1104,7 @@ int icp4r_set_plan_option(icp4r_ctx* ctx, const char* name, int32_t value) {
     if (k == kOptXpad && (value < 0 || value > 1 << 20)) return fail(ICP4R_E_INVALID, "plan option xpad = %d", value);
     if (k == kOptSearchCuDiv && value < 0) return fail(ICP4R_E_INVALID, "plan option search_cu_div = %d", value);
     ctx->plan_val[k] = value;
-    ctx->plan_set |= 1u << k;
+    ctx->plan_set |= 1ull << k;
     return ICP4R_OK;
 }
 
@@ -1109,14 +1112,14 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
     if (!ctx || !value) return fail(ICP4R_E_INVALID, "NULL argument");
     const int k = plan_opt_index(name);
     if (k < 0) return fail(ICP4R_E_INVALID, "unknown plan option '%s'", name ? name : "(null)");
-    const bool set = (ctx->plan_set >> k) & 1u;
+    const bool set = (ctx->plan_set >> k) & 1ull;
     *value = set ? ctx->plan_val[k] : INT32_MIN;
     if (!set) {  // the default in effect (what the plan code falls back to)
         static const int32_t dflt[kNumPlanOpts] = {
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
             0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid,
-            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate, 1};
+            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate, 1, 0};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

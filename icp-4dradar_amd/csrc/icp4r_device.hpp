@@ -44,7 +44,7 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
 
 // Work counters: add v to counter k of this wave's slot.  Call from one lane.
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int k, unsigned long long v) {
-    if (v == 0) return;
+    if (v == 0 || ctr == nullptr) return;  // (null: counting off — WorkArgs::evals)
     const uint32_t blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     const uint32_t slot = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kCountSlots;
     atomicAdd(ctr + (size_t)slot * kCountStride + k, v);

@@ -100,8 +100,8 @@ struct icp4r_ctx {
     int ncu = 256;  // compute units of the device (persistent launches)
     bool kernel_timing = false;  // per-kernel events (icp4r_set_kernel_timing)
     // plan options (icp4r_set_plan_option; icp4r_pipe::PlanOpt): values, and which are set
-    int32_t plan_val[32] = {};
-    uint32_t plan_set = 0;
+    int32_t plan_val[64] = {};  // (indexed by the plan option enum; kNumPlanOpts <= 64)
+    uint64_t plan_set = 0;
     // RCCL communicators created on this context (icp4r_multi.cpp): detached by icp4r_destroy
     std::vector<icp4r_comm*> comms;
     // HIP events on the launch stream: the dominant NN kernel (the batched search, or the whole NN

@@ -5202,6 +5202,7 @@ struct WideShared {
     alignas(16) float buf[2][9][kWideRow];
     float res[8];
     int32_t cnt[kWideWG / 64];
+    int32_t lay[5];  // fold_update_held_kernel: pass B's layout (kc, S, stride, T, chunks), by thread 0
     SolveShared s;
 };
 
@@ -5496,6 +5497,9 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         const float one_over_n = 1.0f / sh.res[6];
         sh.s.one_over_n = one_over_n;
         for (int k = 0; k < 6; ++k) sh.s.mean[k] = sh.res[k] * one_over_n;
+        // pass B's layout, once (its integer divisions in every lane of 16 waves had cost ~1 us of
+        // VALU on pass B's critical path)
+        layout(total, sh.lay[0], sh.lay[1], sh.lay[2], sh.lay[3], sh.lay[4]);
     }
     __syncthreads();
     if (mse && sh.s.mse_sum < 0.0) {  // (uniform) PCL's sequential double chain over the chunks again
@@ -5525,8 +5529,7 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
     // ---- pass B
     SolveShared& s = sh.s;
     const int cntC = (int)s.mom[0];
-    int kc, S, stride, T, nchb;
-    layout(cntC, kc, S, stride, T, nchb);
+    const int kc = sh.lay[0], S = sh.lay[1], stride = sh.lay[2], T = sh.lay[3], nchb = sh.lay[4];
     const int G = S, R = 9 * G, FW = (R + 63) / 64;
     if (weighted || cntC < n || S <= 1 || S > kSliceGroup || nchb > 14) {
         const FoldIn fin{C, Xp, NT, n};

@@ -207,7 +207,9 @@ int icp4r_stage_time_ms(icp4r_ctx* ctx, int32_t stage, double* avg_ms, int32_t* 
 /* Work the NN kernels performed since the last icp4r_kernel_time_reset — the algorithmic work
  * behind the roofline's `achieved`: distance evaluations (query x target; brute force exactly n*m
  * per pair and pass, the pruned search a small fraction) and bounding-box tests (query x box, the
- * pruned search only; may be NULL).  Synchronises the context's device. */
+ * pruned search only; may be NULL).  Synchronises the context's device.  The counters are
+ * diagnostics, counted only by registrations that ran with plan option "counters" = 1 or with
+ * per-kernel timing on (icp4r_set_kernel_timing); otherwise they stay at zero. */
 int icp4r_nn_counters(icp4r_ctx* ctx, uint64_t* evaluations, uint64_t* box_tests);
 
 /* Queries whose nearest neighbour the cached-neighbour test proved unchanged without a search

@@ -327,7 +327,7 @@ def test_cached_neighbour_batch(gpu_ctx, oracle_mod, numerics, huber, plan):
     assert icp4r.plan(npairs, n, n, ctx=gpu_ctx)["lds"] and icp4r.plan(npairs, n, n, ctx=gpu_ctx)["cache"]
     p = icp4r.default_params(max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0,
                              numerics=numerics, huber_delta=huber)
-    plan(nn_cache=0)
+    plan(nn_cache=0, counters=1)  # (the work counters are opt-in diagnostics)
     gpu_ctx.reset_timers()
     plain = gpu_ctx.align_batch_host(*args, params=p)
     ev_plain, _ = gpu_ctx.nn_counters()
@@ -389,6 +389,7 @@ def test_fused_cache_test_identical(gpu_ctx, oracle_mod, early, plan):
     out = {}
     # (fuse_order = 1, the default: the update's last workgroup also builds the next search's
     # work list from the words the other workgroups publish; 0: nn_order_kernel does)
+    plan(counters=1)
     for fuse, order in (("0", "1"), ("1", "0"), ("1", "1")):
         plan(fuse_test=int(fuse))
         plan(fuse_order=int(order))
@@ -484,12 +485,17 @@ def test_source_order_identical(gpu_ctx, npairs, plan):
     assert (out["1"]["status"] == 0).all()
 
 
-def test_pruned_evaluates_fewer_pairs(gpu_ctx):
-    """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer."""
+def test_pruned_evaluates_fewer_pairs(gpu_ctx, plan):
+    """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer; and the
+    counters are opt-in (zero without plan option counters = 1 or per-kernel timing)."""
     import icp4r
 
     s, t = _pair(340, 8192)
     p = dict(max_iterations=5, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0, compute_fitness=0)
+    gpu_ctx.reset_timers()
+    gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_PRUNED, **p))
+    assert gpu_ctx.nn_counters() == (0, 0)
+    plan(counters=1)
     gpu_ctx.reset_timers()
     gpu_ctx.align(s, t, icp4r.default_params(nn_mode=icp4r.NN_BRUTE, **p))
     brute, brute_tests = gpu_ctx.nn_counters()

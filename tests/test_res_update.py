@@ -33,6 +33,7 @@ def _batch(pairs):
 
 def _run_both(gpu_ctx, plan, args, params):
     out = {}
+    plan(counters=1)
     for on in (0, 1):
         plan(res_update=on)
         gpu_ctx.reset_timers()
