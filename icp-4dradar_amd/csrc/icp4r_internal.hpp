@@ -220,7 +220,7 @@ constexpr int kLdsMaxSources = 1 << 14;  // ... with at most this many sources (
 constexpr int kResMaxN = 8192;            // fold_update_res_kernel: sources of at most this many points
 constexpr int kDefaultResUpdate = 0;      // ... plan option res_update's default
 constexpr int kHeldMaxN = 10 * 896;       // fold_update_held_kernel: sources of at most this many points
-constexpr int kHeldSmallN = 3 * 896;      // ... its 3-record form (the 2k scans) up to this many
+constexpr int kHeldSmallN = 3 * 704;      // ... its 3-record form (the 2k scans; 11 filler waves) up to this many
 constexpr int kDefaultHeldUpdate = 1;     // ... plan option held_update's default
 constexpr int kSoloMaxN = 1024;           // solo_kernel by default for single pairs of at most this many sources
 // wide: one 1024-thread workgroup per pair (fold_update_wide_kernel) — plans with at most one pair

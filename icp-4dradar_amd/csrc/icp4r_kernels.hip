@@ -5278,10 +5278,12 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
 // kernel's global path when a correspondence was rejected or weighted (the panels then start by rank),
 // for one panel, or for more panels than one group.
 constexpr int kHeldFill0 = 128;                       // first filler thread
-constexpr int kHeldFillers = kWideWG - kHeldFill0;    // 896
-constexpr int kHeldCH = 2 * kHeldFillers;             // pass A chunk: two slots of every filler
-static_assert(kHeldCH <= kWideChunkP, "pass A's chunk fits the wide buffers");
-static_assert(kHeldMaxN == 10 * kHeldFillers && kHeldSmallN == 3 * kHeldFillers, "held sizes");
+// S0 (the small form): waves 4, 8 and 12 — the fold wave's SIMD partners (wave w runs on SIMD w mod 4)
+// — hold and stage nothing, so that wave 0's add chains run alone on their SIMD: 11 filler waves
+template <bool S0>
+constexpr int held_fillers() { return S0 ? 11 * 64 : kWideWG - kHeldFill0; }  // 704 / 896
+static_assert(2 * held_fillers<false>() <= kWideChunkP, "pass A's chunk fits the wide buffers");
+static_assert(kHeldMaxN == 10 * held_fillers<false>() && kHeldSmallN == 3 * held_fillers<true>(), "held sizes");
 
 // PCL's sequential double chain over LDS, few registers (the MSE fallback beside the held records)
 __device__ __forceinline__ double fold_seq_d_lite(const double* f, int len, double acc) {
@@ -5302,8 +5304,10 @@ __device__ __forceinline__ double fold_seq_d_lite(const double* f, int len, doub
     return acc;
 }
 
-template <int HOLD>
+template <int HOLD, bool S0>
 __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, WorkArgs w) {
+    constexpr int kHeldFillers = held_fillers<S0>();
+    constexpr int kHeldCH = 2 * kHeldFillers;  // pass A chunk: two slots of every filler
     __shared__ WideShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
     if (w.ticks != nullptr && p == 0 && threadIdx.x == 0) w.ticks[9] = __builtin_amdgcn_s_memrealtime();
@@ -5327,7 +5331,9 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
     const bool mse = kp.need_mse != 0;
     const float ident = weighted ? 0.0f : -0.0f;
     const int nch = (n + kHeldCH - 1) / kHeldCH;
-    const int f = tid - kHeldFill0;  // filler slot column (waves 2..15)
+    // filler slot column: waves 2..15 (S0: but 4, 8, 12 — the idle waves, `idle`)
+    const bool idle = S0 && wv >= 2 && (wv & 3) == 0;
+    const int f = S0 ? (wv - 2 - (wv >> 2)) * 64 + lane : tid - kHeldFill0;
 
     // the records (fillers only: loaded inside pass A's filler branch, so that they are never live in
     // the fold wave's branch — a load ahead of the role branches had kept them live there)
@@ -5427,6 +5433,8 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         } else {
             for (int c = 0; c < nch; ++c) __syncthreads();
         }
+    } else if (idle) {
+        for (int c = 0; c < nch; ++c) __syncthreads();
     } else {
         // the held records, every load in flight together (16-B loads: with the two modes' loads
         // merged, a pointer that lost its alignment was split into four dword loads — 2.4 us more)
@@ -5504,7 +5512,7 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
     __syncthreads();
     if (mse && sh.s.mse_sum < 0.0) {  // (uniform) PCL's sequential double chain over the chunks again
         dacc = 0.0;
-        if (wv == 0) {
+        if (wv == 0 || idle) {
             for (int c = 0; c < nch; ++c) __syncthreads();
         } else if (wv == 1) {
             for (int c = 0; c < nch; ++c) {
@@ -5553,6 +5561,8 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
                 if (wv < FW && L < R && len > 0) pacc = fold_row(bufs(c) + L * stride, len, pacc);
             }
             if (ticks) w.ticks[30] = __builtin_amdgcn_s_memrealtime();
+        } else if (idle) {
+            for (int c = 0; c < nchb; ++c) __syncthreads();
         } else {
             // each held record's LDS offset in its chunk's buffer and the chunk (-1: none), by a
             // float reciprocal of kc, corrected
@@ -6376,9 +6386,9 @@ hipError_t launch_update(const PairArgs& a, const WorkArgs& w, int npairs, int m
         if (need_corr)
             hipLaunchKernelGGL(corr_kernel, dim3((max_n + 255) / 256, npairs), dim3(256), 0, st, a, w);
         if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldSmallN)
-            hipLaunchKernelGGL(fold_update_held_kernel<3>, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+            hipLaunchKernelGGL((fold_update_held_kernel<3, true>), dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (wide && !tail_test && order_ncu <= 0 && w.held_update && max_n <= kHeldMaxN)
-            hipLaunchKernelGGL(fold_update_held_kernel<10>, dim3(npairs), dim3(kWideWG), 0, st, a, w);
+            hipLaunchKernelGGL((fold_update_held_kernel<10, false>), dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (wide && !tail_test && order_ncu <= 0)
             hipLaunchKernelGGL(fold_update_wide_kernel, dim3(npairs), dim3(kWideWG), 0, st, a, w);
         else if (w.res_update && !need_corr && !w.corr && max_n <= kResMaxN && w.nn_t && w.nn_u && w.defer_xform &&

@@ -1,6 +1,7 @@
 """fold_update_held_kernel (round 6): the wide update with the correspondence records held in the
 fillers' registers from pass A to pass B (sources of at most 8960 points: 3 records per filler up to
-2688 — the node's C1 scan — and 10 for the 8k scans of C2 / C5) — needs a real MI355X.
+2112 — the node's C1 scan; 11 filler waves, the fold wave alone on its SIMD — and 10 for the 8k scans
+of C2 / C5) — needs a real MI355X.
 
 Every registration must be bit-identical to fold_update_wide_kernel (plan option held_update = 0)
 and to the oracle: sources across the 896-point slot boundaries (a handful of points, one slot, a
@@ -42,8 +43,8 @@ def _both(gpu_ctx, plan, src, tgt, p):
     (1000, 1200, {}),                                     # a partial second slot
     (2048, 2048, {}),                                     # C1: PCL defaults, 4 panels
     (2048, 2048, {"max_iterations": 20, "mse_threshold_absolute": -1.0, "transformation_epsilon": -1.0}),
-    (2688, 3000, {"max_iterations": 15}),                 # the largest 3-record source
-    (2689, 3000, {"max_iterations": 8}),                  # one past it: the 10-record form
+    (2112, 3000, {"max_iterations": 15}),                 # the largest 3-record source (11 filler waves)
+    (2113, 3000, {"max_iterations": 8}),                  # one past it: the 10-record form
     (8192, 8192, {"max_iterations": 20}),                 # C2: 13 panels
     (8192, 8192, {}),                                     # PCL defaults (MSE live) at 8k
     (8960, 9000, {"max_iterations": 6}),                  # the largest held source: 15 panels, pass B's global path
@@ -104,7 +105,7 @@ def test_held_update_small_batch(gpu_ctx, oracle_mod, plan):
     them: the launch takes the form its largest source needs)."""
     import icp4r
 
-    shapes = [(2048, 2048), (37, 500), (1793, 1800), (2688, 2000), (900, 4000), (8192, 6000)]
+    shapes = [(2048, 2048), (37, 500), (1409, 1800), (2112, 2000), (900, 4000), (8192, 6000)]
     pairs = [_pair(4500 + k, n, m) for k, (n, m) in enumerate(shapes)]
     src = np.concatenate([s for s, _ in pairs]).astype(np.float32)
     tgt = np.concatenate([t for _, t in pairs]).astype(np.float32)
