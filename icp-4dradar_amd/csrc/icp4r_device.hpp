@@ -89,7 +89,7 @@ __device__ __forceinline__ float wave_maxf(float x) {
 }
 
 // Write-through stores (experiment, ICP4R_WT bit mask: 1 = the fused test's stores, 2 = the batched
-// search's result stores): `sc1` vector stores leave no dirty line in the XCD's L2, so the kernel
+// search's result stores, 4 = the one-tile search's stores: X, keys, correspondence records): `sc1` vector stores leave no dirty line in the XCD's L2, so the kernel
 // boundary has less to write back (MI355X_MICROARCH.md §kernel boundary: + dirty bytes / 6 TB/s).
 #ifndef ICP4R_WT
 #define ICP4R_WT 0

@@ -1972,12 +1972,13 @@ __device__ __forceinline__ bool cache_hit(float L, float dj2) {
     return L * L * (1.0f - kCacheMargin) > dj2 * (1.0f + kCacheMargin);
 }
 
+template <int WT = 0>
 __device__ __forceinline__ void write_corr_t(const WorkArgs& w, const PairArgs& a, int p, int i, float sx, float sy,
                                              float sz, float d2, const float4 t) {
     float4* C = w.corr + ((int64_t)p * w.x_stride + i) * 2;
     const float wt = a.kp.huber_delta < INFINITY ? (float)huber_w(d2, a.kp.huber_delta) : 1.0f;
-    C[0] = make_float4(sx, sy, sz, wt);
-    C[1] = make_float4(t.x, t.y, t.z, d2);
+    st_v4<WT>(C, make_float4(sx, sy, sz, wt));
+    st_v4<WT>(C + 1, make_float4(t.x, t.y, t.z, d2));
 }
 
 // With the cached-neighbour state a pass's keys are read only by the finish kernel's fitness (the
@@ -2892,7 +2893,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
 #pragma unroll
             for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].final_T[q]);
             xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
-            if (live) w.X[xs0 + o] = v;
+            if (live) st_v4<4>(w.X + xs0 + o, v);
         }
         if (own && first == 0 && !fitness_pass && w.defer_xform) {
             // the previous update's transformCloud(T_inc), deferred to here (one read and write of X
@@ -2902,7 +2903,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
 #pragma unroll
             for (int q = 0; q < 16; ++q) T[q] = uload(&w.state[p].T_inc[q]);
             xform_pt(T, v.x, v.y, v.z, v.x, v.y, v.z);
-            if (live) w.X[xs0 + o] = v;
+            if (live) st_v4<4>(w.X + xs0 + o, v);
         }
         x = v.x;
         y = v.y;
@@ -3016,13 +3017,13 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
         // real LDS slot; the sentinel position (kb == init) is handled all the same
         const NNKey ko = kb < init ? make_key(key_d2(kb), lk_idx(kb)) : k0;
         if (live) {
-            key[o] = ko;
+            st_sc<4>(key + o, ko);
             if (w.corr != nullptr && !fitness_pass) {  // PCL numerics: the update's correspondence records
                 const float4 t = kb < init ? [&] {
                     const v4f c = sh.tl[lds_swz((int)lk_pos(kb))];
                     return make_float4(tl_x(c), tl_y(c), tl_z(c), 0.f);
                 }() : a.tgt[uload(a.tgt_off + p) + key_idx(k0)];
-                write_corr_t(w, a, p, o, x, y, z, key_d2(ko), t);
+                write_corr_t<4>(w, a, p, o, x, y, z, key_d2(ko), t);
             }
         }
     } else if (live && kb < init) {
