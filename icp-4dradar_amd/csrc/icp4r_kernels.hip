@@ -5284,6 +5284,12 @@ constexpr int kHeldFill0 = 128;                       // first filler thread
 template <bool S0>
 constexpr int held_fillers() { return S0 ? 11 * 64 : kWideWG - kHeldFill0; }  // 704 / 896
 static_assert(2 * held_fillers<false>() <= kWideChunkP, "pass A's chunk fits the wide buffers");
+// pass B's first chunk in the small form (steps; 0: every chunk T steps).  Measured (two A/B rounds):
+// C1 0.384 (0) / 0.381 (128) / 0.385 (64) / 0.388 ms (32); at 8k any ramp lost (C2 1.162 -> 1.175
+// with 128, 1.197 with 32), so the 8k form keeps uniform chunks.
+#ifndef ICP4R_PASSB_RAMP
+#define ICP4R_PASSB_RAMP 128
+#endif
 static_assert(kHeldMaxN == 10 * held_fillers<false>() && kHeldSmallN == 3 * held_fillers<true>(), "held sizes");
 
 // PCL's sequential double chain over LDS, few registers (the MSE fallback beside the held records)
@@ -5308,6 +5314,7 @@ __device__ __forceinline__ double fold_seq_d_lite(const double* f, int len, doub
 template <int HOLD, bool S0>
 __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, WorkArgs w) {
     constexpr int kHeldFillers = held_fillers<S0>();
+    constexpr int kPassBRamp = S0 ? ICP4R_PASSB_RAMP : 0;
     constexpr int kHeldCH = 2 * kHeldFillers;  // pass A chunk: two slots of every filler
     __shared__ WideShared sh;
     const int p = xcd_remap(blockIdx.x, gridDim.x);
@@ -5347,14 +5354,18 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         S = (cnt_ > 0 && kc > 0) ? (cnt_ + kc - 1) / kc : 1;
         stride = (((CAP / max(9 * S, 18)) - 4) & ~7) + 4;
         T = stride - 4;
-        nchb = (kc + T - 1) / T;  // the first panel is the longest
+        // chunks of a ramp: kPassBRamp steps first, doubling up to T (the first chunk's fill is on the
+        // critical path; the later fills overlap the folds before them)
+        nchb = 0;
+        for (int b = 0, len = kPassBRamp > 0 ? min(T, kPassBRamp) : T; b < kc; b += len, len = min(T, 2 * len)) ++nchb;
     };
     int pk[HOLD];
     auto held_offsets = [&](int cnt_) __attribute__((always_inline)) {
         int kc, S, stride, T, nchb;
         layout(cnt_, kc, S, stride, T, nchb);
-        // (the quotients by float reciprocals, corrected: exact for these small operands)
-        const float invkc = 1.0f / (float)kc, invT = 1.0f / (float)T;
+        // (the panel by a float reciprocal, corrected: exact for these small operands; the chunk by
+        // walking the ramp)
+        const float invkc = 1.0f / (float)kc;
 #pragma unroll
         for (int k = 0; k < HOLD; ++k) {
             const int i = f + k * kHeldFillers;
@@ -5362,11 +5373,13 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
             int t = i - q * kc;
             if (t >= kc) { ++q; t -= kc; }
             if (t < 0) { --q; t += kc; }
-            int c = (int)((float)t * invT);
-            int u = t - c * T;
-            if (u >= T) { ++c; u -= T; }
-            if (u < 0) { --c; u += T; }
-            pk[k] = i < n ? ((q * 9 * stride + u) << 4) | (c + 1) : 0;
+            int c = 0, len = kPassBRamp > 0 ? min(T, kPassBRamp) : T;
+            while (t >= len) {
+                t -= len;
+                len = min(T, 2 * len);
+                ++c;
+            }
+            pk[k] = i < n ? ((q * 9 * stride + t) << 4) | (c + 1) : 0;
         }
     };
     clear_need(w, p, n, tid, kWideWG);
@@ -5555,10 +5568,10 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
             const int L = tid;
             const int my_sl = L / 9;
             const int my_len = (wv < FW && L < R) ? min(kc, n - my_sl * kc) : 0;
-            for (int c = 0; c < nchb; ++c) {
+            for (int c = 0, cb = 0, cl = kPassBRamp > 0 ? min(T, kPassBRamp) : T; c < nchb; ++c, cb += cl, cl = min(T, 2 * cl)) {
                 __syncthreads();
                 if (ticks && c < 2) w.ticks[28 + c] = __builtin_amdgcn_s_memrealtime();
-                const int len = min(T, my_len - c * T);
+                const int len = min(cl, my_len - cb);
                 if (wv < FW && L < R && len > 0) pacc = fold_row(bufs(c) + L * stride, len, pacc);
             }
             if (ticks) w.ticks[30] = __builtin_amdgcn_s_memrealtime();
