@@ -2825,6 +2825,9 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     const bool own = first >= 0;  // (single tile: launched with gridDim.x == 1)
     const int tile = blockIdx.x, part = blockIdx.y, p = blockIdx.z;
     const unsigned long long tk_entry = w.pass_ticks ? __builtin_amdgcn_s_memrealtime() : 0;
+#if defined(ICP4R_DIAG_TILE) && ICP4R_DIAG_TILE == 1  // (timing diagnostic only: later passes do nothing — wrong results)
+    if (first == 0 && !fitness_pass) return;
+#endif
     const int phase = uload(&w.state[p].phase);
     if (fitness_pass ? (phase == kPhaseInvalid) : (phase != kPhaseActive)) return;
     const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
@@ -3012,6 +3015,12 @@ __global__ __launch_bounds__(kLdsWG) void nn_tile_kernel(PairArgs a, WorkArgs w,
     if (tail != head) drain(tail - head);
     const NNKey kb = bestl[lane];
     if (tk0) tk[3] = __builtin_amdgcn_s_memrealtime();
+#if defined(ICP4R_DIAG_TILE) && ICP4R_DIAG_TILE == 2  // (timing diagnostic only: no result stores in later passes — wrong results)
+    if (first == 0 && !fitness_pass) {
+        if (lane == 0 && kb == 0x1234) key[0] = kb;  // (keeps the search from being optimised away)
+        return;
+    }
+#endif
     if (own) {
         // the seed target lies in the tile and its block's bound cannot prune it, so the winner is a
         // real LDS slot; the sentinel position (kb == init) is handled all the same

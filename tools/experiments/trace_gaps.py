@@ -43,5 +43,6 @@ for nme in dur:
     mg = statistics.fmean(gap[nme]) if gap[nme] else 0.0
     tot_d += md * per
     tot_g += mg * len(gap[nme]) / len(regs)
-    print(f"{nme:28s} x{per:5.1f}  dur {md:7.2f} us  gap before {mg:5.2f} us")
+    print(f"{nme:28s} x{per:5.1f}  dur {md:7.2f} us (median {statistics.median(dur[nme]):6.2f}, min "
+          f"{min(dur[nme]):6.2f})  gap before {mg:5.2f} us")
 print(f"sum of durations {tot_d:.1f} us, of gaps {tot_g:.1f} us per registration")
