@@ -5364,14 +5364,20 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         stride = (((CAP / max(9 * S, 18)) - 4) & ~7) + 4;
         T = stride - 4;
         // chunks of a ramp: kPassBRamp steps first, doubling up to T (the first chunk's fill is on the
-        // critical path; the later fills overlap the folds before them)
-        nchb = 0;
-        for (int b = 0, len = kPassBRamp > 0 ? min(T, kPassBRamp) : T; b < kc; b += len, len = min(T, 2 * len)) ++nchb;
+        // critical path; the later fills overlap the folds before them).  More panels than one group
+        // (rows too short, down to T = 0 for hundreds of panels) take pass B's global path: 15 chunks
+        // stands for "not held" there, and no loop runs on such a layout.
+        nchb = 15;
+        if (S <= kSliceGroup && T >= 8) {
+            nchb = 0;
+            for (int b = 0, len = kPassBRamp > 0 ? min(T, kPassBRamp) : T; b < kc; b += len, len = min(T, 2 * len)) ++nchb;
+        }
     };
     int pk[HOLD];
     auto held_offsets = [&](int cnt_) __attribute__((always_inline)) {
         int kc, S, stride, T, nchb;
         layout(cnt_, kc, S, stride, T, nchb);
+        if (nchb > 14) return;  // (pass B's global path: no offsets needed, and no loop on T = 0)
         // (the panel by a float reciprocal, corrected: exact for these small operands; the chunk by
         // walking the ramp)
         const float invkc = 1.0f / (float)kc;

@@ -50,6 +50,8 @@ def _both(gpu_ctx, plan, src, tgt, p):
     (8960, 9000, {"max_iterations": 6}),                  # the largest held source: 15 panels, pass B's global path
     (8961, 9000, {"max_iterations": 6}),                  # one past it: the wide kernel
     (6000, 7000, {"eigen_l1_bytes": 49152, "eigen_gebp_mr": 16}),  # other panel widths
+    (2048, 2048, {"eigen_l1_bytes": 1024, "max_iterations": 5}),  # narrow panels: more than one group (global path)
+    (8192, 8192, {"eigen_l1_bytes": 2048, "max_iterations": 4}),
     (2048, 2048, {"max_correspondence_distance": 0.6}),   # rejections: pass B's global ranked path
     (2400, 2048, {"huber_delta": 0.4}),                   # Huber: the same
 ])
