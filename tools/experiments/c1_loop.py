@@ -1,4 +1,5 @@
-"""Registrations of one single pair back to back (for a kernel trace): python3 c1_loop.py [n] [reps]."""
+"""Registrations of one single pair back to back (for a kernel trace): python3 c1_loop.py [n] [reps] [fixed]
+(2048 points: PCL's defaults unless `fixed`; fixed / other sizes: 20 iterations, no early stops)."""
 import os
 import sys
 
@@ -11,7 +12,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 ctx = icp4r.Context(0, plan=icp4r.env_plan())
 pr = synth.make_pair(0, n)
-p = icp4r.default_params() if n == 2048 else icp4r.default_params(
+fixed = len(sys.argv) > 3
+p = icp4r.default_params() if n == 2048 and not fixed else icp4r.default_params(
     max_iterations=20, mse_threshold_absolute=-1.0, transformation_epsilon=-1.0)
 for _ in range(reps):
     ctx.align(pr.src_xyzi(), pr.tgt_xyzi(), p)

@@ -19,6 +19,20 @@ __global__ __launch_bounds__(T) void body_kernel(int* v, int spin) {
     if (threadIdx.x == 0) v[blockIdx.x] = fixed[(blockIdx.x + 1) % (L / 4)] + v[blockIdx.x];
 }
 
+struct Big {  // a kernel argument block the size of icp4r's PairArgs + WorkArgs
+    long long f[96];
+};
+template <int T, int L>
+__global__ __launch_bounds__(T) void big_kernel(Big b, int* v, int spin) {
+    __shared__ int fixed[L / 4];
+    fixed[threadIdx.x % (L / 4)] = threadIdx.x;
+    __syncthreads();
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < spin) {
+    }
+    if (threadIdx.x == 0) v[blockIdx.x] = fixed[(blockIdx.x + 1) % (L / 4)] + v[blockIdx.x] + (int)b.f[blockIdx.x % 96];
+}
+
 int main() {
     int* v;
     hipMalloc(&v, 1 << 20);
@@ -59,5 +73,13 @@ int main() {
         hipLaunchKernelGGL((body_kernel<256, 40 * 1024>), dim3(64), dim3(256), 0, s, v, spin);
     });
     run("no search (update-like only)", [&] {});
+    Big big = {};
+    for (int k = 0; k < 96; ++k) big.f[k] = k;
+    run("search 16 x 1024 thr, 155 KB LDS, 768-B args", [&] {
+        hipLaunchKernelGGL((big_kernel<1024, 155 * 1024>), dim3(16), dim3(1024), 0, s, big, v, spin);
+    });
+    run("search 1 x 64 thr, 4 KB LDS, 768-B args", [&] {
+        hipLaunchKernelGGL((big_kernel<64, 4 * 1024>), dim3(1), dim3(64), 0, s, big, v, spin);
+    });
     return 0;
 }

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 for v in base dtile1 dtile2; do
     ICP4R_LIBRARY=_var/ab/$v/libicp4r.so timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/td_$v -o run --output-format csv -- \
-        python3 tools/experiments/c1_loop.py 2048 30 > gpurun_out/td_$v.log 2>&1
+        python3 tools/experiments/c1_loop.py 2048 30 fixed > gpurun_out/td_$v.log 2>&1
     echo "== $v"
     python3 tools/experiments/trace_gaps.py gpurun_out/td_$v | grep -E "nn_tile|update|span"
 done
