@@ -5293,6 +5293,9 @@ constexpr int kHeldFill0 = 128;                       // first filler thread
 template <bool S0>
 constexpr int held_fillers() { return S0 ? 11 * 64 : kWideWG - kHeldFill0; }  // 704 / 896
 static_assert(2 * held_fillers<false>() <= kWideChunkP, "pass A's chunk fits the wide buffers");
+#ifndef ICP4R_PACKED_FILL
+#define ICP4R_PACKED_FILL 0  // (experiment) the held pass B's products with packed float math
+#endif
 // pass B's first chunk in the small form (steps; 0: every chunk T steps).  Measured (two A/B rounds):
 // C1 0.384 (0) / 0.381 (128) / 0.385 (64) / 0.388 ms (32); at 8k any ramp lost (C2 1.162 -> 1.175
 // with 128, 1.197 with 32), so the 8k form keeps uniform chunks.
@@ -5602,6 +5605,23 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
                 for (int k = 0; k < HOLD; ++k) {
                     if ((pk[k] & 15) != c + 1) continue;
                     const int off = pk[k] >> 4;
+#if ICP4R_PACKED_FILL
+                    // packed (v_pk_add / v_pk_mul: two IEEE float operations per instruction, the same
+                    // roundings — contraction is off): the fill is VALU work of 14 waves on 4 SIMDs
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    const f2 s01 = f2{sx[k], sy[k]} - f2{ms[0], ms[1]};
+                    const f2 d01 = f2{dx[k], dy[k]} - f2{md[0], md[1]};
+                    const float s2 = sz[k] - ms[2], d2 = dz[k] - md[2];
+                    const float dvs[3] = {d01.x, d01.y, d2};
+                    float* o = b + off;
+#pragma unroll
+                    for (int ra = 0; ra < 3; ++ra) {
+                        const f2 pr = f2{dvs[ra], dvs[ra]} * s01;
+                        o[(ra * 3 + 0) * stride] = pr.x;
+                        o[(ra * 3 + 1) * stride] = pr.y;
+                        o[(ra * 3 + 2) * stride] = dvs[ra] * s2;
+                    }
+#else
                     const float sv[3] = {sx[k] - ms[0], sy[k] - ms[1], sz[k] - ms[2]};
                     const float dv[3] = {dx[k] - md[0], dy[k] - md[1], dz[k] - md[2]};
                     float* o = b + off;
@@ -5609,6 +5629,7 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
                     for (int ra = 0; ra < 3; ++ra)
 #pragma unroll
                         for (int rb = 0; rb < 3; ++rb) o[(ra * 3 + rb) * stride] = dv[ra] * sv[rb];
+#endif
                 }
             };
             fill(0);
