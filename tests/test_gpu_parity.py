@@ -485,6 +485,26 @@ def test_source_order_identical(gpu_ctx, npairs, plan):
     assert (out["1"]["status"] == 0).all()
 
 
+def test_work_item_parts_identical(gpu_ctx, oracle_mod, plan):
+    """The batched search's work list cuts a heavy pair's misses into parts of at least `part`
+    misses (round 6 default 2048): any part size — none, small, the default — gives bit-identical
+    registrations, equal to the oracle."""
+    import icp4r
+
+    pairs = [_pair(2600 + k, 8192 if k % 7 == 0 else 2048) for k in range(260)]
+    args = _batch(pairs)
+    assert icp4r.plan(len(pairs), 8192, 8192, ctx=gpu_ctx)["lds"]
+    p = icp4r.default_params(max_iterations=8)
+    out = {}
+    for part in (0, 256, 2048):
+        plan(part=part)
+        out[part] = gpu_ctx.align_batch_host(*args, params=p)
+    assert out[0].tobytes() == out[256].tobytes() == out[2048].tobytes()
+    for k in (0, 7, 259):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=8)
+        assert (np.array(out[2048][k]["T"], np.float32).reshape(4, 4).T == o["T"]).all(), k
+
+
 def test_pruned_evaluates_fewer_pairs(gpu_ctx, plan):
     """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer; and the
     counters are opt-in (zero without plan option counters = 1 or per-kernel timing)."""
