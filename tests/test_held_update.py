@@ -147,3 +147,17 @@ def test_fitness_transform_in_search_identical(gpu_ctx, oracle_mod, plan, n, m, 
     o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True, **kw)
     assert out[1][1] == o["fitness"] and (out[1][0] == o["T"]).all()
     assert (out[1][3] == o["aligned"].view(np.uint32)).all()
+
+
+def test_aligned_without_fitness_keeps_prep(gpu_ctx, oracle_mod, plan):
+    """compute_fitness = 0 with the aligned cloud asked for: no fitness pass to form X := final *
+    input in, so fitness_prep_kernel runs (fit_xform applies only with the fitness pass) — the aligned
+    cloud still equals the oracle's."""
+    import icp4r
+
+    src, tgt = _pair(4800, 2048)
+    p = icp4r.default_params(compute_fitness=0)
+    r, al = gpu_ctx.align(src, tgt, p, want_aligned=True)
+    o = oracle_mod.align(src, tgt, numerics=oracle_mod.NUM_F32, aligned=True)
+    assert (r.matrix() == o["T"]).all()
+    assert (al.view(np.uint32) == o["aligned"].view(np.uint32)).all()
