@@ -5272,11 +5272,12 @@ __global__ __launch_bounds__(kWideWG) void fold_update_wide_kernel(PairArgs a, W
 }
 
 // ---------------------------------------------------------------------------------------------
-// fold_update_held_kernel<HOLD> (round 6): fold_update_wide_kernel for sources of at most
-// HOLD x 896 points (HOLD = 3: the node's 2k C1 scan; 10: the 8k scans of C2 / C5), with the pair's
-// correspondence records read from HBM once per update.  The 896 filler threads (waves 2..15) load
-// their records (record i is filler i mod 896's slot i / 896) before the first barrier, every load in
-// flight together, and keep each as six floats in registers (s and d; d² and the weight are
+// fold_update_held_kernel<HOLD, S0> (round 6): fold_update_wide_kernel for sources of at most
+// HOLD x F points (F filler threads: <3, true> up to 2,112 — the node's 2k C1 scan, F = 704; <10, false>
+// up to 8,960 — the 8k scans of C2 / C5, F = 896), with the pair's correspondence records read from
+// HBM once per update.  The filler threads (waves 2..15; S0: but 4, 8, 12) load their records (record
+// i is filler i mod F's slot i / F) — chunk 0's two slots first, the rest after the first barrier —
+// and keep each as six floats in registers (s and d; d² and the weight are
 // recomputed — the search formed the record's d² as l2_simple(s, d) and its weight from that, with
 // contraction off, so the same bits): pass A's chunk c is slots 2c and 2c + 1 of every filler (LDS
 // stores only, no round trip per chunk), and pass B's panel chunks take each record's nine products
