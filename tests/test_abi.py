@@ -177,6 +177,13 @@ def test_plan_options_api():
             v, is_set = ctx.get_plan_option(name)
             assert not is_set, name
         assert ctx.get_plan_option("groups") == (2, False) and ctx.get_plan_option("leaf") == (16, False)
+        # round-6 options: held update and in-search fitness transform on, counters opt-in
+        assert ctx.get_plan_option("held_update") == (1, False)
+        assert ctx.get_plan_option("fit_xform") == (1, False)
+        assert ctx.get_plan_option("counters") == (0, False)
+        ctx.set_plan(held_update=0, counters=1)
+        assert ctx.get_plan_option("held_update") == (0, True) and ctx.get_plan_option("counters") == (1, True)
+        ctx.reset_plan_options()
         ctx.set_plan(groups=1, nn_cache=0)
         assert ctx.get_plan_option("groups") == (1, True) and ctx.get_plan_option("nn_cache") == (0, True)
         for bad in (("groups", 4), ("groups", 0), ("no_such_option", 1), ("xpad", -1)):
