@@ -38,7 +38,7 @@ enum PlanOpt : int {
     kOptPhaseTicks, kOptKd, kOptMortonMwg, kOptPart, kOptSrcOrder, kOptFuseSeed, kOptTileOwn, kOptTileDefer,
     kOptGroups, kOptSearchCuDiv, kOptFuseTest, kOptFuseOrder, kOptSumsTail, kOptWideUpdate, kOptGatherPadded,
     kOptGicpCovBrute, kOptFoldKeys, kOptGicpSpec, kOptGicpGrid, kOptGicpKnnLanes, kOptResUpdate, kOptHeldUpdate,
-    kOptFitXform, kOptCounters, kNumPlanOpts
+    kOptFitXform, kOptCounters, kOptStageSel, kNumPlanOpts
 };
 static_assert(kNumPlanOpts <= 64, "icp4r_ctx::plan_set is a 64-bit mask");
 extern const char* const kPlanOptNames[kNumPlanOpts];

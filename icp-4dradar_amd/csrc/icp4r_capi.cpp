@@ -105,7 +105,7 @@ const char* const kPlanOptNames[kNumPlanOpts] = {
     "phase_ticks", "kd", "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer",
     "groups", "search_cu_div", "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded",
     "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update",
-    "held_update", "fit_xform", "counters"};
+    "held_update", "fit_xform", "counters", "stage_sel"};
 
 int opt(const icp4r_ctx* ctx, PlanOpt k, int dflt) {
     return (ctx && (ctx->plan_set >> k & 1ull)) ? ctx->plan_val[k] : dflt;
@@ -386,6 +386,7 @@ int setup_work(icp4r_ctx* ctx, const Plan& pl, int npairs, int max_n, int max_m,
             w.miss_cnt = static_cast<int32_t*>(ctx->miss_cnt.p);
             w.part_size = opt(ctx, kOptPart, kDefaultPartSize);
             if (w.part_size != 0 && w.part_size < 64) w.part_size = 64;
+            w.stage_sel = std::max(0, opt(ctx, kOptStageSel, kDefaultStageSel));
             // (a fresh registration starts from zero: init_kernel clears the pair's bitmap and count —
             // three memset launches per batch, and their boundaries, fewer)
         }
@@ -1119,7 +1120,7 @@ int icp4r_get_plan_option(const icp4r_ctx* ctx, const char* name, int32_t* value
             0 /*nn_q: per plan*/, kDefaultLeaf, 0 /*chunk_sb: auto*/, -1 /*nn_lds: auto*/, 1, 1, 0 /*tile_run: auto*/,
             -1 /*solo: auto*/, 0, 0, 3, 1, kDefaultPartSize, -1 /*src_order: per plan*/, 1, 1, 1, kDefaultGroups,
             0 /*search_cu_div: groups*/, 1, 1, 0, 1, 0, 0, 1, kGicpSpec, kGicpGrid,
-            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate, 1, 0};
+            0 /*gicp_knn_lanes: auto*/, kDefaultResUpdate, kDefaultHeldUpdate, 1, 0, kDefaultStageSel};
         *value = dflt[k];
     }
     if (is_set) *is_set = set ? 1 : 0;

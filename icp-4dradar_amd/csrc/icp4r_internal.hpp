@@ -18,6 +18,7 @@ constexpr int kDefaultPrunedQ = 2;  // pruned: default cap
 constexpr int kDefaultLeaf = 16;    // pruned: targets per block
 constexpr int kMaxGroups = 3;        // batched plans: pair groups on their own streams (run_pairs)
 constexpr int kDefaultGroups = 2;
+constexpr int kDefaultStageSel = 32;    // batched search: plan option stage_sel's default
 constexpr int kDefaultPartSize = 2048;  // batched search: misses per work item of a heavy pair (round 6: 1024 -> 2048, C3 +0.6 %)
 constexpr int kFoldChunk = 1024;  // points per LDS chunk of the sequential fitness fold
 constexpr int kSuper = 8;         // target blocks per superblock (pruned NN)
@@ -182,6 +183,8 @@ struct WorkArgs {
                         // builds the work list itself (plist_n[3]: its arrival counter)
     int32_t part_size;  // nn_lds_kernel: misses per work item of a heavy pair (0: one item per pair);
                         // plist holds items (pair << 10 | part)
+    int32_t stage_sel;  // nn_lds_kernel: a ranked item of at most this many misses stages only the
+                        // superblocks its queries can reach (stage_tile_sel; plan option stage_sel, 0: off)
     unsigned long long* evals;  // [kCountSlots][kCountStride]: per slot distance evaluations, box tests,
                                 // cached-neighbour hits (count_add; the host sums the slots)
     uint64_t* ticks;    // debug (plan option phase_ticks = 1): s_memrealtime (100 MHz) at fold_update phase

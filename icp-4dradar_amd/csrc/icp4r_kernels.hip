@@ -1902,6 +1902,7 @@ struct LdsNN {
     uint16_t items[kLdsWaves][kRing + 64];             // 6 KB: (query lane << 9) | block; + a spare slot per lane
     int32_t wsum[kLdsWaves];                           // staging: bitmap popcounts per wave
     int32_t cur;                                       // the pair this workgroup works on
+    unsigned long long selm[kLdsWaves];                // staging (reach_all): superblocks per wave's queries
 };
 
 // LDS slot of sorted target position p: the slot inside its 16-target block XOR the block's low
@@ -2227,14 +2228,15 @@ struct TileRegs {
     v4f blo, bhi, isl, ish;
 };
 template <int WG>
-__device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, TileRegs<WG>& r) {
+__device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, TileRegs<WG>& r, uint64_t M = ~0ull) {
     const int tid = threadIdx.x, lane = tid & 63;
     const v4f* tsg = reinterpret_cast<const v4f*>(w.tsort + (int64_t)p * w.t_stride);
     const int nt = nsb * kSuper * kLdsLeaf;
     constexpr int kPerT = kLdsTargets / WG;
     static_assert(kLdsTargets % WG == 0, "targets per thread");
 #pragma unroll
-    for (int k = 0; k < kPerT; ++k) r.tv[k] = tsg[min(tid + k * WG, nt - 1)];
+    for (int k = 0; k < kPerT; ++k)  // (M: superblocks to stage; a wave's 64 positions lie in one)
+        if (M == ~0ull || ((M >> ((tid + k * WG) / (kLdsLeaf * kSuper))) & 1ull)) r.tv[k] = tsg[min(tid + k * WG, nt - 1)];
     const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
     const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
     static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= WG, "one box per thread");
@@ -2249,7 +2251,7 @@ __device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, Til
     r.ish = sbg[2 * sbl + 1];
 }
 template <int WG>
-__device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const TileRegs<WG>& r) {
+__device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const TileRegs<WG>& r, uint64_t M = ~0ull) {
     const int tid = threadIdx.x;
     const int nt = nsb * kSuper * kLdsLeaf;
     constexpr int kPerT = kLdsTargets / WG;
@@ -2259,7 +2261,8 @@ __device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const Til
         // (opaque: the slot addresses are formed here, not hoisted out of a caller's item loop as
         // invariants — kept live across the search they pushed its other values into scratch)
         asm volatile("" : "+v"(i));
-        if (i < nt) sh.tl[lds_swz(i)] = tl_slot(r.tv[k], (__float_as_uint(r.tv[k].w) << kLdsPosBits) | (uint32_t)i);
+        if (i < nt && (M == ~0ull || ((M >> (i / (kLdsLeaf * kSuper))) & 1ull)))
+            sh.tl[lds_swz(i)] = tl_slot(r.tv[k], (__float_as_uint(r.tv[k].w) << kLdsPosBits) | (uint32_t)i);
     }
     const int nbx = nsb * (kSuper + 1);
     if (tid < nbx) {
@@ -2277,12 +2280,96 @@ __device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const Til
 // issued before the first store: a load-store loop waited out one global round trip per target (8
 // per thread, ~10-20 us per item under load).  The caller's barrier makes the LDS visible.
 template <int WG>
-__device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w, int p, int nsb, v4f& isl, v4f& ish) {
+__device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w, int p, int nsb, v4f& isl, v4f& ish,
+                                           uint64_t M = ~0ull) {
     TileRegs<WG> r;
-    tile_load<WG>(w, p, nsb, r);
-    tile_store<WG>(sh, nsb, r);
+    tile_load<WG>(w, p, nsb, r, M);
+    tile_store<WG>(sh, nsb, r, M);
     isl = r.isl;
     ish = r.ish;
+}
+
+// The superblocks an item's queries can reach (plan option stage_sel): a lane-per-superblock test of
+// each query against lds_runs' initial pruning bound.  lds_runs reads a target only (a) in a query's
+// seed block, or (b) in a block it queued, whose superblock passed pt_lb(superblock, q) <= bnd_q for
+// that query; and bnd_q = min(seed block's second-smallest d², U²·1.00001) · kLbGrow never exceeds
+// B_q = (U²·1.00001) · kLbGrow (the same float expressions: rounding is monotone), nor grows.  So
+// every target the search reads lies in a superblock with pt_lb <= B_q for some query of the item,
+// or in a seed's superblock — the mask below holds both (idle lanes shadow a run's first query, so
+// they read its seed).  A U that is not finite stages everything.  Wave w tests queries w, w + NW, …
+// (uniform loads); the caller ORs the waves' masks.  Items of more than kSelExact queries: per run of 64.
+constexpr int kSelExact = 64;
+template <int WG>
+__device__ __forceinline__ uint64_t reach_mask(const float4* qv, const uint2* qm, int nlist, int m, int nsb,
+                                               const v4f isl, const v4f ish) {
+    constexpr int NW = WG / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const float b[6] = {isl.x, isl.y, isl.z, ish.x, ish.y, ish.z};  // (an empty box passes: a superset)
+    const bool mine = lane < nsb;
+    uint64_t mk = 0;
+    if (nlist > kSelExact) {
+        // larger items: 64 consecutive queries (a compact run of sorted positions) at a time, tested as
+        // their bounding box against their largest bound — box_lb(sb, box) <= pt_lb(sb, q) <= B_q <= max B
+        // for every query q in the box (the same per-axis gaps, monotone float arithmetic): a superset
+        const v4f lo4 = isl, hi4 = ish;
+        for (int j0 = wave * 64; j0 < nlist; j0 += NW * 64) {
+            const int j = min(j0 + lane, nlist - 1);
+            const float4 q = qv[j];
+            const uint32_t sd = qm[j].y;
+            const float B = __uint_as_float(__float_as_uint(q.w * q.w * 1.00001f)) * kLbGrow;
+            if (__ballot(!(B < INFINITY)) != 0ull) return ~0ull;
+            float qlo[3] = {q.x, q.y, q.z}, qhi[3] = {q.x, q.y, q.z};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                qlo[k] = wave_minf(qlo[k]);
+                qhi[k] = wave_maxf(qhi[k]);
+            }
+            const float bmax = wave_maxf(B);
+            mk |= __ballot(mine && box_lb(lo4, hi4, qlo, qhi) <= bmax);
+            unsigned long long s = 1ull << (min(sd, (uint32_t)(m - 1)) / (uint32_t)(kLdsLeaf * kSuper));
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s |= __shfl_xor(s, off, 64);
+            mk |= s;
+        }
+        return mk;
+    }
+    for (int j0 = wave; j0 < nlist; j0 += 4 * NW) {
+        float4 q[4];
+        uint32_t sd[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int j = min(j0 + e * NW, nlist - 1);
+            q[e] = qv[j];
+            sd[e] = qm[j].y;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float B = __uint_as_float(__float_as_uint(q[e].w * q[e].w * 1.00001f)) * kLbGrow;
+            mk |= (B < INFINITY) ? __ballot(mine && pt_lb(b, q[e].x, q[e].y, q[e].z) <= B) : ~0ull;
+            mk |= 1ull << (min(sd[e], (uint32_t)(m - 1)) / (uint32_t)(kLdsLeaf * kSuper));
+        }
+    }
+    return mk;
+}
+
+// The superblock mask of a small item (stage_sel): reach_mask over the workgroup's waves, ORed through
+// selm (kLdsWaves words of LDS); ends with a barrier.  stage_tile then loads the targets of the named
+// superblocks only (a late pass's item of a few misses stages a few KB instead of the whole 128-KB
+// tile, for one more round trip: the queries and superblock boxes before the targets).
+template <int WG>
+__device__ __forceinline__ uint64_t reach_all(unsigned long long* selm, const WorkArgs& w, int p, int nsb, int m,
+                                              const float4* qv, const uint2* qm, int nlist) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
+    const int sbl = min(lane, nsb - 1);
+    const uint64_t mk = reach_mask<WG>(qv, qm, nlist, m, nsb, sbg[2 * sbl], sbg[2 * sbl + 1]);
+    if (lane == 0) selm[tid >> 6] = mk;
+    __syncthreads();
+    uint64_t M = 0;
+#pragma unroll
+    for (int v = 0; v < WG / 64; ++v) M |= selm[v];
+    return M;
 }
 
 // The exact LDS search of one query list [0, nlist) of pair p (qv / qm: {x, y, z, U}, {source index |
@@ -2647,6 +2734,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         //    reading it).
         int nlist;
         const int mc = (CACHE && !first && ranked) ? uload(w.miss_cnt + p) : kMissUnranked;
+        bool sel = false;  // a small ranked item: stage the superblocks its queries can reach only
         if (!(mc & kMissUnranked)) {
             // the fused test put the pair's misses in rank order already (pair_cache_test)
             const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
@@ -2655,6 +2743,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             nlist = min(hi, mc) - lo;
             qv += lo;
             qm += lo;
+            sel = nlist <= w.stage_sel;
         } else if (CACHE && !first) {
             const uint32_t* gneed = w.need + (int64_t)p * w.need_stride;
             const int ps = uload(w.plist_n + 2);  // the order kernel's part size for this pass
@@ -2755,7 +2844,8 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         // (8 per thread, ~10-20 us per item under load).
         const LdsTile tv{sh.tl, sh.bx, sh.sbx};
         v4f isl, ish;
-        stage_tile<kLdsWG>(tv, w, p, nsb, isl, ish);
+        const uint64_t M = sel ? reach_all<kLdsWG>(sh.selm, w, p, nsb, m, qv, qm, nlist) : ~0ull;
+        stage_tile<kLdsWG>(tv, w, p, nsb, isl, ish, M);
         __syncthreads();  // LDS targets; qv / qm (global, this workgroup's) visible to every wave
         if (tk) tk2 = __builtin_amdgcn_s_memrealtime();
         unsigned long long* bestl = sh.r.best[wave];

@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = [
 PLAN_OPTIONS = (
     "nn_q", "leaf", "chunk_sb", "nn_lds", "nn_cache", "nn_tile", "tile_run", "solo", "xpad", "phase_ticks", "kd",
     "morton_mwg", "part", "src_order", "fuse_seed", "tile_own", "tile_defer", "groups", "search_cu_div",
-    "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded", "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update", "held_update", "fit_xform", "counters",
+    "fuse_test", "fuse_order", "sums_tail", "wide_update", "gather_padded", "gicp_cov_brute", "fold_keys", "gicp_spec", "gicp_grid", "gicp_knn_lanes", "res_update", "held_update", "fit_xform", "counters", "stage_sel",
 )
 # include/icp4r/icp4r_ego.h (radar ego velocity and the scan parse; icp4r.ego)
 EGO_EXPORTED_SYMBOLS = [

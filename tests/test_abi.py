@@ -181,6 +181,7 @@ def test_plan_options_api():
         assert ctx.get_plan_option("held_update") == (1, False)
         assert ctx.get_plan_option("fit_xform") == (1, False)
         assert ctx.get_plan_option("counters") == (0, False)
+        assert ctx.get_plan_option("stage_sel") == (32, False)
         ctx.set_plan(held_update=0, counters=1)
         assert ctx.get_plan_option("held_update") == (0, True) and ctx.get_plan_option("counters") == (1, True)
         ctx.reset_plan_options()

@@ -505,6 +505,28 @@ def test_work_item_parts_identical(gpu_ctx, oracle_mod, plan):
         assert (np.array(out[2048][k]["T"], np.float32).reshape(4, 4).T == o["T"]).all(), k
 
 
+def test_stage_sel_identical(gpu_ctx, oracle_mod, plan):
+    """Small ranked work items stage only the superblocks their queries can reach (plan option
+    stage_sel: items of at most that many misses): off, tiny, the default and every item give
+    bit-identical registrations and fitness, equal to the oracle — a superblock the search needed and
+    the mask left out would be read as the previous item's targets."""
+    import icp4r
+
+    pairs = [_pair(2900 + k, 8192 if k % 5 == 0 else 4096) for k in range(300)]
+    args = _batch(pairs)
+    assert icp4r.plan(len(pairs), 8192, 8192, ctx=gpu_ctx)["lds"]
+    p = icp4r.default_params(max_iterations=12)
+    out = {}
+    for sel in (0, 16, 128, 1 << 20):
+        plan(stage_sel=sel)
+        out[sel] = gpu_ctx.align_batch_host(*args, params=p)
+    assert out[0].tobytes() == out[16].tobytes() == out[128].tobytes() == out[1 << 20].tobytes()
+    for k in (0, 3, 299):
+        o = oracle_mod.align(*pairs[k], numerics=oracle_mod.NUM_F32, max_iterations=12)
+        assert (np.array(out[128][k]["T"], np.float32).reshape(4, 4).T == o["T"]).all(), k
+        assert out[128][k]["fitness"] == o["fitness"], k
+
+
 def test_pruned_evaluates_fewer_pairs(gpu_ctx, plan):
     """The evaluation counter: brute force evaluates exactly n*m per pass; pruning far fewer; and the
     counters are opt-in (zero without plan option counters = 1 or per-kernel timing)."""
