@@ -2234,9 +2234,15 @@ __device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, Til
     const int nt = nsb * kSuper * kLdsLeaf;
     constexpr int kPerT = kLdsTargets / WG;
     static_assert(kLdsTargets % WG == 0, "targets per thread");
+    // M: the superblocks to stage; the others load target 0 (one line for the whole wave) into slots
+    // no search reads.  A wave's 64 positions lie in one superblock: the test is scalar.
+    static_assert(kLdsLeaf * kSuper % 64 == 0 && WG % (kLdsLeaf * kSuper) == 0, "wave-uniform superblock");
+    const int wsb = __builtin_amdgcn_readfirstlane(tid / (kLdsLeaf * kSuper));
 #pragma unroll
-    for (int k = 0; k < kPerT; ++k)  // (M: superblocks to stage; a wave's 64 positions lie in one)
-        if (M == ~0ull || ((M >> ((tid + k * WG) / (kLdsLeaf * kSuper))) & 1ull)) r.tv[k] = tsg[min(tid + k * WG, nt - 1)];
+    for (int k = 0; k < kPerT; ++k) {
+        const bool on = M == ~0ull || ((M >> (wsb + k * (WG / (kLdsLeaf * kSuper)))) & 1ull);
+        r.tv[k] = tsg[on ? min(tid + k * WG, nt - 1) : 0];
+    }
     const v4f* tb = reinterpret_cast<const v4f*>(w.tbox + (int64_t)p * 2 * w.b_stride);
     const v4f* sbg = reinterpret_cast<const v4f*>(w.sbox + (int64_t)p * 2 * w.sb_stride);
     static_assert(kLdsTargets / kLdsLeaf / kSuper * (kSuper + 1) <= WG, "one box per thread");
@@ -2251,7 +2257,7 @@ __device__ __forceinline__ void tile_load(const WorkArgs& w, int p, int nsb, Til
     r.ish = sbg[2 * sbl + 1];
 }
 template <int WG>
-__device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const TileRegs<WG>& r, uint64_t M = ~0ull) {
+__device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const TileRegs<WG>& r) {
     const int tid = threadIdx.x;
     const int nt = nsb * kSuper * kLdsLeaf;
     constexpr int kPerT = kLdsTargets / WG;
@@ -2261,8 +2267,7 @@ __device__ __forceinline__ void tile_store(const LdsTile& sh, int nsb, const Til
         // (opaque: the slot addresses are formed here, not hoisted out of a caller's item loop as
         // invariants — kept live across the search they pushed its other values into scratch)
         asm volatile("" : "+v"(i));
-        if (i < nt && (M == ~0ull || ((M >> (i / (kLdsLeaf * kSuper))) & 1ull)))
-            sh.tl[lds_swz(i)] = tl_slot(r.tv[k], (__float_as_uint(r.tv[k].w) << kLdsPosBits) | (uint32_t)i);
+        if (i < nt) sh.tl[lds_swz(i)] = tl_slot(r.tv[k], (__float_as_uint(r.tv[k].w) << kLdsPosBits) | (uint32_t)i);
     }
     const int nbx = nsb * (kSuper + 1);
     if (tid < nbx) {
@@ -2284,7 +2289,7 @@ __device__ __forceinline__ void stage_tile(const LdsTile& sh, const WorkArgs& w,
                                            uint64_t M = ~0ull) {
     TileRegs<WG> r;
     tile_load<WG>(w, p, nsb, r, M);
-    tile_store<WG>(sh, nsb, r, M);
+    tile_store<WG>(sh, nsb, r);
     isl = r.isl;
     ish = r.ish;
 }
@@ -2369,7 +2374,9 @@ __device__ __forceinline__ uint64_t reach_all(unsigned long long* selm, const Wo
     uint64_t M = 0;
 #pragma unroll
     for (int v = 0; v < WG / 64; ++v) M |= selm[v];
-    return M;
+    // (uniform: scalar registers, not two VGPRs live across the staging)
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(M >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)M);
 }
 
 // The exact LDS search of one query list [0, nlist) of pair p (qv / qm: {x, y, z, U}, {source index |
