@@ -1903,7 +1903,10 @@ struct LdsNN {
     int32_t wsum[kLdsWaves];                           // staging: bitmap popcounts per wave
     int32_t cur;                                       // the pair this workgroup works on
     unsigned long long selm[kLdsWaves];                // staging (reach_all): superblocks per wave's queries
+    int32_t fin;                                       // (claim-ahead) waves done with their runs, all items
+    int32_t nx[2][5];                                  // (claim-ahead) item k's {index, item, n, m, misses} in nx[k & 1]
 };
+
 
 // LDS slot of sorted target position p: the slot inside its 16-target block XOR the block's low
 // bits — an involution per block (bank spreading for the drain, see nn_lds_kernel)
@@ -2691,6 +2694,31 @@ __device__ __forceinline__ void lds_runs(const LdsTile& sh, unsigned long long* 
     }
 }
 
+// Claim-ahead (ICP4R_CLAIM_AHEAD): the next work item's index, pair word, sizes and miss count are
+// fetched by lane 0 of the first wave of the workgroup to finish its runs of the current item —
+// three dependent round trips (the queue add, the list, the pair's sizes) that then overlap the
+// slower waves' runs instead of sitting between two items.  The claim is at most one item's runs
+// early (the list is heaviest first: the last items are the smallest).
+#ifndef ICP4R_CLAIM_AHEAD
+#define ICP4R_CLAIM_AHEAD 1
+#endif
+__device__ __forceinline__ void claim_item(const PairArgs& a, const WorkArgs& w, int npl, int32_t* nx) {
+    const int idx = atomicAdd(w.queue, 1);
+    int item = 0, n = 0, m = 0, mc = 0;
+    if (idx < npl) {
+        item = w.plist[idx];
+        const int p = item >> kPartBits;
+        n = a.src_n[p];
+        m = a.tgt_n[p];
+        mc = w.miss_cnt ? w.miss_cnt[p] : 0;
+    }
+    nx[0] = idx;
+    nx[1] = item;
+    nx[2] = n;
+    nx[3] = m;
+    nx[4] = mc;
+}
+
 // ---- nn_lds_kernel<CACHE>: persistent search over the pair work list.
 // CACHE: per searched query the exact second-nearest distance too, stored as the cached-neighbour
 // state: L in X_i.w, U in nn_u[i], the NN's coordinates in nn_t[i] with .w = its index | the query's
@@ -2709,6 +2737,22 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
     // summed over the registration in ticks[16..26], and per pass in pass_ticks[0..10];
     // tools/experiments/nn_events.py): wave-uniform adds, stored once at the end
     RunStats rs;
+#if ICP4R_CLAIM_AHEAD
+    if (tid == 0) {
+        claim_item(a, w, npl, sh.nx[0]);
+        sh.fin = 0;
+    }
+    __syncthreads();
+    for (int it = 0;; ++it) {
+        const int32_t* nx = sh.nx[it & 1];
+        const int idx = __builtin_amdgcn_readfirstlane(nx[0]);
+        if (idx >= npl) break;  // uniform: every wave read the same word
+        const bool tk = w.ticks != nullptr && tid == 0;
+        uint64_t tk0 = tk ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = tk0, tk2 = tk0;
+        const int item = __builtin_amdgcn_readfirstlane(nx[1]);
+        const int p = item >> kPartBits, part = item & ((1 << kPartBits) - 1);
+        const int n = __builtin_amdgcn_readfirstlane(nx[2]), m = __builtin_amdgcn_readfirstlane(nx[3]);
+#else
     for (;;) {
         if (tid == 0) sh.cur = atomicAdd(w.queue, 1);
         __syncthreads();
@@ -2721,6 +2765,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         const int item = w.plist[idx];
         const int p = item >> kPartBits, part = item & ((1 << kPartBits) - 1);
         const int n = uload(a.src_n + p), m = uload(a.tgt_n + p);
+#endif
         const int nb = (m + kLdsLeaf - 1) / kLdsLeaf, nsb = (nb + kSuper - 1) / kSuper;
         const int64_t xs0 = (int64_t)p * w.x_stride;
         float4* X = w.X + xs0;
@@ -2740,7 +2785,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         //    rank in the miss bitmap.  The update kernel clears the bitmap (other parts may still be
         //    reading it).
         int nlist;
+#if ICP4R_CLAIM_AHEAD
+        const int mc = (CACHE && !first && ranked) ? __builtin_amdgcn_readfirstlane(nx[4]) : kMissUnranked;
+#else
         const int mc = (CACHE && !first && ranked) ? uload(w.miss_cnt + p) : kMissUnranked;
+#endif
         bool sel = false;  // a small ranked item: stage the superblocks its queries can reach only
         if (!(mc & kMissUnranked)) {
             // the fused test put the pair's misses in rank order already (pair_cache_test)
@@ -2859,6 +2908,11 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
         uint32_t* secl = sh.sec[wave];
         uint16_t* ring = sh.items[wave];
         lds_runs<CACHE>(tv, bestl, secl, ring, qv, qm, nlist, m, nsb, isl, ish, a, w, p, xs0, X, key, want_key, corr, rs);
+#if ICP4R_CLAIM_AHEAD
+        // the first wave done claims the next item (sh.nx[(it + 1) & 1]: item it - 1's words, read by
+        // every wave before this item's staging barrier)
+        if (lane == 0 && atomicAdd(&sh.fin, 1) == it * kLdsWaves) claim_item(a, w, npl, sh.nx[(it + 1) & 1]);
+#endif
         __syncthreads();  // LDS (targets, per-wave state, sh.cur) is reused by the next pair
         if (tk) {
             unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ticks);
