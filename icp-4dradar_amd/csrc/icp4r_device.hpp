@@ -78,6 +78,22 @@ __device__ __forceinline__ float wave_minf(float x) {
     x = fminf(x, dpp_f<0x143, 0xc>(x));  // row_bcast31 -> rows 2, 3
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
+// Wave-wide integer sum by the same DPP steps (exact in any order).  No lane addresses: the
+// __shfl_xor butterfly's ds_bpermute addresses, shared by the compiler across a kernel's reductions,
+// were kept live — and spilled — from pass A's count to the fused test's (fold_update_kernel).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ int wave_sumi(int x) {
+    x += dpp_i<0xB1>(x);
+    x += dpp_i<0x4E>(x);
+    x += dpp_i<0x141>(x);
+    x += dpp_i<0x140>(x);
+    x += dpp_i<0x142, 0xa>(x);
+    x += dpp_i<0x143, 0xc>(x);
+    return __builtin_amdgcn_readlane(x, 63);
+}
 __device__ __forceinline__ float wave_maxf(float x) {
     x = fmaxf(x, dpp_f<0xB1>(x));
     x = fmaxf(x, dpp_f<0x4E>(x));

@@ -3751,8 +3751,8 @@ __device__ __forceinline__ int test_place(const WorkArgs& w, int p, int n, int h
                                           uint64_t* stamp) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t xs = (int64_t)p * w.x_stride;
-    hits = wave_sum(hits);
-    misses = wave_sum(misses);
+    hits = wave_sumi(hits);
+    misses = wave_sumi(misses);
     if (lane == 0) {
         wcnt[wave] = misses;
         count_add(w.evals, 0, (unsigned long long)hits);
@@ -4205,8 +4205,7 @@ __device__ __forceinline__ void fold_pass_a(const KParams& kp, const FoldIn& f, 
         }
     }
     // |C|: exact integer reduction of the fillers' counts
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    cnt = wave_sumi(cnt);
     if (lane == 0) wcnt[wave] = cnt;
     if (wave == 0 && lane < 7) res[lane] = (sums && lane < 3) ? sums[lane] : acc;
     if (wave == 1 && lane == 0) s.mse_sum = dacc;  // 0 without the MSE chain (not used then)
