@@ -5674,9 +5674,8 @@ __global__ __launch_bounds__(kWideWG) void fold_update_held_kernel(PairArgs a, W
         // pass B's critical path)
         held_offsets(n);
     }
-    // |C|: exact integer reduction of the fillers' counts
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    // |C|: exact integer reduction of the fillers' counts (DPP: wave 0 runs it after its chain)
+    cnt = wave_sumi(cnt);
     if (lane == 0) sh.cnt[wave] = cnt;
     if (wave == 0 && lane < 7) sh.res[lane] = acc;
     if (wave == 1 && lane == 0) sh.s.mse_sum = dacc;
