@@ -78,6 +78,27 @@ __device__ __forceinline__ float wave_minf(float x) {
     x = fminf(x, dpp_f<0x143, 0xc>(x));  // row_bcast31 -> rows 2, 3
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
+// Min / max over each aligned group of B lanes (B = 16: the DPP quad xors and the half-row and row
+// mirrors leave every lane of a 16-lane row holding the row's extreme; B = 32 adds one xor-16
+// shuffle).  Replaces a __shfl_xor butterfly whose ds_bpermute per step went through the LDS unit
+// (the index's block boxes: 6 values x 4 steps per 64 points).  Every lane of the wave active.
+__device__ __forceinline__ float seg_minf(float x, int B) {
+    x = fminf(x, dpp_f<0xB1>(x));
+    x = fminf(x, dpp_f<0x4E>(x));
+    x = fminf(x, dpp_f<0x141>(x));
+    x = fminf(x, dpp_f<0x140>(x));
+    if (B > 16) x = fminf(x, __shfl_xor(x, 16, 64));
+    return x;
+}
+__device__ __forceinline__ float seg_maxf(float x, int B) {
+    x = fmaxf(x, dpp_f<0xB1>(x));
+    x = fmaxf(x, dpp_f<0x4E>(x));
+    x = fmaxf(x, dpp_f<0x141>(x));
+    x = fmaxf(x, dpp_f<0x140>(x));
+    if (B > 16) x = fmaxf(x, __shfl_xor(x, 16, 64));
+    return x;
+}
+
 // Wave-wide integer sum by the same DPP steps (exact in any order).  No lane addresses: the
 // __shfl_xor butterfly's ds_bpermute addresses, shared by the compiler across a kernel's reductions,
 // were kept live — and spilled — from pass A's count to the fused test's (fold_update_kernel).

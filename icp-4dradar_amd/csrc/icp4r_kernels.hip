@@ -229,12 +229,10 @@ __global__ __launch_bounds__(kInitWG) void init_kernel(PairArgs a, WorkArgs w) {
     if (w.tbb) {
         __shared__ float bred[kInitWG / 64][6];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                bl[k] = fminf(bl[k], __shfl_xor(bl[k], off, 64));
-                bh[k] = fmaxf(bh[k], __shfl_xor(bh[k], off, 64));
-            }
+        for (int k = 0; k < 3; ++k) {  // (DPP)
+            bl[k] = wave_minf(bl[k]);
+            bh[k] = wave_maxf(bh[k]);
+        }
         if ((tid & 63) == 0)
             for (int k = 0; k < 3; ++k) {
                 bred[tid >> 6][k] = bl[k];
@@ -473,12 +471,10 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
         mx[0] = fmaxf(mx[0], v.x); mx[1] = fmaxf(mx[1], v.y); mx[2] = fmaxf(mx[2], v.z);
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            mn[k] = fminf(mn[k], __shfl_xor(mn[k], off, 64));
-            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off, 64));
-        }
+    for (int k = 0; k < 3; ++k) {  // (DPP: no ds_bpermute round trips)
+        mn[k] = wave_minf(mn[k]);
+        mx[k] = wave_maxf(mx[k]);
+    }
     if (lane == 0)
         for (int k = 0; k < 3; ++k) {
             sh.red[wave][k] = mn[k];
@@ -908,11 +904,9 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
                             h = v;
                         }
                         ts[pos] = v;
-                        for (int off = 1; off < B; off <<= 1) {
-                            l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
-                            l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
-                            l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
-                        }
+                        l.x = seg_minf(l.x, B); h.x = seg_maxf(h.x, B);
+                        l.y = seg_minf(l.y, B); h.y = seg_maxf(h.y, B);
+                        l.z = seg_minf(l.z, B); h.z = seg_maxf(h.z, B);
                         if ((lane & (B - 1)) == 0) {
                             const int b = pos / B;
                             l.w = 0.f;
@@ -982,12 +976,10 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
         });
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            mn[k] = fminf(mn[k], __shfl_xor(mn[k], off, 64));
-            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off, 64));
-        }
+    for (int k = 0; k < 3; ++k) {  // (DPP: no ds_bpermute round trips)
+        mn[k] = wave_minf(mn[k]);
+        mx[k] = wave_maxf(mx[k]);
+    }
     if (lane == 0)
         for (int k = 0; k < 3; ++k) {
             red[wave][k] = mn[k];
@@ -1499,11 +1491,9 @@ __global__ __launch_bounds__(kIdxWG, 4) void index_refine_kernel(PairArgs a, Wor
         }
         float4 l = real ? v[k] : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
         float4 h = real ? v[k] : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-        for (int off = 1; off < B; off <<= 1) {
-            l.x = fminf(l.x, __shfl_xor(l.x, off, 64)); h.x = fmaxf(h.x, __shfl_xor(h.x, off, 64));
-            l.y = fminf(l.y, __shfl_xor(l.y, off, 64)); h.y = fmaxf(h.y, __shfl_xor(h.y, off, 64));
-            l.z = fminf(l.z, __shfl_xor(l.z, off, 64)); h.z = fmaxf(h.z, __shfl_xor(h.z, off, 64));
-        }
+        l.x = seg_minf(l.x, B); h.x = seg_maxf(h.x, B);
+        l.y = seg_minf(l.y, B); h.y = seg_maxf(h.y, B);
+        l.z = seg_minf(l.z, B); h.z = seg_maxf(h.z, B);
         if ((lane & (B - 1)) == 0 && pos / B < nbc) {
             const int b = pos / B;
             l.w = 0.f;
