@@ -99,6 +99,25 @@ __device__ __forceinline__ float seg_maxf(float x, int B) {
     return x;
 }
 
+// Inclusive wave prefix sum by DPP (Hillis-Steele inside each 16-lane row by row_shr 1, 2, 4, 8 with
+// zero fill, then the row totals carried by row_bcast15 into rows 1, 3 and row_bcast31 into rows
+// 2, 3).  Integer adds: exact, the same values as the __shfl_up ladder it replaces, without its six
+// dependent ds_bpermute round trips through the LDS unit (the kd builds run one per level).  Every
+// lane of the wave active.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_z(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += dpp_z<0x111>(x);       // row_shr:1
+    x += dpp_z<0x112>(x);       // row_shr:2
+    x += dpp_z<0x114>(x);       // row_shr:4
+    x += dpp_z<0x118>(x);       // row_shr:8
+    x += dpp_z<0x142, 0xa>(x);  // row_bcast15 -> rows 1, 3
+    x += dpp_z<0x143, 0xc>(x);  // row_bcast31 -> rows 2, 3
+    return x;
+}
+
 // Wave-wide integer sum by the same DPP steps (exact in any order).  No lane addresses: the
 // __shfl_xor butterfly's ds_bpermute addresses, shared by the compiler across a kernel's reductions,
 // were kept live — and spilled — from pass A's count to the fused test's (fold_update_kernel).

@@ -521,10 +521,7 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             run += hb[gb];
         }
         uint32_t incl = run;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += o;
-        }
+        incl = wave_scan_incl(incl);  // (DPP)
         if (lane == 63) sh.red[wave][0] = __uint_as_float(incl);  // (the bbox partials are consumed)
         __syncthreads();
         uint32_t wbase = 0;
@@ -674,13 +671,9 @@ __device__ void kd_order(KdShared& sh, Get pts, int n, int leaf, uint64_t* tk, u
             }
         }
         const int cnt[3] = {__builtin_popcount(fb[0]), __builtin_popcount(fb[1]), __builtin_popcount(fb[2])};
-        int incl[3] = {cnt[0], cnt[1], cnt[2]};
-        for (int off = 1; off < 64; off <<= 1)
+        int incl[3];
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const int o = __shfl_up(incl[a], off, 64);
-                if (lane >= off) incl[a] += o;
-            }
+        for (int a = 0; a < 3; ++a) incl[a] = (int)wave_scan_incl((uint32_t)cnt[a]);  // (DPP)
         if (lane == 63)
 #pragma unroll
             for (int a = 0; a < 3; ++a) sh.wsum[a][wave] = (uint16_t)incl[a];
@@ -1011,11 +1004,7 @@ __device__ __forceinline__ void index_cloud(IndexShared& shu, const PairArgs& a,
         run += bins[tid * per + k];
     }
     uint32_t incl = run;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-    }
+    incl = wave_scan_incl(incl);  // (DPP)
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     uint32_t wbase = 0;
@@ -1145,11 +1134,7 @@ __global__ __launch_bounds__(kIdxWG) void index_mo_scatter_kernel(PairArgs a, Wo
         run += t;
     }
     uint32_t incl = run;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += o;
-    }
+    incl = wave_scan_incl(incl);  // (DPP)
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     uint32_t tbase = incl - run;
@@ -1304,11 +1289,7 @@ __device__ void src_order_pair(const PairArgs& a, const WorkArgs& w, int p, SoSh
             run += bins[tid * per + k];
         }
         uint32_t incl = run;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += o;
-        }
+        incl = wave_scan_incl(incl);  // (DPP)
         if (lane == 63) wsum[wave] = incl;
         __syncthreads();
         uint32_t base = 0;
@@ -2799,11 +2780,7 @@ __global__ __launch_bounds__(kLdsWG) void nn_lds_kernel(PairArgs a, WorkArgs w, 
             const uint32_t f = tid < nwords ? gneed[tid] : 0u;
             const int c = __builtin_popcount(f);
             int incl = c;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int o = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += o;
-            }
+incl = (int)wave_scan_incl((uint32_t)incl);  // (DPP)
             if (lane == 63) sh.wsum[wave] = incl;
             __syncthreads();
             int base = 0, total = 0;
@@ -3790,11 +3767,7 @@ __device__ __forceinline__ int test_place(const WorkArgs& w, int p, int n, int h
             sum += c[j];
         }
         int incl = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += o;
-        }
+incl = (int)wave_scan_incl((uint32_t)incl);  // (DPP)
         int run = incl - sum;
 #pragma unroll
         for (int j = 0; j < kW; ++j) {
