@@ -1910,7 +1910,9 @@ __device__ __forceinline__ void put_miss(const WorkArgs& w, int p, int k, uint32
                                          float z, float U, uint32_t tpos) {
     const int64_t slot = (int64_t)p * w.x_stride + k;
     w.sq[slot] = make_float4(x, y, z, U);
-    w.sm[slot] = make_uint2((uint32_t)i | (tpos << kNtPosShift), sp);
+    // (one 8-B store: stored as two dwords, the second was merged with the LDS record's into a flat
+    // store that every miss of the fused test paid)
+    *reinterpret_cast<uint64_t*>(&w.sm[slot]) = (uint64_t)((uint32_t)i | (tpos << kNtPosShift)) | ((uint64_t)sp << 32);
 }
 
 // Slot of this lane's record in an append list shared by the workgroup (ctr: an LDS counter): one
@@ -3906,7 +3908,8 @@ __device__ __forceinline__ int pair_cache_test(const PairArgs& a, const WorkArgs
                 atomicOr(&need[sp >> 5], 1u << (sp & 31));
                 if (k < lcap) {
                     lv[k] = make_float4(o.x, o.y, o.z, Lm.y);
-                    lm[k] = make_uint2((uint32_t)i | (nt_tpos(t[e].w) << kNtPosShift), sp);
+                    *reinterpret_cast<uint64_t*>(&lm[k]) =
+                        (uint64_t)((uint32_t)i | (nt_tpos(t[e].w) << kNtPosShift)) | ((uint64_t)sp << 32);
                 } else {
                     put_miss(w, p, k, sp, i, o.x, o.y, o.z, Lm.y, nt_tpos(t[e].w));
                 }
