@@ -2092,6 +2092,9 @@ constexpr int kOrderBuckets = 32;
 constexpr int kPartBits = 10;  // work item = pair << kPartBits | part (parts of >= 64 misses)
 static_assert(kCacheMaxN / 64 <= (1 << kPartBits), "part field");
 
+#ifndef ICP4R_ITEMS_PER_CU
+#define ICP4R_ITEMS_PER_CU 1  // the work list's target items per CU when heavy pairs are cut (round 6: 1 +0.6 % over 2; 3, 4 slower)
+#endif
 struct OrderShared {
     int32_t bcnt[kOrderBuckets], boff[kOrderBuckets];
     unsigned long long tot;
@@ -2136,7 +2139,8 @@ __device__ __forceinline__ void order_items_body(const PairArgs& a, const WorkAr
     // the few slowly converging pairs with thousands of misses spread over several CUs
     // (at least part_size, and large enough that the pass has about 2 items per CU: a part costs a
     // target staging, so only the heavy tail of a light pass is worth cutting)
-    const int ps = (!all && w.part_size > 0) ? max(w.part_size, (int)((tot_s + 2ull * ncu - 1) / (2ull * ncu))) : (1 << 30);
+    constexpr unsigned long long kIpc = ICP4R_ITEMS_PER_CU;
+    const int ps = (!all && w.part_size > 0) ? max(w.part_size, (int)((tot_s + kIpc * ncu - 1) / (kIpc * ncu))) : (1 << 30);
     auto heavy_parts = [&](int c) { return (c + ps - 1) / ps; };
     auto heavy_size = [&](int c, int k) { return min(ps, c - k * ps); };
     for (int p = tid; p < npairs; p += WG) {
